@@ -1,0 +1,262 @@
+"""Benchmark: DOF-updates/s of the SEM Laplacian+convection matvec on MI355X.
+
+One step = one application of the convection-diffusion system operator with
+Dirichlet identity rows -- the LGMRES matvec of ConvectionDiffusion_Solver
+(`_get_dresiduals`, ConvectionDiffusion_Solver.py:104-121):
+
+    y = K T + Pe (u . G_x T + v . G_y T),   y[W/E boundary rows] = T
+
+on a synthetic 64 x 64-element, P = 8 mesh per GPU (BASELINE.json configs[1];
+Pe = 40, T, u, v ~ U(-1, 1) from default_rng(2024)).  N = 263,169 DOFs per
+GPU; inputs resident in HBM before the timed region.  With --gpus N > 1 each
+rank holds one 64-element-column strip of a (64 N) x 64 mesh (weak scaling)
+and every step ends with the interface-line exchange (RCCL all-reduce of the
+shared-edge partial sums).
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N bench.py --gpus N ...
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector / matrix dense peak (datasheet)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--ne", type=int, default=64, help="elements per direction per GPU")
+    ap.add_argument("--P", type=int, default=8)
+    ap.add_argument("--Pe", type=float, default=40.0)
+    ap.add_argument("--graph", type=int, default=1, help="capture steps in hipGraphs (N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--hbm-ne", type=int, default=1024, help="HBM-regime mesh size (0 = skip)")
+    return ap.parse_args()
+
+
+def algorithmic(P, nex, ney):
+    n = P + 1
+    N = (nex * P + 1) * (ney * P + 1)
+    return N, 32.0 * N, 8.0 * n ** 3 * nex * ney   # DOFs, bytes (T,u,v read + y write), flops
+
+
+def make_inputs(mesh, seed=2024):
+    r = np.random.default_rng(seed)
+    N = mesh.n_local
+    return [mesh.to_device(r.uniform(-1, 1, N)) for _ in range(3)]
+
+
+def time_steps(step, steps, warmup, dev, use_graph, dist=None):
+    """Time exactly `steps` steps between barrier + synchronize on both sides."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    replay = None
+    if use_graph:
+        batch = 100
+        while steps % batch:
+            batch //= 2
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(batch):
+                    step()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize(dev)
+        replay = (g, steps // batch)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    if replay:
+        g, reps = replay
+        for _ in range(reps):
+            g.replay()
+    else:
+        for _ in range(steps):
+            step()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    return e0.elapsed_time(e1) / 1e3, wall
+
+
+def isolated_kernel_us(step, dev, n=50):
+    """Median device time of single launches, each bracketed by HIP events on the launch stream."""
+    ts = []
+    for _ in range(n):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        step()
+        b.record()
+        torch.cuda.synchronize(dev)
+        ts.append(a.elapsed_time(b) * 1e3)
+    return float(np.median(ts))
+
+
+def cpu_baseline(P, ne, Pe, seconds):
+    """Oracle (CPU restatement of the reference path): SciPy CSR `Sys @ T` + Dirichlet rows,
+    single core, cfg2.  Sys assembled once as the reference does (SEM.py:186-223)."""
+    from oracle import sem_oracle as O
+    d = 1.0 / ne
+    K = O.global_stiffness_matrix(P, ne, ne, d, d)
+    Gx, Gy = O.global_gradient_matrices(P, ne, ne, d, d)
+    N = K.shape[0]
+    r = np.random.default_rng(2024)
+    T, u, v = r.uniform(-1, 1, N), r.uniform(-1, 1, N), r.uniform(-1, 1, N)
+    Sys = (Pe * (O.conv_left(Gx, u) + O.conv_left(Gy, v)) + K).tocsr()
+    NY = ne * P + 1
+    mask = np.zeros(N, dtype=bool)
+    mask[:NY] = True
+    mask[-NY:] = True
+    try:
+        aff = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {min(aff)})
+    except (AttributeError, OSError):
+        aff = None
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        y = Sys @ T
+        y[mask] = T[mask]
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    if aff is not None:
+        os.sched_setaffinity(0, aff)
+    return {"value": N * reps / el, "unit": "DOF-updates/s", "cores": 1, "kind": "port",
+            "sample": f"cfg2 64x64 P=8 (N={N}): {reps} x (SciPy CSR Sys@T + Dirichlet rows), {el:.1f} s, "
+                      f"1 of {os.cpu_count()} host threads (oracle/sem_oracle.py restatement of "
+                      f"ConvectionDiffusion_Solver.py:85-87,112-119)"}
+
+
+def load_pmc(workload):
+    """HBM traffic per launch measured with rocprofv3 PMC passes (profiles/pmc_traffic.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(workload, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from sem_amd import _lib
+    from sem_amd.device import get_mesh
+    from sem_amd.parallel import StripPartition
+
+    P, ne, Pe = args.P, args.ne, args.Pe
+    nex, ney = ne * world, ne
+    d = 1.0 / ne
+    part = StripPartition(nex, world)
+    eb, ee = part.bounds[rank], part.bounds[rank + 1]
+    mesh = get_mesh(P, nex, ney, d, d, eb, ee, dev.index)
+    T, u, v = make_inputs(mesh, seed=2024 + rank)
+    y = torch.empty_like(T)
+    sides = _lib.SIDE_W | _lib.SIDE_E
+    kw = dict(c_stiff=1.0, c_gradx=Pe, cu=u, c_grady=Pe, cv=v, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides)
+    exch = part.exchanger(mesh, dist) if world > 1 else None
+
+    def step():
+        mesh.apply(T, y, **kw)
+        if exch is not None:
+            exch(y)
+
+    secs, wall = time_steps(step, args.steps, args.warmup, dev, use_graph=(args.graph and world == 1), dist=dist)
+    if dist is not None:
+        t = torch.tensor([secs], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        secs = float(t.item())
+    N_glob = (nex * P + 1) * (ney * P + 1)
+    value = N_glob * args.steps / secs
+    ms = secs / args.steps * 1e3
+
+    # roofline of the dominant kernel (the fused apply) on this rank
+    n_loc = mesh.n_local
+    bytes_launch, flops_launch = 32.0 * n_loc, 8.0 * (P + 1) ** 3 * (ee - eb) * ney
+    apply_only = (lambda: mesh.apply(T, y, **kw))
+    if world == 1:
+        kern_s = secs / args.steps          # timed region / launches (graph-replayed, includes launch gaps)
+    else:
+        k_secs, _ = time_steps(apply_only, 500, 50, dev, use_graph=True)
+        kern_s = k_secs / 500
+    iso_us = isolated_kernel_us(apply_only, dev)
+    achieved = bytes_launch / kern_s / 1e9
+    workload = f"cd_matvec_{ne}x{ne}_P{P}"
+    out = {
+        "metric": "DOF-updates/sec, SEM Laplacian+convection matvec, P=8",
+        "value": value, "unit": "DOF-updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (T,u,v ~ U(-1,1), default_rng(2024+rank); Pe=40; Dirichlet W/E rows)",
+        "config": {"workload": workload, "mesh_per_gpu": f"{ne}x{ne} elements", "P": P,
+                   "global_mesh": f"{nex}x{ney}", "dofs_global": N_glob, "dofs_per_gpu": n_loc,
+                   "partition": f"element-column strips x{world}" + (", RCCL all-reduce of interface lines"
+                                                                       if world > 1 else ""),
+                   "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": bool(args.graph and
+                                                                                         world == 1)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
+                     "kernel": "sem::apply_tp_valu<8>", "bytes_per_launch": bytes_launch,
+                     "flops_per_launch": flops_launch, "kernel_us": kern_s * 1e6, "kernel_us_isolated": iso_us,
+                     "fp64_tflops": flops_launch / kern_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
+    }
+
+    if rank == 0 and world == 1 and args.hbm_ne > 0:
+        # HBM regime: 1024^2 elements, P=8 (N = 67.1 M, 2.15 GB moved per apply > 256 MB MALL)
+        big = get_mesh(P, args.hbm_ne, args.hbm_ne, 1.0 / args.hbm_ne, 1.0 / args.hbm_ne)
+        Tb, ub, vb = (torch.rand(big.n_local, dtype=torch.float64, device=dev) * 2 - 1 for _ in range(3))
+        yb = torch.empty_like(Tb)
+        kwb = dict(kw, cu=ub, cv=vb)
+        sb, _ = time_steps(lambda: big.apply(Tb, yb, **kwb), 20, 3, dev, use_graph=False)
+        kb = sb / 20
+        bb = 32.0 * big.n_local
+        wl = f"cd_matvec_{args.hbm_ne}x{args.hbm_ne}_P{P}"
+        out["roofline_hbm"] = {"workload": wl, "dofs": big.n_local, "value": big.n_local / kb, "unit": "DOF-updates/s",
+                               "bound": "hbm", "achieved": bb / kb / 1e9, "peak": HBM_PEAK_GBS, "unit_bw": "GB/s",
+                               "frac": bb / kb / 1e9 / HBM_PEAK_GBS, "traffic": load_pmc(wl), "kernel_us": kb * 1e6}
+        del Tb, ub, vb, yb
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(P, ne, Pe, args.cpu_seconds)
+        out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

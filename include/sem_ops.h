@@ -1,0 +1,173 @@
+/*
+ * sem_ops.h -- C ABI of the MI355X-native SEM operator layer (libsemops.so).
+ *
+ * Drop-in boundary for the hot path of Tangxiaotian11/SEM: the GLL reference
+ * tables of Solvers/GLL.py and the global operator / assembly API of
+ * Solvers/SEM.py, applied matrix-free on gfx950.  Every entry point names the
+ * reference interface it replaces.  The reference is pure Python, so the
+ * "binding a maintainer would add" is the ctypes layer in sem_amd/_lib.py
+ * (shown in INTEGRATION.md); no torch types cross this boundary.
+ *
+ * Conventions
+ *   - All arithmetic is IEEE fp64.  Vectors are global-DOF vectors in the
+ *     reference's x-major numbering p = (N_ey*P+1)*(m*P+i) + n*P+j
+ *     (SEM.py:97-110), restricted to the handle's local line range.
+ *   - Device pointers are plain device (HBM) pointers; `stream` is a
+ *     hipStream_t passed as void* (NULL = default stream).  Every device call
+ *     is asynchronous and stream-ordered; nothing is allocated or synchronised
+ *     inside an apply, so applies may be captured into a hipGraph.
+ *   - Status codes: 0 = ok, otherwise SEM_E*.  No exceptions cross the ABI;
+ *     sem_last_error() returns a thread-local message for the last failure.
+ *     The Python wrapper maps SEM_EINVAL -> ValueError (the reference raises
+ *     ValueError for bad indices / vector lengths, SEM.py:18-19,108-109,158-159)
+ *     and everything else -> RuntimeError.
+ *   - Handles are immutable after sem_create: concurrent applies on distinct
+ *     streams are safe.
+ */
+#ifndef SEM_OPS_H
+#define SEM_OPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SEM_ABI_VERSION 1
+
+enum sem_status {
+  SEM_OK = 0,
+  SEM_EINVAL = 1,       /* bad argument (maps to ValueError) */
+  SEM_EHIP = 2,         /* HIP runtime error */
+  SEM_ENOMEM = 3,       /* device allocation failed */
+  SEM_EUNSUPPORTED = 4  /* e.g. polynomial order outside the compiled range */
+};
+
+/* Dirichlet side bits (used when no explicit mask is given). */
+enum sem_side { SEM_SIDE_W = 1u, SEM_SIDE_E = 2u, SEM_SIDE_S = 4u, SEM_SIDE_N = 8u };
+
+/* Dirichlet row modes applied after the operator (and after any accumulate). */
+enum sem_dir_mode {
+  SEM_DIR_NONE = 0,     /* plain operator rows                                        */
+  SEM_DIR_IDENTITY = 1, /* y[p] = x[p] - g[p] (g = dir_val, NULL -> 0):
+                           ConvectionDiffusion_Solver.py:90 (res) and :119 (dres)      */
+  SEM_DIR_REPLACE = 2   /* y[p] = dir_val[p]                                            */
+};
+
+enum sem_algo { SEM_ALGO_AUTO = 0, SEM_ALGO_VALU = 1, SEM_ALGO_MFMA = 2 };
+
+typedef struct sem_handle sem_handle;
+
+/* Static description of a handle (all sizes in DOFs / lines). */
+typedef struct sem_info {
+  int P, nex, ney, ex_begin, ex_end, device;
+  double dx, dy;
+  int64_t NX, NY;       /* global node lines in x / nodes per line (N_ex*P+1, N_ey*P+1) */
+  int64_t N;            /* global DOFs = NX*NY  (ConvectionDiffusion_Solver.py:50)       */
+  int64_t line_begin;   /* first global line held locally = ex_begin*P                   */
+  int64_t line_end;     /* last global line held locally  = ex_end*P   (inclusive)       */
+  int64_t n_local;      /* local vector length = (line_end-line_begin+1)*NY              */
+  int64_t dof_begin;    /* global DOF index of local element 0 = line_begin*NY           */
+} sem_info;
+
+/*
+ * Fused operator descriptor.  One launch computes
+ *     z = c_mass*M x + c_stiff*K x + c_gradx*cu.(G_x x) + c_grady*cv.(G_y x)
+ *         + c_extra*(ea.eb + ec.ed) + c_acc*y_in
+ * then applies the Dirichlet rows, and writes y.
+ *   M, K, G_x, G_y : SEM.global_{mass,stiffness,gradient}_matrices (SEM.py:170-223)
+ *   cu.(G_x x)     : Pe * tensordot(C_x, u, (1,0)) @ x  == diag(u) G_x x
+ *                    (SEM.py:226-245 contracted at ConvectionDiffusion_Solver.py:82-83)
+ *   ea.eb          : Jacobian terms Pe*tensordot(C_x, T, (2,0)) @ du == (G_x T).du
+ *                    (ConvectionDiffusion_Solver.py:101-102,114-116)
+ * NULL cu/cv mean "all ones"; an extra pair (ea,eb) or (ec,ed) is skipped when
+ * either of its pointers is NULL.  c_acc != 0 reads y before overwriting it.
+ * x must not alias y.
+ */
+typedef struct sem_apply_desc {
+  double c_mass, c_stiff, c_gradx, c_grady;
+  const double* cu;
+  const double* cv;
+  double c_extra;
+  const double* ea;
+  const double* eb;
+  const double* ec;
+  const double* ed;
+  double c_acc;
+  int dir_mode;              /* enum sem_dir_mode */
+  const uint8_t* dir_mask;   /* nullable: per-DOF mask (np.isclose-derived masks) */
+  const double* dir_val;     /* nullable */
+  unsigned dir_sides;        /* SEM_SIDE_* bits used when dir_mask == NULL */
+  int algo;                  /* enum sem_algo */
+} sem_apply_desc;
+
+/* ---- library ------------------------------------------------------------ */
+int sem_abi_version(void);
+const char* sem_last_error(void);
+/* Largest polynomial order with a compiled device kernel. */
+int sem_max_order(void);
+
+/* ---- GLL reference element (host), Solvers/GLL.py ------------------------ */
+/* GLL.standard_nodes (GLL.py:7-33): xi[P+1], w[P+1], V[(P+1)^2] row-major (V nullable). */
+int sem_gll_nodes(int P, double* xi, double* w, double* V);
+/* GLL.standard_differentiation_matrix (GLL.py:45-59): D[i*(P+1)+j] = l'_j(xi_i). */
+int sem_gll_differentiation(int P, double* D);
+/* GLL.standard_gradient_matrix (GLL.py:62-70): G[i][j] = w_i D_ij. */
+int sem_gll_gradient(int P, double* G);
+/* GLL.standard_stiffness_matrix (GLL.py:73-81): K[i][j] = sum_k w_k D_ki D_kj. */
+int sem_gll_stiffness(int P, double* K);
+/* GLL.standard_evaluation_matrix (GLL.py:105-116): S[q*(P+1)+j] = l_j(xi_eval[q]). */
+int sem_gll_evaluation(int P, const double* xi_eval, int64_t count, double* S);
+
+/* ---- connectivity (host), Solvers/SEM.py ------------------------------- */
+/* SEM.global_index (SEM.py:97-110), vectorised; SEM_EINVAL if any index is out of range. */
+int sem_global_index(int P, int nex, int ney, const int64_t* m, const int64_t* n, const int64_t* i,
+                     const int64_t* j, int64_t count, int64_t* out);
+
+/* ---- handles ------------------------------------------------------------ */
+/* Mesh of nex x ney elements of order P, widths dx, dy; this handle holds the
+ * element columns [ex_begin, ex_end) (ex_begin=0, ex_end=nex for one GPU).
+ * Uploads the reference-element tables to `device`. */
+int sem_create(int P, int nex, int ney, double dx, double dy, int ex_begin, int ex_end, int device,
+               sem_handle** out);
+int sem_destroy(sem_handle* h);
+int sem_get_info(const sem_handle* h, sem_info* out);
+
+/* ---- device operators ------------------------------------------------- */
+/* Fused matrix-free operator apply (see sem_apply_desc).  x, y: n_local doubles. */
+int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y, void* stream);
+
+/* SEM.scatter (SEM.py:149-167): u_e[m][n][i][j] = u[global_index(m,n,i,j)] for the
+ * local elements; u_e has (ex_end-ex_begin)*ney*(P+1)^2 doubles. */
+int sem_gather_elements(sem_handle* h, const double* u, double* u_e, void* stream);
+
+/* SEM.assemble for a 4-D element array (SEM.py:113-127,146): direct-stiffness
+ * summation a[p] = sum over elements holding p of a_e[m][n][i][j], summed in the
+ * reference's (m,n) lexicographic order starting from +0.0 (bit-exact). */
+int sem_dss(sem_handle* h, const double* a_e, double* a, void* stream);
+
+/* SEM.eval_interpolation (SEM.py:248-273) for an ij-meshgrid of plot points:
+ * out[a*nb+b] = sum_kl Sx[a][k] u_e[m_idx[a]][n_idx[b]][k][l] Sy[b][l], where m_idx / Sx are
+ * the element index and Lagrange evaluation row (GLL.standard_evaluation_matrix) of plot
+ * row a (SEM.x2xi, SEM.py:23-36) and n_idx / Sy those of plot column b.  Entries whose
+ * element is not held locally are left untouched.  All pointers are device pointers. */
+int sem_eval_interpolation(sem_handle* h, const double* u_e, int na, const int* m_idx, const double* Sx, int nb,
+                           const int* n_idx, const double* Sy, double* out, void* stream);
+
+/* ---- multi-GPU interface lines (element-strip partition) --------------- */
+/* Pack the local partial sums on the two interface lines into buf[(G-1)*NY]
+ * (slot s = global line (s+1)*... of partition boundary s), zeros elsewhere;
+ * `bounds` = the G+1 element-column boundaries of the partition.  After a sum
+ * all-reduce of buf over all ranks, sem_interface_unpack writes the assembled
+ * values back into y. */
+int sem_interface_pack(sem_handle* h, const double* y, const int* bounds, int G, double* buf,
+                       void* stream);
+int sem_interface_unpack(sem_handle* h, const double* buf, const int* bounds, int G, double* y,
+                         void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SEM_OPS_H */

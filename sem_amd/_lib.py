@@ -1,0 +1,102 @@
+"""ctypes binding of libsemops.so (include/sem_ops.h).
+
+This is the only place Python touches the C ABI.  The library is built in-tree
+(sem_amd/lib/libsemops.so, see sem_amd/build.py) and loaded from there; if it is
+missing or fails to load, every entry point raises -- there is no CPU fallback.
+Status codes are mapped the way the reference reports errors: SEM_EINVAL ->
+ValueError (Solvers/SEM.py:18-19,108-109,158-159), anything else -> RuntimeError.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
+
+SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
+SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
+DIR_NONE, DIR_IDENTITY, DIR_REPLACE = 0, 1, 2
+ALGO_AUTO, ALGO_VALU, ALGO_MFMA = 0, 1, 2
+
+_dp = C.POINTER(C.c_double)
+_i64p = C.POINTER(C.c_int64)
+
+
+class SemInfo(C.Structure):
+    _fields_ = [("P", C.c_int), ("nex", C.c_int), ("ney", C.c_int), ("ex_begin", C.c_int), ("ex_end", C.c_int),
+                ("device", C.c_int), ("dx", C.c_double), ("dy", C.c_double), ("NX", C.c_int64), ("NY", C.c_int64),
+                ("N", C.c_int64), ("line_begin", C.c_int64), ("line_end", C.c_int64), ("n_local", C.c_int64),
+                ("dof_begin", C.c_int64)]
+
+
+class SemApplyDesc(C.Structure):
+    _fields_ = [("c_mass", C.c_double), ("c_stiff", C.c_double), ("c_gradx", C.c_double), ("c_grady", C.c_double),
+                ("cu", C.c_void_p), ("cv", C.c_void_p), ("c_extra", C.c_double), ("ea", C.c_void_p),
+                ("eb", C.c_void_p), ("ec", C.c_void_p), ("ed", C.c_void_p), ("c_acc", C.c_double),
+                ("dir_mode", C.c_int), ("dir_mask", C.c_void_p), ("dir_val", C.c_void_p), ("dir_sides", C.c_uint),
+                ("algo", C.c_int)]
+
+
+# name -> (restype, argtypes); mirrors include/sem_ops.h one-for-one
+_SIGS = {
+    "sem_abi_version": (C.c_int, []),
+    "sem_last_error": (C.c_char_p, []),
+    "sem_max_order": (C.c_int, []),
+    "sem_gll_nodes": (C.c_int, [C.c_int, _dp, _dp, _dp]),
+    "sem_gll_differentiation": (C.c_int, [C.c_int, _dp]),
+    "sem_gll_gradient": (C.c_int, [C.c_int, _dp]),
+    "sem_gll_stiffness": (C.c_int, [C.c_int, _dp]),
+    "sem_gll_evaluation": (C.c_int, [C.c_int, _dp, C.c_int64, _dp]),
+    "sem_global_index": (C.c_int, [C.c_int, C.c_int, C.c_int, _i64p, _i64p, _i64p, _i64p, C.c_int64, _i64p]),
+    "sem_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, C.c_int, C.c_int,
+                             C.POINTER(C.c_void_p)]),
+    "sem_destroy": (C.c_int, [C.c_void_p]),
+    "sem_get_info": (C.c_int, [C.c_void_p, C.POINTER(SemInfo)]),
+    "sem_apply": (C.c_int, [C.c_void_p, C.POINTER(SemApplyDesc), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sem_gather_elements": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sem_dss": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sem_eval_interpolation": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sem_interface_pack": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int), C.c_int, C.c_void_p, C.c_void_p]),
+    "sem_interface_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int), C.c_int, C.c_void_p,
+                                       C.c_void_p]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libsemops.so (building it first if sources are newer).  Raises if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # Build only when the library is absent (or SEM_AUTOBUILD=1 asks for a staleness check):
+    # snapshot copies reset mtimes, and concurrent ranks must not race a rebuild.
+    if not os.path.exists(LIB_PATH) or os.environ.get("SEM_AUTOBUILD", "0") == "1":
+        try:
+            from . import build as _build
+            _build.build()
+        except Exception as e:  # noqa: BLE001 - surface the real reason below
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"libsemops.so is missing and could not be built: {e}") from e
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.sem_abi_version() != 1:
+        raise RuntimeError("libsemops ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(status):
+    if status == SEM_OK:
+        return
+    msg = load().sem_last_error().decode(errors="replace")
+    if status == SEM_EINVAL:
+        raise ValueError(msg)
+    raise RuntimeError(f"libsemops error {status}: {msg}")
+
+
+def exported_symbols():
+    return list(_SIGS)

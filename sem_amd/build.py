@@ -1,0 +1,53 @@
+"""Build libsemops.so (HIP kernels for gfx950 + C ABI) in-tree.
+
+The shared library lands in sem_amd/lib/ so it travels with the repository
+snapshot to the GPU box; no JIT cache, no site-packages install.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libsemops.so")
+ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["sem_ops.hip", "gll_tables.cpp"]
+HEADERS = ["sem_internal.h", os.path.join("..", "..", "include", "sem_ops.h")]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the SEM operator layer needs ROCm's hipcc to build")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
+           "-I", os.path.join(ROOT, "include"), "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
+    print(LIB)

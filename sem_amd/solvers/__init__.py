@@ -1,0 +1,5 @@
+"""Solver counterparts (callers of the operator layer): the operator applies of
+Solvers/ConvectionDiffusion_Solver.py and Solvers/NavierStokes_Solver.py on the GPU."""
+from .convection_diffusion import ConvectionDiffusionSolver  # noqa: F401
+
+__all__ = ["ConvectionDiffusionSolver"]

@@ -1,0 +1,186 @@
+"""Convection-diffusion solver counterpart on the device operators.
+
+Mirrors Solvers/ConvectionDiffusion_Solver.py:9-203 (same constructor, same
+private methods the OpenMDAO component calls, same error behaviour), with the
+operator applies on the GPU:
+
+  * `_get_residuals`  (:73-92)   -> ONE fused launch: Sys T with Dirichlet rows
+                                    res = T - T_dir (SEM_DIR_IDENTITY + dir_val)
+  * `_calc_jacobians` (:94-102)  -> Pe*G_x T, Pe*G_y T once per linearisation
+  * `_get_dresiduals` (:104-121) -> ONE fused launch: Sys dT + (Pe G_x T).du
+                                    + (Pe G_y T).dv with Dirichlet rows dres = dT
+
+Vectors may be NumPy arrays (returned as NumPy, like the reference) or float64
+device tensors (kept on the device).  The Dirichlet mask is built exactly as the
+reference builds it (np.isclose on the node coordinates, :62-71); when it is the
+plain boundary-line set the kernel derives it from geometry (no mask traffic).
+`_get_update` keeps the reference's LGMRES (SciPy, host Arnoldi) around device
+matvecs; a device-resident Krylov solver is the next step.
+"""
+import typing
+
+import numpy as np
+import scipy.sparse.linalg as linalg
+import torch
+
+from .. import SEM, _lib
+from ..device import get_mesh
+
+
+def side_mask(points, L_x, L_y, sides):
+    """Boundary-line mask for side bits, from the same np.isclose tests as the reference."""
+    m = np.zeros(points.shape[1], dtype=bool)
+    if sides & _lib.SIDE_W:
+        m |= np.isclose(points[0], 0)
+    if sides & _lib.SIDE_E:
+        m |= np.isclose(points[0], L_x)
+    if sides & _lib.SIDE_S:
+        m |= np.isclose(points[1], 0)
+    if sides & _lib.SIDE_N:
+        m |= np.isclose(points[1], L_y)
+    return m
+
+
+def geometric_mask(NX, NY, sides):
+    gx, gy = np.divmod(np.arange(NX * NY), NY)
+    m = np.zeros(NX * NY, dtype=bool)
+    if sides & _lib.SIDE_W:
+        m |= gx == 0
+    if sides & _lib.SIDE_E:
+        m |= gx == NX - 1
+    if sides & _lib.SIDE_S:
+        m |= gy == 0
+    if sides & _lib.SIDE_N:
+        m |= gy == NY - 1
+    return m
+
+
+class DirichletRows:
+    """Device form of a reference Dirichlet mask: side bits when the np.isclose mask is exactly
+    the boundary lines (the usual case), an explicit uint8 mask otherwise."""
+
+    def __init__(self, mesh, mask, sides):
+        self.mask_np = np.asarray(mask, dtype=bool)
+        if np.array_equal(self.mask_np, geometric_mask(mesh.NX, mesh.NY, sides)):
+            self.sides, self.mask = sides, None
+        else:
+            self.sides = 0
+            self.mask = torch.as_tensor(self.mask_np.astype(np.uint8), device=mesh.device)
+
+    def kw(self):
+        return dict(dir_sides=self.sides, dir_mask=self.mask)
+
+
+class ConvectionDiffusionSolver:
+    def __init__(self, L_x: float, L_y: float, Pe: float, P: int, N_ex: int, N_ey: int,
+                 T_W: float = None, T_E: float = None, T_S: float = None, T_N: float = None,
+                 mtol=1e-7, iprint: list = []):  # noqa: B006 - reference signature
+        self._iprint = iprint
+        self._Pe = Pe
+        self._mtol = mtol
+        self._L_x, self._L_y = L_x, L_y
+        self._P, self._N_ex, self._N_ey = P, N_ex, N_ey
+        dx, dy = L_x / N_ex, L_y / N_ey
+        self.points = SEM.global_nodes(P, N_ex, N_ey, L_x / N_ex, L_y / N_ey)
+        self.points_e = SEM.element_nodes(P, N_ex, N_ey, dx, dy)
+        self.N = (N_ex * P + 1) * (N_ey * P + 1)
+        self._mesh = get_mesh(P, N_ex, N_ey, dx, dy)
+
+        # global operators (matrix-free)
+        self._M = SEM.global_mass_matrix(P, N_ex, N_ey, dx, dy)
+        self._K = SEM.global_stiffness_matrix(P, N_ex, N_ey, dx, dy)
+        self._C_x, self._C_y = SEM.global_convection_matrices(P, N_ex, N_ey, dx, dy)
+        self._Sys = None
+        self._Jac_T_u = None
+        self._Jac_T_v = None
+
+        # Dirichlet values and mask (ConvectionDiffusion_Solver.py:62-71)
+        self._dirichlet = np.full(self.N, np.nan)
+        sides = 0
+        for val, coord, target, bit in ((T_W, 0, 0, _lib.SIDE_W), (T_E, 0, L_x, _lib.SIDE_E),
+                                        (T_S, 1, 0, _lib.SIDE_S), (T_N, 1, L_y, _lib.SIDE_N)):
+            if val is not None:
+                self._dirichlet[np.isclose(self.points[coord], target)] = val
+                sides |= bit
+        self._mask_dir = ~np.isnan(self._dirichlet)
+        self._dir = DirichletRows(self._mesh, self._mask_dir, sides)
+        self._dir_val = self._mesh.to_device(np.where(self._mask_dir, self._dirichlet, 0.0))
+
+    # ------------------------------------------------------------------ helpers
+    def _dev(self, a):
+        return None if a is None else self._mesh.to_device(a)
+
+    @staticmethod
+    def _out(y, like):
+        return y if isinstance(like, torch.Tensor) else y.cpu().numpy()
+
+    # ------------------------------------------------------------------ reference methods
+    def _get_residuals(self, T, u, v):
+        """res = Sys T, Dirichlet rows T - T_dir (ConvectionDiffusion_Solver.py:73-92)."""
+        Conv = self._Pe * (SEM.tensordot(self._C_x, u, (1, 0)) + SEM.tensordot(self._C_y, v, (1, 0)))
+        self._Sys = Conv + self._K
+        y = self._Sys.apply(self._dev(T), dir_mode=_lib.DIR_IDENTITY, dir_val=self._dir_val, **self._dir.kw())
+        return self._out(y, T)
+
+    def _calc_jacobians(self, T):
+        """Pe diag(G_x T), Pe diag(G_y T) (ConvectionDiffusion_Solver.py:94-102)."""
+        self._Jac_T_u = self._Pe * SEM.tensordot(self._C_x, T, (2, 0))
+        self._Jac_T_v = self._Pe * SEM.tensordot(self._C_y, T, (2, 0))
+
+    def _get_dresiduals(self, dT, du=None, dv=None):
+        """dres = Sys dT + J_u du + J_v dv, Dirichlet rows dT (ConvectionDiffusion_Solver.py:104-121)."""
+        kw = {}
+        if du is not None or dv is not None:
+            ju = self._Jac_T_u._coeffs()[4] if du is not None else None
+            jv = self._Jac_T_v._coeffs()[4] if dv is not None else None
+            kw = dict(c_extra=1.0, ea=ju, eb=self._dev(du), ec=jv, ed=self._dev(dv))
+        cX, cu, cY, cv, d = self._Sys._coeffs()
+        y = self._mesh.apply(self._dev(dT), c_stiff=self._Sys.cK, c_mass=self._Sys.cM, c_gradx=cX, cu=cu,
+                             c_grady=cY, cv=cv, dir_mode=_lib.DIR_IDENTITY, **self._dir.kw(), **kw)
+        return self._out(y, dT)
+
+    def _get_update(self, dres, dT0=None):
+        """LGMRES on the device matvec (ConvectionDiffusion_Solver.py:123-156)."""
+
+        def lhs_mv(dT):
+            lhs_mv.fCount += 1
+            return self._get_dresiduals(np.ascontiguousarray(dT, dtype=np.float64).ravel())
+
+        lhs_mv.fCount = 0
+        lhs_LO = linalg.LinearOperator((self.N,) * 2, lhs_mv, dtype=float)
+        dres = np.asarray(dres.cpu().numpy() if isinstance(dres, torch.Tensor) else dres)
+
+        def print_res(xk):
+            print_res.iterCount += 1
+            if "LGMRES_iter" in self._iprint:
+                print(f"ConvectionDiffusion LGMRES: {print_res.iterCount}\t{np.linalg.norm(lhs_LO.matvec(xk) - dres)}")
+
+        print_res.iterCount = 0
+        dT, info = linalg.lgmres(A=lhs_LO, b=dres, M=None, x0=dT0, atol=self._mtol * np.sqrt(self.N), rtol=0,
+                                 inner_m=int(self.N * 0.3), callback=print_res)
+        if info != 0:
+            raise RuntimeError(f"ConvectionDiffusion LGMRES: Failed to converge in {info} iterations")
+        if "LGMRES_suc" in self._iprint:
+            res = np.linalg.norm(lhs_LO.matvec(dT) - dres, ord=np.inf)
+            print(f"ConvectionDiffusion LGMRES: Converged in {lhs_mv.fCount} evaluations with max-norm {res}")
+        return dT
+
+    def _get_solution(self, u, v, T0=None):
+        """Single Newton step (ConvectionDiffusion_Solver.py:158-170)."""
+        T = T0 if T0 is not None else np.zeros(self.N)
+        res = self._get_residuals(T, u, v)
+        dT = self._get_update(-res)
+        return T + dT
+
+    def _get_vector(self, f_func: typing.Callable[[np.ndarray, np.ndarray], np.ndarray]) -> np.ndarray:
+        return f_func(self.points[0], self.points[1])
+
+    def _get_interpol(self, f, points_plot):
+        f_e = SEM.scatter(f, self._P, self._N_ex, self._N_ey)
+        return SEM.eval_interpolation(f_e, self.points_e, points_plot)
+
+    def run(self, u_func, v_func, points_plot):
+        u = self._get_vector(u_func)
+        v = self._get_vector(v_func)
+        T = self._get_solution(u, v)
+        return self._get_interpol(T, points_plot)

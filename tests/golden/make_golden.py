@@ -1,0 +1,270 @@
+"""Generate golden vectors for the SEM operator layer from the reference itself.
+
+Runs ONLY in the build container, where the read-only reference lives at
+/root/reference.  It imports the reference's own `Solvers/GLL.py`, `Solvers/SEM.py`
+and the two solver classes, runs them on small seeded cases and writes the
+inputs/outputs as .npz fixtures next to this script.  No reference source is
+copied; only numbers are written.
+
+Two in-process adapters are needed because this container lacks two pinned
+dependencies of the reference (`requirements.txt:1-4`):
+
+* pydata `sparse` 0.12 (absent).  `SEM.py:8` imports it and `SEM.assemble`
+  (`SEM.py:139-145`) builds `sparse.COO(coords, data, shape)` for the 8-D
+  convection tensors.  The stub below is a plain holder for the (coords, data,
+  shape) triplet the reference builds; `tensordot(C, x, (ax, 0))` is restated as
+  "sum data * x[coords[ax]] over duplicate remaining coordinates", which is the
+  published semantics of pydata-sparse tensordot with a dense vector, followed
+  by `.tocsr()` through SciPy's COO->CSR (which sums duplicates).
+* SciPy 1.15 removed `lgmres(tol=...)`; the solvers call it with `tol=0`
+  (`ConvectionDiffusion_Solver.py:146-148`, `NavierStokes_Solver.py:222-224`).
+  The shim forwards `tol` as `rtol` (same meaning in SciPy <1.12).
+
+Usage:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------- adapters
+class _COO:
+    """Holder for the (coords, data, shape) triplet `SEM.assemble` builds (SEM.py:145)."""
+
+    def __init__(self, coords, data, shape):
+        self.coords = np.asarray(coords).astype(np.int64)
+        self.data = np.asarray(data, dtype=np.float64)
+        self.shape = tuple(shape)
+
+    def tocsr(self):
+        assert len(self.shape) == 2
+        return sp.coo_matrix((self.data, (self.coords[0], self.coords[1])), shape=self.shape).tocsr()
+
+    def __mul__(self, s):
+        return _COO(self.coords, self.data * s, self.shape)
+
+    __rmul__ = __mul__
+
+    def __add__(self, other):
+        return _COO(np.hstack([self.coords, other.coords]), np.hstack([self.data, other.data]), self.shape)
+
+
+def _tensordot(a, x, axes, return_type=None):
+    ax, bx = axes
+    assert bx == 0 and np.ndim(x) == 1
+    keep = [d for d in range(len(a.shape)) if d != ax]
+    data = a.data * np.asarray(x)[a.coords[ax]]
+    return _COO(a.coords[keep], data, tuple(a.shape[d] for d in keep))
+
+
+def install_adapters():
+    stub = types.ModuleType("sparse")
+    stub.COO = _COO
+    stub.tensordot = _tensordot
+    sys.modules["sparse"] = stub
+    orig = spla.lgmres
+
+    def lgmres(*args, tol=None, **kw):
+        if tol is not None:
+            kw["rtol"] = tol
+        return orig(*args, **kw)
+
+    spla.lgmres = lgmres
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+
+
+def csr_parts(A, prefix):
+    A = A.tocsr()
+    return {prefix + "_indptr": A.indptr.astype(np.int64), prefix + "_indices": A.indices.astype(np.int64),
+            prefix + "_data": A.data.astype(np.float64)}
+
+
+def rng_fields(N, seed=2024):
+    r = np.random.default_rng(seed)
+    T = r.uniform(-1, 1, N)
+    u = r.uniform(-1, 1, N)
+    v = r.uniform(-1, 1, N)
+    return T, u, v
+
+
+# --------------------------------------------------------------------------- fixtures
+def gen_gll(GLL):
+    d = {}
+    for P in range(1, 17):
+        x, w, V = GLL.standard_nodes(P)
+        d[f"P{P}_x"], d[f"P{P}_w"], d[f"P{P}_V"] = x, w, V
+        d[f"P{P}_M"] = GLL.standard_mass_matrix(P)
+        d[f"P{P}_D"] = GLL.standard_differentiation_matrix(P)
+        d[f"P{P}_G"] = GLL.standard_gradient_matrix(P)
+        d[f"P{P}_K"] = GLL.standard_stiffness_matrix(P)
+        if P <= 8:
+            d[f"P{P}_F"] = GLL.standard_product_matrix(P)
+            d[f"P{P}_C"] = GLL.standard_convection_matrix(P)
+        xi = np.linspace(-1, 1, 7)
+        d[f"P{P}_S"] = GLL.standard_evaluation_matrix(P, xi)
+    np.savez_compressed(os.path.join(OUT, "gll.npz"), **d)
+
+
+MESHES = [(4, 4, 4, 1.0, 1.0), (4, 3, 2, 2.0, 1.0), (8, 8, 8, 1.0, 1.0), (12, 5, 3, 1.0, 1.0)]
+
+
+def gen_mesh(SEM):
+    d = {}
+    for (P, nex, ney, Lx, Ly) in MESHES:
+        key = f"P{P}_{nex}x{ney}"
+        dx, dy = Lx / nex, Ly / ney
+        m, n, i, j = np.meshgrid(np.arange(nex), np.arange(ney), np.arange(P + 1), np.arange(P + 1), indexing="ij")
+        d[key + "_gidx"] = np.asarray(SEM.global_index(P, nex, ney, m, n, i, j), dtype=np.int64)
+        d[key + "_points"] = SEM.global_nodes(P, nex, ney, dx, dy)
+        d[key + "_points_e"] = SEM.element_nodes(P, nex, ney, dx, dy)
+        d[key + "_dxdy"] = np.array([dx, dy])
+        N = (nex * P + 1) * (ney * P + 1)
+        r = np.random.default_rng(7)
+        u = r.uniform(-1, 1, N)
+        d[key + "_scatter_in"] = u
+        d[key + "_scatter_out"] = SEM.scatter(u, P, nex, ney)
+        a_e = r.uniform(-1, 1, (nex, ney, P + 1, P + 1))
+        d[key + "_assemble4_in"] = a_e
+        d[key + "_assemble4_out"] = SEM.assemble(a_e)
+    np.savez_compressed(os.path.join(OUT, "mesh.npz"), **d)
+
+
+def gen_matrices(SEM):
+    d = {}
+    for (P, nex, ney, Lx, Ly) in [(4, 4, 4, 1.0, 1.0), (4, 3, 2, 2.0, 1.0), (8, 8, 8, 1.0, 1.0)]:
+        key = f"P{P}_{nex}x{ney}"
+        dx, dy = Lx / nex, Ly / ney
+        M = SEM.global_mass_matrix(P, nex, ney, dx, dy)
+        K = SEM.global_stiffness_matrix(P, nex, ney, dx, dy)
+        Gx, Gy = SEM.global_gradient_matrices(P, nex, ney, dx, dy)
+        d.update(csr_parts(M, key + "_M"))
+        d.update(csr_parts(K, key + "_K"))
+        d.update(csr_parts(Gx, key + "_Gx"))
+        d.update(csr_parts(Gy, key + "_Gy"))
+        N = K.shape[0]
+        T, u, v = rng_fields(N)
+        d[key + "_T"], d[key + "_u"], d[key + "_v"] = T, u, v
+        d[key + "_KT"] = K @ T
+        d[key + "_MT"] = M @ T
+        d[key + "_GxT"] = Gx @ T
+        d[key + "_GyT"] = Gy @ T
+        if nex * ney <= 16:
+            Cx, Cy = SEM.global_convection_matrices(P, nex, ney, dx, dy)
+            uCx = _tensordot(Cx, u, (1, 0)).tocsr()
+            vCy = _tensordot(Cy, v, (1, 0)).tocsr()
+            CxT = _tensordot(Cx, T, (2, 0)).tocsr()
+            CyT = _tensordot(Cy, T, (2, 0)).tocsr()
+            d.update(csr_parts(uCx, key + "_uCx"))
+            d.update(csr_parts(vCy, key + "_vCy"))
+            d.update(csr_parts(CxT, key + "_CxT"))
+            d.update(csr_parts(CyT, key + "_CyT"))
+            Sys = 40.0 * (uCx + vCy) + K
+            d[key + "_SysT_Pe40"] = Sys @ T
+    np.savez_compressed(os.path.join(OUT, "matrices.npz"), **d)
+
+
+def gen_cd(CDS):
+    d = {}
+    # residual / differential residual through the reference solver class
+    for (P, nex, ney, Lx, Ly, bc) in [(4, 4, 4, 1.0, 1.0, dict(T_W=0.5, T_E=-0.5)),
+                                      (4, 3, 2, 2.0, 1.0, dict(T_W=0.5, T_E=-0.5, T_S=0.25, T_N=1.0)),
+                                      (8, 8, 8, 1.0, 1.0, dict(T_W=0.5, T_E=-0.5))]:
+        key = f"P{P}_{nex}x{ney}"
+        cd = CDS(Lx, Ly, 40.0, P, nex, ney, **bc)
+        T, u, v = rng_fields(cd.N)
+        res = cd._get_residuals(T, u, v)
+        cd._calc_jacobians(T)
+        r = np.random.default_rng(11)
+        dT, du, dv = r.uniform(-1, 1, cd.N), r.uniform(-1, 1, cd.N), r.uniform(-1, 1, cd.N)
+        dres = cd._get_dresiduals(dT)
+        dres_full = cd._get_dresiduals(dT, du, dv)
+        d[key + "_bc"] = np.array([bc.get(s, np.nan) for s in ("T_W", "T_E", "T_S", "T_N")])
+        d[key + "_LxLy"] = np.array([Lx, Ly])
+        d[key + "_T"], d[key + "_u"], d[key + "_v"] = T, u, v
+        d[key + "_dT"], d[key + "_du"], d[key + "_dv"] = dT, du, dv
+        d[key + "_mask_dir"] = cd._mask_dir
+        d[key + "_dirichlet"] = cd._dirichlet
+        d[key + "_res"] = res
+        d[key + "_dres"] = dres
+        d[key + "_dres_full"] = dres_full
+    # cfg1: Examples/ConvectionDiffusion_Example.py physics on 4x4, P=4
+    cd = CDS(1.0, 1.0, 40.0, 4, 4, 4, T_E=-0.5, T_W=0.5)
+    u = cd._get_vector(lambda x, y: y - 0.5)
+    v = cd._get_vector(lambda x, y: 0.5 - x)
+    Tsol = cd._get_solution(u, v)
+    d["cfg1_T"] = Tsol
+    d["cfg1_res_after"] = cd._get_residuals(Tsol, u, v)
+    xp, yp = np.meshgrid(np.linspace(0, 1, 11), np.linspace(0, 1, 11), indexing="ij")
+    d["cfg1_plot_x"], d["cfg1_plot_y"] = xp, yp
+    d["cfg1_T_plot"] = cd._get_interpol(Tsol, (xp, yp))
+    np.savez_compressed(os.path.join(OUT, "cd.npz"), **d)
+
+
+def gen_ns(NSS):
+    d = {}
+    P, nex, ney = 4, 4, 4
+    ns = NSS(1.0, 1.0, 100.0, 50.0, P, nex, ney, u_N=1.0, iprint=[])
+    r = np.random.default_rng(5)
+    u, v, p, T = (r.uniform(-1, 1, ns.N) for _ in range(4))
+    ru, rv, rc = ns._get_residuals(u, v, p, T)
+    ns._calc_jacobians(u, v)
+    du, dv, dp, dT = (r.uniform(-1, 1, ns.N) for _ in range(4))
+    dru, drv, drc = ns._get_dresiduals(du, dv, dp, dT)
+    for k, a in dict(u=u, v=v, p=p, T=T, du=du, dv=dv, dp=dp, dT=dT, ru=ru, rv=rv, rc=rc,
+                     dru=dru, drv=drv, drc=drc, mask_bound=ns._mask_bound, mask_dir_p=ns._mask_dir_p,
+                     dir_u=ns._dirichlet_u, dir_v=ns._dirichlet_v).items():
+        d["P4_4x4_" + k] = a
+    # one lid-driven solve (Re=100) on the same mesh
+    ns2 = NSS(1.0, 1.0, 100.0, 0.0, P, nex, ney, u_N=1.0, iprint=[])
+    us, vs, ps = ns2._get_solution(np.zeros(ns2.N))
+    d["lid_u"], d["lid_v"], d["lid_p"], d["lid_newton_iters"] = us, vs, ps, np.array(ns2._k)
+    np.savez_compressed(os.path.join(OUT, "ns.npz"), **d)
+
+
+def gen_checksums(SEM):
+    """Full-size cfg2 (64x64, P=8) checksums: arrays are too big to commit."""
+    d = {}
+    P, ne = 8, 64
+    dx = dy = 1.0 / ne
+    K = SEM.global_stiffness_matrix(P, ne, ne, dx, dy)
+    M = SEM.global_mass_matrix(P, ne, ne, dx, dy)
+    Gx, Gy = SEM.global_gradient_matrices(P, ne, ne, dx, dy)
+    N = K.shape[0]
+    T, u, v = rng_fields(N)
+    KT = K @ T
+    GxT, GyT = Gx @ T, Gy @ T
+    SysT = KT + 40.0 * (u * GxT + v * GyT)
+    d["N"] = np.array(N)
+    d["nnz_K"], d["nnz_Gx"], d["nnz_M"] = np.array(K.nnz), np.array(Gx.nnz), np.array(M.nnz)
+    d["norm_KT"], d["norm_SysT"] = np.array(np.linalg.norm(KT)), np.array(np.linalg.norm(SysT))
+    d["sample_idx"] = np.arange(0, N, 97)
+    d["sample_KT"], d["sample_SysT"], d["sample_MT"] = KT[::97], SysT[::97], (M @ T)[::97]
+    np.savez_compressed(os.path.join(OUT, "cfg2_checksums.npz"), **d)
+
+
+def main():
+    install_adapters()
+    from Solvers import GLL, SEM
+    from Solvers.ConvectionDiffusion_Solver import ConvectionDiffusionSolver
+    from Solvers.NavierStokes_Solver import NavierStokesSolver
+    gen_gll(GLL)
+    gen_mesh(SEM)
+    gen_matrices(SEM)
+    gen_cd(ConvectionDiffusionSolver)
+    gen_ns(NavierStokesSolver)
+    gen_checksums(SEM)
+    for f in sorted(os.listdir(OUT)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,208 @@
+"""GPU parity of the fused operator kernel (libsemops via the C ABI) against the
+reference's golden vectors and the pinned oracle.
+
+Tolerance: operator applies max|y - y_ref| <= 1e-13 * max|y_ref|
+(fp64, different association order than SciPy's CSR SpMV); connectivity, gathers
+and the direct-stiffness sum are bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import sem_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-13
+
+
+def rel(a, b):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+GOLDEN_MESHES = {"P4_4x4": (4, 4, 4, 1.0, 1.0), "P4_3x2": (4, 3, 2, 2.0, 1.0), "P8_8x8": (8, 8, 8, 1.0, 1.0)}
+
+
+@pytest.mark.parametrize("key", list(GOLDEN_MESHES))
+def test_operators_vs_reference_golden(gpu, key):
+    from sem_amd import SEM
+    P, nex, ney, Lx, Ly = GOLDEN_MESHES[key]
+    g = golden("matrices.npz")
+    dx, dy = Lx / nex, Ly / ney
+    T = g[key + "_T"]
+    M = SEM.global_mass_matrix(P, nex, ney, dx, dy)
+    K = SEM.global_stiffness_matrix(P, nex, ney, dx, dy)
+    Gx, Gy = SEM.global_gradient_matrices(P, nex, ney, dx, dy)
+    assert rel(M @ T, g[key + "_MT"]) < TOL
+    assert rel(K @ T, g[key + "_KT"]) < TOL
+    assert rel(Gx @ T, g[key + "_GxT"]) < TOL
+    assert rel(Gy @ T, g[key + "_GyT"]) < TOL
+    if key + "_SysT_Pe40" in g:
+        Cx, Cy = SEM.global_convection_matrices(P, nex, ney, dx, dy)
+        u, v = g[key + "_u"], g[key + "_v"]
+        Sys = 40.0 * (SEM.tensordot(Cx, u, (1, 0)) + SEM.tensordot(Cy, v, (1, 0))) + K
+        assert rel(Sys @ T, g[key + "_SysT_Pe40"]) < TOL
+        # right contraction diag(G_x T) against the reference's own tensor
+        import scipy.sparse as sp
+        R = sp.csr_matrix((g[key + "_CxT_data"], g[key + "_CxT_indices"], g[key + "_CxT_indptr"]))
+        J = SEM.tensordot(Cx, T, (2, 0))
+        w = np.random.default_rng(3).uniform(-1, 1, T.size)
+        assert rel(J @ w, R @ w) < TOL
+
+
+def test_tocsr_matches_reference_pattern(gpu):
+    from sem_amd import SEM
+    g = golden("matrices.npz")
+    for key, (P, nex, ney, Lx, Ly) in GOLDEN_MESHES.items():
+        dx, dy = Lx / nex, Ly / ney
+        ops = {"M": SEM.global_mass_matrix(P, nex, ney, dx, dy), "K": SEM.global_stiffness_matrix(P, nex, ney, dx, dy)}
+        ops["Gx"], ops["Gy"] = SEM.global_gradient_matrices(P, nex, ney, dx, dy)
+        for nm, op in ops.items():
+            A = op.tocsr()
+            assert np.array_equal(A.indptr, g[f"{key}_{nm}_indptr"]), (key, nm)
+            assert np.array_equal(A.indices, g[f"{key}_{nm}_indices"]), (key, nm)
+            assert rel(A.data, g[f"{key}_{nm}_data"]) < 1e-14
+            assert rel(op.diagonal(), A.diagonal()) < 1e-14
+
+
+CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4, 2), (8, 8, 8), (8, 1, 13),
+         (8, 17, 5), (9, 3, 4), (10, 2, 2), (11, 3, 1), (12, 5, 3), (13, 2, 3), (14, 1, 2), (15, 2, 2), (16, 3, 2)]
+
+
+@pytest.mark.parametrize("P,nex,ney", CASES)
+def test_fused_apply_vs_oracle(gpu, P, nex, ney):
+    from sem_amd.device import get_mesh
+    Lx, Ly = 1.3, 0.7
+    dx, dy = Lx / nex, Ly / ney
+    mesh = get_mesh(P, nex, ney, dx, dy)
+    N = mesh.n_local
+    r = np.random.default_rng(P * 1000 + nex * 10 + ney)
+    x, u, v, a, b = (r.uniform(-1, 1, N) for _ in range(5))
+    X, U, V, A, B = (mesh.to_device(t) for t in (x, u, v, a, b))
+    ref = {k: O.apply_matrix_free(P, nex, ney, dx, dy, x, **kw) for k, kw in
+           {"M": dict(c_mass=1.0), "K": dict(c_stiff=1.0), "Gx": dict(c_gradx=1.0), "Gy": dict(c_grady=1.0)}.items()}
+    assert rel(mesh.apply(X, c_mass=1.0), ref["M"]) < TOL
+    assert rel(mesh.apply(X, c_stiff=1.0), ref["K"]) < TOL
+    assert rel(mesh.apply(X, c_gradx=1.0), ref["Gx"]) < TOL
+    assert rel(mesh.apply(X, c_grady=1.0), ref["Gy"]) < TOL
+    # everything at once: 0.5 M + K + 40 u.Gx + 40 v.Gy + 3 (a.b + u.v) + 2 y_in
+    yin = r.uniform(-1, 1, N)
+    Y = mesh.to_device(yin)
+    mesh.apply(X, Y, c_mass=0.5, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, c_extra=3.0, ea=A, eb=B,
+               ec=U, ed=V, c_acc=2.0)
+    want = 0.5 * ref["M"] + ref["K"] + 40 * u * ref["Gx"] + 40 * v * ref["Gy"] + 3 * (a * b + u * v) + 2 * yin
+    assert rel(Y, want) < TOL
+
+
+@pytest.mark.parametrize("P,nex,ney", [(4, 4, 4), (8, 6, 5), (12, 3, 4)])
+def test_dirichlet_rows(gpu, P, nex, ney):
+    from sem_amd import _lib
+    from sem_amd.device import get_mesh
+    mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.0 / ney)
+    N, NX, NY = mesh.n_local, mesh.NX, mesh.NY
+    r = np.random.default_rng(1)
+    x, g = r.uniform(-1, 1, N), r.uniform(-1, 1, N)
+    X, G = mesh.to_device(x), mesh.to_device(g)
+    base = O.apply_matrix_free(P, nex, ney, 1.0 / nex, 1.0 / ney, x, c_stiff=1.0)
+    gx, gy = np.divmod(np.arange(N), NY)
+    for sides, sel in ((_lib.SIDE_W | _lib.SIDE_E, (gx == 0) | (gx == NX - 1)),
+                       (_lib.SIDE_S, gy == 0), (_lib.SIDE_N | _lib.SIDE_W, (gy == NY - 1) | (gx == 0)),
+                       (15, (gx == 0) | (gx == NX - 1) | (gy == 0) | (gy == NY - 1))):
+        want = base.copy()
+        want[sel] = x[sel] - g[sel]
+        y1 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides, dir_val=G)
+        y2 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_IDENTITY,
+                        dir_mask=torch.as_tensor(sel.astype(np.uint8), device=mesh.device), dir_val=G)
+        assert rel(y1, want) < TOL and torch.equal(y1, y2)
+        want[sel] = g[sel]
+        y3 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_REPLACE, dir_sides=sides, dir_val=G)
+        assert rel(y3, want) < TOL
+    # an irregular mask (as np.isclose could produce) is honoured row by row
+    sel = r.uniform(size=N) < 0.1
+    want = base.copy()
+    want[sel] = x[sel]
+    y = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_IDENTITY,
+                   dir_mask=torch.as_tensor(sel.astype(np.uint8), device=mesh.device))
+    assert rel(y, want) < TOL
+
+
+@pytest.mark.parametrize("key", ["P4_4x4", "P4_3x2", "P8_8x8", "P12_5x3"])
+def test_gather_and_dss_bit_exact(gpu, key):
+    from sem_amd import SEM
+    P, nex, ney = {"P4_4x4": (4, 4, 4), "P4_3x2": (4, 3, 2), "P8_8x8": (8, 8, 8), "P12_5x3": (12, 5, 3)}[key]
+    g = golden("mesh.npz")
+    assert np.array_equal(SEM.scatter(g[key + "_scatter_in"], P, nex, ney), g[key + "_scatter_out"])
+    assert np.array_equal(SEM.assemble(g[key + "_assemble4_in"]), g[key + "_assemble4_out"])
+    # round trip: DSS of gathered values multiplies each node by its multiplicity
+    u = g[key + "_scatter_in"]
+    mult = SEM.assemble(np.ones((nex, ney, P + 1, P + 1)))
+    assert np.array_equal(SEM.assemble(SEM.scatter(u, P, nex, ney)), u * mult)
+
+
+def test_cfg2_checksums_full_size(gpu):
+    """cfg2 (64x64, P=8, N=263169) against the reference's full-size norms / samples."""
+    from sem_amd import SEM
+    g = golden("cfg2_checksums.npz")
+    N = int(g["N"])
+    r = np.random.default_rng(2024)
+    T, u, v = r.uniform(-1, 1, N), r.uniform(-1, 1, N), r.uniform(-1, 1, N)
+    d = 1.0 / 64
+    K = SEM.global_stiffness_matrix(8, 64, 64, d, d)
+    Cx, Cy = SEM.global_convection_matrices(8, 64, 64, d, d)
+    Sys = 40.0 * (SEM.tensordot(Cx, u, (1, 0)) + SEM.tensordot(Cy, v, (1, 0))) + K
+    KT, ST = K @ T, Sys @ T
+    assert abs(np.linalg.norm(KT) - float(g["norm_KT"])) < 1e-12 * float(g["norm_KT"])
+    assert abs(np.linalg.norm(ST) - float(g["norm_SysT"])) < 1e-12 * float(g["norm_SysT"])
+    assert rel(KT[g["sample_idx"]], g["sample_KT"]) < TOL
+    assert rel(ST[g["sample_idx"]], g["sample_SysT"]) < TOL
+    M = SEM.global_mass_matrix(8, 64, 64, d, d)
+    assert rel((M @ T)[g["sample_idx"]], g["sample_MT"]) < TOL
+
+
+@pytest.mark.parametrize("P,ne", [(12, 128), (8, 1024)])
+def test_full_size_properties(gpu, P, ne):
+    """cfg5 (128^2, P=12) and the HBM-regime mesh (1024^2, P=8, N=67M): size-independent
+    identities of the assembled operators, plus bitwise determinism."""
+    from sem_amd.device import get_mesh
+    d = 1.0 / ne
+    mesh = get_mesh(P, ne, ne, d, d)
+    N = mesh.n_local
+    gen = torch.Generator(device=mesh.device).manual_seed(5)
+    x = torch.rand(N, dtype=torch.float64, device=mesh.device, generator=gen) * 2 - 1
+    z = torch.rand(N, dtype=torch.float64, device=mesh.device, generator=gen) * 2 - 1
+    ones = torch.ones(N, dtype=torch.float64, device=mesh.device)
+    Kx = mesh.apply(x, c_stiff=1.0)
+    scale = Kx.abs().max().item()
+    assert mesh.apply(ones, c_stiff=1.0).abs().max().item() < 1e-12 * scale          # constant null space
+    Kz = mesh.apply(z, c_stiff=1.0)
+    assert abs(torch.dot(z, Kx).item() - torch.dot(x, Kz).item()) < 1e-11 * scale * N ** 0.5  # symmetry
+    M1 = mesh.apply(ones, c_mass=1.0)
+    assert abs(M1.sum().item() - 1.0) < 1e-12                                         # area of [0,1]^2
+    xs = torch.as_tensor(np.repeat(np.asarray(__import__("sem_amd").SEM.global_nodes_1d(P, ne, d)), mesh.NY),
+                         device=mesh.device)
+    assert (mesh.apply(xs, c_gradx=1.0) - M1).abs().max().item() < 1e-13 * M1.abs().max().item()  # d(x)/dx = 1
+    assert mesh.apply(xs, c_grady=1.0).abs().max().item() < 1e-13 * M1.abs().max().item()          # d(x)/dy = 0
+    lin = mesh.apply(2.0 * x - 3.0 * z, c_stiff=1.0)
+    assert (lin - (2.0 * Kx - 3.0 * Kz)).abs().max().item() < 1e-12 * scale            # linearity
+    assert torch.equal(Kx, mesh.apply(x, c_stiff=1.0))                                # deterministic
+
+
+def test_interpolation_vs_reference(gpu):
+    from sem_amd import SEM
+    g = golden("cd.npz")
+    pe = SEM.element_nodes(4, 4, 4, 0.25, 0.25)
+    val = SEM.eval_interpolation(SEM.scatter(g["cfg1_T"], 4, 4, 4), pe, (g["cfg1_plot_x"], g["cfg1_plot_y"]))
+    assert np.abs(val - g["cfg1_T_plot"]).max() < 1e-13
+
+
+def test_bad_arguments_raise(gpu):
+    from sem_amd.device import get_mesh
+    mesh = get_mesh(4, 3, 3, 0.1, 0.1)
+    x = torch.zeros(mesh.n_local, dtype=torch.float64, device=mesh.device)
+    with pytest.raises(ValueError):
+        mesh.apply(x[:-1], c_stiff=1.0)
+    with pytest.raises(ValueError):
+        mesh.apply(x, x, c_stiff=1.0)
+    with pytest.raises(ValueError):
+        mesh.apply(x.float(), c_stiff=1.0)
