@@ -16,7 +16,7 @@ LIB = os.path.join(LIBDIR, "libsemops.so")
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["sem_ops.hip", "gll_tables.cpp"]
-HEADERS = ["sem_internal.h", os.path.join("..", "..", "include", "sem_ops.h")]
+HEADERS = ["sem_internal.h", "gll_consts.h", os.path.join("..", "..", "include", "sem_ops.h")]
 
 
 def _hipcc():
@@ -34,10 +34,31 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+CONSTS = os.path.join(CSRC, "gll_consts.h")
+
+
+def gen_consts(verbose=False):
+    """Regenerate gll_consts.h (compile-time GLL tables) with the host GLL code."""
+    exe = os.path.join(LIBDIR, "gen_consts")
+    cxx = shutil.which("g++") or _hipcc()
+    cmd = [cxx, "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"), "-o", exe,
+           os.path.join(CSRC, "gen_consts.cpp"), os.path.join(CSRC, "gll_tables.cpp")]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    text = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
+    old = open(CONSTS).read() if os.path.exists(CONSTS) else None
+    if text != old:
+        with open(CONSTS, "w") as f:
+            f.write(text)
+    return CONSTS
+
+
 def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
+    gen_consts(verbose)
     tmp = LIB + ".tmp"
     cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
            "-I", os.path.join(ROOT, "include"), "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]

@@ -20,6 +20,15 @@
 
 namespace sem {
 
+static thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+void clear_error() { g_last_error.clear(); }
+const char* last_error() { return g_last_error.c_str(); }
+
 int gll_nodes(int P, double* xi, double* w, double* V) {
   if (P < 1 || P > 64) return set_error(SEM_EINVAL, "polynomial order must be in [1, 64]");
   const int n = P + 1;

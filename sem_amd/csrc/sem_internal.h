@@ -11,6 +11,7 @@ namespace sem {
 // Thread-local last-error text (sem_last_error); returns `code` for chaining.
 int set_error(int code, const std::string& msg);
 void clear_error();
+const char* last_error();
 
 int gll_nodes(int P, double* xi, double* w, double* V);
 int gll_differentiation(int P, double* D);

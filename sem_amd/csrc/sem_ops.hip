@@ -25,22 +25,18 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include "gll_consts.h"
 #include "sem_internal.h"
 
 namespace sem {
-
-static thread_local std::string g_last_error;
-
-int set_error(int code, const std::string& msg) {
-  g_last_error = msg;
-  return code;
-}
-void clear_error() { g_last_error.clear(); }
 
 static int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) return SEM_OK;
@@ -65,23 +61,26 @@ struct ApplyArgs {
   double sx, sy, hx, hy, hxy;  // dy/dx, dx/dy, dx/2, dy/2, dx*dy/4
   int64_t NY, NXg, line_begin, line_end;
   int nex, ney, ex_begin, ex_end;
-  int tiles_y, dir_mode;
+  int tiles_x, tiles_y, dir_mode;
   unsigned sides;
   int has_e1, has_e2;
+  int n_local32;  // local vector length (MFMA path: < 2^31)
 };
 
 template <int P>
 struct TileCfg {
   static constexpr int n = P + 1;
-  static constexpr int TX = (16 / P) > 0 ? 16 / P : 1;  // elements per tile in x
-  static constexpr int TY = (64 / P) > 0 ? 64 / P : 1;  // elements per tile in y
-  static constexpr int BX = TX * P;                    // owned lines (+1 at the last tile)
-  static constexpr int BY = TY * P;                    // owned columns (+1 at the last tile)
-  static constexpr int RX = BX + P + 1;                // staged lines
-  static constexpr int RY = BY + P + 1;                // staged columns
-  static constexpr int PT = RY | 1;                    // odd pitch: conflict-free strided reads
-  static constexpr int PY = (BY + 1) | 1;
   static constexpr int THREADS = 128;
+  static constexpr int TX = (16 / P) > 0 ? 16 / P : 1;                       // elements per tile in x
+  static constexpr int TY = (THREADS / (TX * P)) > 0 ? THREADS / (TX * P) : 1; // elements per tile in y
+  static constexpr int BX = TX * P;      // owned lines (+1 closing line at the last tile)
+  static constexpr int BY = TY * P;      // owned columns (+1 closing column at the last tile)
+  static constexpr int RX = BX + P + 1;  // staged lines   [gx0-P, gx0+BX]
+  static constexpr int RY = BY + P + 1;  // staged columns [gy0-P, gy0+BY]
+  static constexpr int PT = RY | 1;      // odd pitch: conflict-free strided LDS reads
+  static constexpr int PY = (BY + 1) | 1;
+  static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;  // staging loads per thread
+  static_assert(TX * BY <= THREADS && TY * BX <= THREADS, "one phase item per thread");
 };
 
 // Sum of GLL weights of the elements in [e_lo, e_hi) that hold 1-D node g.
@@ -93,6 +92,144 @@ __device__ __forceinline__ double weight_sum(int64_t g, int P, int e_lo, int e_h
   if (e - 1 >= e_lo && e - 1 < e_hi) s += w[P];
   if (e >= e_lo && e < e_hi) s += w[0];
   return s;
+}
+
+// One element's K_s / G_s contraction for output row `row` from a (2P+1)-window t
+// (t[P..2P] = this element's nodes, t[0..P] = the left neighbour's, used at row 0).
+// The K_s / G_s coefficients are compile-time constants (gll_consts.h, generated from the same
+// host code that builds each handle's tables).  They are read through template indices into
+// constexpr locals, so every coefficient is folded into the instruction stream: the
+// contraction issues no table loads (a constexpr *array* indexed in a loop is emitted as a
+// global and re-fetched with serialised scalar loads).
+template <int P, int I>
+__device__ __forceinline__ constexpr double kc() {
+  constexpr double v = GllConst<P>::K[I];
+  return v;
+}
+template <int P, int I>
+__device__ __forceinline__ constexpr double gc() {
+  constexpr double v = GllConst<P>::G[I];
+  return v;
+}
+
+template <int P, int ROW, int... L>
+__device__ __forceinline__ void row_dot(const double* t, double& k, double& g, std::integer_sequence<int, L...>) {
+  ((k = fma(kc<P, ROW * (P + 1) + L>(), t[L], k), g = fma(gc<P, ROW * (P + 1) + L>(), t[L], g)), ...);
+}
+
+// One element's K_s / G_s contraction for output row ROW from a (2P+1)-window t
+// (t[P..2P] = this element's nodes, t[0..P] = the left neighbour's, used at row 0).
+template <int P, int ROW>
+__device__ __forceinline__ void contract_row(const double (&t)[2 * P + 1], bool hasL, double& k, double& g) {
+  using Seq = std::make_integer_sequence<int, P + 1>;
+  k = 0.0;
+  g = 0.0;
+  if (ROW == 0 && hasL) row_dot<P, P>(t, k, g, Seq{});
+  row_dot<P, ROW>(t + P, k, g, Seq{});
+}
+
+// Compile-time loop over output rows 0..P: f(std::integral_constant<int, ROW>).
+template <int... R, class F>
+__device__ __forceinline__ void for_rows(std::integer_sequence<int, R...>, F&& f) {
+  (f(std::integral_constant<int, R>{}), ...);
+}
+
+// Phase B item: y-direction contractions of element row `ae` on owned line r (lanes along lines).
+template <int P>
+__device__ __forceinline__ void phase_b(const ApplyArgs& a, const double* Ts, double* Yk, double* Yg, const double* ws,
+                                       int ae, int r, int n0, int64_t gx0) {
+  using C = TileCfg<P>;
+  const int ne = n0 + ae;
+  double t[2 * P + 1];
+#pragma unroll
+  for (int q = 0; q <= 2 * P; ++q) t[q] = Ts[(r + P) * C::PT + ae * P + q];
+  const double mx = weight_sum(gx0 + r, P, a.ex_begin, a.ex_end, ws);
+  const double fk = a.sy * mx, fg = a.hx * mx;
+  const bool hasL = ne > 0, last = ne == a.ney - 1;
+  for_rows(std::make_integer_sequence<int, P + 1>{}, [&](auto J) {
+    constexpr int j = decltype(J)::value;
+    if (j == P && !last) return;  // the closing column exists only in the last element row
+    double k, g;
+    contract_row<P, j>(t, hasL, k, g);
+    Yk[r * C::PY + ae * P + j] = fk * k;
+    Yg[r * C::PY + ae * P + j] = fg * g;
+  });
+}
+
+// Phase A item: x-direction contractions of element column `be` at owned column c, combined
+// with phase B's results and the pointwise terms; writes P (or P+1) outputs of column c.
+template <int P>
+__device__ __forceinline__ void phase_a(const ApplyArgs& a, const double* Ts, const double* Yk, const double* Yg,
+                                        const double* ws, int be, int c, int m0, int64_t gx0, int64_t gy0,
+                                        const double (&pu)[P + 1], const double (&pv)[P + 1]) {
+  using C = TileCfg<P>;
+  const int me = m0 + be;
+  const int64_t gy = gy0 + c;
+  double t[2 * P + 1];
+#pragma unroll
+  for (int q = 0; q <= 2 * P; ++q) t[q] = Ts[(be * P + q) * C::PT + c + P];
+  const double my = weight_sum(gy, P, 0, a.ney, ws);
+  const bool hasL = me - 1 >= a.ex_begin, last = me == a.ex_end - 1;
+  for_rows(std::make_integer_sequence<int, P + 1>{}, [&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if (i == P && !last) return;  // the closing line exists only in the last element column
+    double k, g;
+    contract_row<P, i>(t, hasL, k, g);
+    const int rl = be * P + i;
+    const int64_t gx = gx0 + rl;
+    const int64_t p = (gx - a.line_begin) * a.NY + gy;
+    const double xv = t[P + i];
+    double z = 0.0;
+    if (a.cK != 0.0) z = a.cK * fma(a.sx * my, k, Yk[rl * C::PY + c]);
+    if (a.cM != 0.0) z = fma(a.cM * a.hxy * weight_sum(gx, P, a.ex_begin, a.ex_end, ws) * my, xv, z);
+    if (a.cX != 0.0) z = fma(a.cX * pu[i], a.hy * my * g, z);
+    if (a.cY != 0.0) z = fma(a.cY * pv[i], Yg[rl * C::PY + c], z);
+    if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
+    if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
+    if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
+    if (a.dir_mode != SEM_DIR_NONE) {
+      const bool isd = a.mask ? (a.mask[p] != 0)
+                              : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
+                                 ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1));
+      if (isd) {
+        // an interface line's Dirichlet row is written by its owner (the right strip) only
+        const bool owner = !(gx == a.line_end && a.ex_end < a.nex);
+        if (!owner)
+          z = 0.0;
+        else if (a.dir_mode == SEM_DIR_IDENTITY)
+          z = xv - (a.dval ? a.dval[p] : 0.0);
+        else
+          z = a.dval[p];
+      }
+    }
+    a.y[p] = z;
+  });
+}
+
+// Pointwise coefficients u, v of the P (+1) outputs of a phase-A item, loaded up front so
+// their latency hides under the staging loads (and no load has to wait behind a y store).
+template <int P>
+__device__ __forceinline__ void prefetch_uv(const ApplyArgs& a, int be, int c, int m0, int64_t gx0, int64_t gy0,
+                                            double (&pu)[P + 1], double (&pv)[P + 1]) {
+  const bool last = m0 + be == a.ex_end - 1;
+  // row P of a non-last element column is the next element's row 0: still a valid address,
+  // so every load is unconditional (see the staging loop); its value is simply unused.
+  (void)last;
+  const int64_t p0 = (gx0 + be * P - a.line_begin) * a.NY + gy0 + c;
+  if (a.cu) {
+#pragma unroll
+    for (int i = 0; i <= P; ++i) pu[i] = a.cu[p0 + i * a.NY];
+  } else {
+#pragma unroll
+    for (int i = 0; i <= P; ++i) pu[i] = 1.0;
+  }
+  if (a.cv) {
+#pragma unroll
+    for (int i = 0; i <= P; ++i) pv[i] = a.cv[p0 + i * a.NY];
+  } else {
+#pragma unroll
+    for (int i = 0; i <= P; ++i) pv[i] = 1.0;
+  }
 }
 
 template <int P>
@@ -117,116 +254,58 @@ __global__ __launch_bounds__(TileCfg<P>::THREADS) void apply_tp_valu(const Apply
   const int n1 = min(n0 + C::TY, a.ney);
   const int64_t gx0 = static_cast<int64_t>(m0) * P;
   const int64_t gy0 = static_cast<int64_t>(n0) * P;
-  const int BXo = (m1 - m0) * P + (m1 == a.ex_end ? 1 : 0);  // owned lines
-  const int BYo = (n1 - n0) * P + (n1 == a.ney ? 1 : 0);     // owned columns
   const int tid = threadIdx.x;
+  const bool lastx = m1 == a.ex_end, lasty = n1 == a.ney;
 
-  const double* Ks = a.tab;
-  const double* Gs = a.tab + n * n;
-  if (tid < n) ws[tid] = a.tab[2 * n * n + tid];
+  // ---- issue every global load of this thread first: the staged tile and u, v
+  // GLL weights for weight_sum: issued first so the LDS store below waits for this load only
+  const double wreg = a.tab[2 * n * n + min(tid, n - 1)];
 
-  // ---- stage x tile (zero outside the locally held lines / the domain)
-  for (int idx = tid; idx < C::RX * C::RY; idx += C::THREADS) {
+  // Loads are unconditional from clamped (always in-bounds) addresses: a per-element
+  // "load or zero" select makes hipcc branch around, and wait for, each load in turn.
+  // Staged entries outside the domain / the local lines hold clamped copies; they are
+  // never consumed (they only feed left windows gated by hasL, or non-owned rows).
+  double stage[C::NSTAGE];
+#pragma unroll
+  for (int s = 0; s < C::NSTAGE; ++s) {
+    const int idx = min(tid + s * C::THREADS, C::RX * C::RY - 1);
     const int rr = idx / C::RY, cc = idx - rr * C::RY;
-    const int64_t gx = gx0 - P + rr, gy = gy0 - P + cc;
-    double v = 0.0;
-    if (gx >= a.line_begin && gx <= a.line_end && gy >= 0 && gy < a.NY) v = a.x[(gx - a.line_begin) * a.NY + gy];
-    Ts[rr * C::PT + cc] = v;
+    const int64_t gx = min(max(gx0 - P + rr, a.line_begin), a.line_end);
+    const int64_t gy = min(max(gy0 - P + cc, int64_t(0)), a.NY - 1);
+    stage[s] = a.x[(gx - a.line_begin) * a.NY + gy];
   }
-  __syncthreads();
+  // phase-A item of this thread: (element column be, owned column c)
+  const int be = tid / C::BY, cA = tid - be * C::BY;
+  const bool hasA = be < m1 - m0 && cA < (n1 - n0) * P;
+  double pu[P + 1], pv[P + 1];
+  if (hasA) prefetch_uv<P>(a, be, cA, m0, gx0, gy0, pu, pv);
 
-  // ---- phase B: y-direction (K_s / G_s along each x-line), lanes along lines
-  const int itemsB = (n1 - n0) * BXo;
-  for (int it = tid; it < itemsB; it += C::THREADS) {
-    const int ae = it / BXo, r = it - ae * BXo;
-    const int ne = n0 + ae;
-    const int64_t gx = gx0 + r;
-    double t[2 * P + 1];
+  if (tid < n) ws[tid] = wreg;
 #pragma unroll
-    for (int qq = 0; qq <= 2 * P; ++qq) t[qq] = Ts[(r + P) * C::PT + ae * P + qq];
-    const double mx = weight_sum(gx, P, a.ex_begin, a.ex_end, ws);
-    const double fk = a.sy * mx, fg = a.hx * mx;
-    const bool hasL = ne > 0;
-    const bool last = ne == a.ney - 1;
-#pragma unroll
-    for (int j = 0; j <= P; ++j) {
-      if (j == P && !last) continue;  // the closing column exists only in the last element row
-      double k = 0.0, g = 0.0;
-      if (j == 0 && hasL) {
-#pragma unroll
-        for (int l = 0; l <= P; ++l) {
-          k = fma(Ks[P * n + l], t[l], k);
-          g = fma(Gs[P * n + l], t[l], g);
-        }
-      }
-#pragma unroll
-      for (int l = 0; l <= P; ++l) {
-        k = fma(Ks[j * n + l], t[P + l], k);
-        g = fma(Gs[j * n + l], t[P + l], g);
-      }
-      Yk[r * C::PY + ae * P + j] = fk * k;
-      Yg[r * C::PY + ae * P + j] = fg * g;
+  for (int s = 0; s < C::NSTAGE; ++s) {
+    const int idx = tid + s * C::THREADS;
+    if (idx < C::RX * C::RY) {
+      const int rr = idx / C::RY, cc = idx - rr * C::RY;
+      Ts[rr * C::PT + cc] = stage[s];
     }
   }
   __syncthreads();
 
-  // ---- phase A: x-direction + combine + epilogue, lanes along columns (coalesced)
-  const int itemsA = (m1 - m0) * BYo;
-  for (int it = tid; it < itemsA; it += C::THREADS) {
-    const int be = it / BYo, c = it - be * BYo;
-    const int me = m0 + be;
-    const int64_t gy = gy0 + c;
-    double t[2 * P + 1];
-#pragma unroll
-    for (int qq = 0; qq <= 2 * P; ++qq) t[qq] = Ts[(be * P + qq) * C::PT + c + P];
-    const double my = weight_sum(gy, P, 0, a.ney, ws);
-    const bool hasL = me - 1 >= a.ex_begin;
-    const bool last = me == a.ex_end - 1;
-#pragma unroll
-    for (int i = 0; i <= P; ++i) {
-      if (i == P && !last) continue;  // the closing line exists only in the last element column
-      double k = 0.0, g = 0.0;
-      if (i == 0 && hasL) {
-#pragma unroll
-        for (int l = 0; l <= P; ++l) {
-          k = fma(Ks[P * n + l], t[l], k);
-          g = fma(Gs[P * n + l], t[l], g);
-        }
-      }
-#pragma unroll
-      for (int l = 0; l <= P; ++l) {
-        k = fma(Ks[i * n + l], t[P + l], k);
-        g = fma(Gs[i * n + l], t[P + l], g);
-      }
-      const int rl = be * P + i;  // owned-line index within the tile
-      const int64_t gx = gx0 + rl;
-      const int64_t p = (gx - a.line_begin) * a.NY + gy;
-      const double xv = t[P + i];
-      double z = 0.0;
-      if (a.cK != 0.0) z = a.cK * fma(a.sx * my, k, Yk[rl * C::PY + c]);
-      if (a.cM != 0.0) z = fma(a.cM * a.hxy * weight_sum(gx, P, a.ex_begin, a.ex_end, ws) * my, xv, z);
-      if (a.cX != 0.0) z = fma(a.cX * (a.cu ? a.cu[p] : 1.0), a.hy * my * g, z);
-      if (a.cY != 0.0) z = fma(a.cY * (a.cv ? a.cv[p] : 1.0), Yg[rl * C::PY + c], z);
-      if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
-      if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
-      if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
-      if (a.dir_mode != SEM_DIR_NONE) {
-        const bool isd = a.mask ? (a.mask[p] != 0)
-                                : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
-                                   ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1));
-        if (isd) {
-          // an interface line's Dirichlet row is written by its owner (the right strip) only
-          const bool owner = !(gx == a.line_end && a.ex_end < a.nex);
-          if (!owner)
-            z = 0.0;
-          else if (a.dir_mode == SEM_DIR_IDENTITY)
-            z = xv - (a.dval ? a.dval[p] : 0.0);
-          else
-            z = a.dval[p];
-        }
-      }
-      a.y[p] = z;
-    }
+  // ---- phase B: (element row ae, owned line r), lanes along lines
+  {
+    const int ae = tid / C::BX, r = tid - ae * C::BX;
+    if (ae < n1 - n0 && r < (m1 - m0) * P) phase_b<P>(a, Ts, Yk, Yg, ws, ae, r, n0, gx0);
+    if (lastx && tid < n1 - n0) phase_b<P>(a, Ts, Yk, Yg, ws, tid, (m1 - m0) * P, n0, gx0);  // closing line
+  }
+  __syncthreads();
+
+  // ---- phase A: (element column be, owned column c), lanes along columns (coalesced I/O)
+  if (hasA) phase_a<P>(a, Ts, Yk, Yg, ws, be, cA, m0, gx0, gy0, pu, pv);
+  if (lasty && tid < m1 - m0) {  // closing column
+    const int cz = (n1 - n0) * P;
+    double qu[P + 1], qv[P + 1];
+    prefetch_uv<P>(a, tid, cz, m0, gx0, gy0, qu, qv);
+    phase_a<P>(a, Ts, Yk, Yg, ws, tid, cz, m0, gx0, gy0, qu, qv);
   }
 }
 
@@ -242,6 +321,539 @@ static int launch_apply(const ApplyArgs& args_in, const sem_handle* h, hipStream
   if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
   hipLaunchKernelGGL(apply_tp_valu<P>, dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0, s, args);
   return hip_check(hipGetLastError(), "apply launch");
+}
+
+// =========================================================================== MFMA path
+//
+// Same operator, same tile ownership; the per-element contractions run on the fp64
+// matrix cores (v_mfma_f64_16x16x4_f64) instead of the VALU:
+//   phase A (x): for each element column e of the tile (plus the left halo element) and
+//                each 16-column block,  D[i][c] = sum_k K_s[i][k] T[eP+k][c]  (and G_s),
+//                A = K_s (rows i <= P, zero-padded to 16 x 4*KS), B = staged x.
+//   phase B (y): for each element row e and each 16-line block,
+//                D[line][j] = sum_l T[line][eP+l] K_s[j][l]                    (and G_s),
+//                A = staged x, B = K_s^T -- the SAME per-lane registers as phase A's A.
+// Results go to LDS per element (all P+1 rows), and the epilogue sums the one or two
+// element contributions of every owned node in a fixed order (deterministic DSS).
+// The VALU is left with staging, the epilogue and the pointwise terms.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int pitch18(int w) { return w + ((18 - (w % 32)) + 32) % 32; }  // >= w, == 18 (mod 32)
+
+template <int P, int TX_, int TY_, int NW_>
+struct MCfg {
+  static constexpr int n = P + 1, TX = TX_, TY = TY_, NW = NW_, THREADS = 64 * NW_;
+  static constexpr int BX = TX * P, BY = TY * P;          // owned lines / columns (w/o closing ones)
+  static constexpr int NLB = (BX + 15) / 16, NCB = (BY + 15) / 16;  // 16-wide MFMA blocks
+  static constexpr int KS = (n + 3) / 4;                  // k-steps of 4
+  static constexpr int RX = cmax(TX * P + 4 * KS, P + 16 * NLB);    // staged lines from gx0-P
+  static constexpr int RY = cmax(TY * P + 4 * KS, P + 16 * NCB);    // staged columns from gy0-P
+  static constexpr int PT = pitch18(RY);
+  static constexpr int EC = 16 * NCB;   // E (x-results) column pitch
+  static constexpr int FL = 16 * NLB;   // F (y-results) lines per element row
+  static constexpr int TA = (TX + 1) * NCB, TB = (TY + 1) * NLB;
+  static constexpr int TPW = (TA + TB + NW - 1) / NW;     // MFMA tasks per wave
+  static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
+  static constexpr int NMAIN = (BX * BY + THREADS - 1) / THREADS;  // epilogue nodes per thread
+  static_assert(n <= 16, "MFMA path needs P+1 <= 16");
+};
+
+template <class C>
+struct MSmem {
+  double Ts[C::RX * C::PT];
+  double EK[(C::TX + 1) * C::n * C::EC];
+  double EG[(C::TX + 1) * C::n * C::EC];
+  double FK[(C::TY + 1) * C::FL * C::n];
+  double FG[(C::TY + 1) * C::FL * C::n];
+  double Kt[C::n * C::n];  // coefficient tables for the closing-line / closing-column path
+  double Gt[C::n * C::n];
+  double ws[C::n];
+};
+
+// Generic (VALU) contraction along one staged direction for nodes the MFMA blocks do not
+// cover (the domain's closing line / column): `base` points at the element's node 0 in the
+// staged tile, `stride` is the distance between consecutive nodes of the direction.
+template <int P>
+__device__ __forceinline__ void contract_generic(const double* Kt, const double* Gt, const double* base, int stride,
+                                                 int row, bool hasR, bool hasL, double& k, double& g) {
+  constexpr int n = P + 1;
+  k = 0.0;
+  g = 0.0;
+  if (row == 0 && hasL) {
+    for (int l = 0; l <= P; ++l) {
+      const double t = base[(l - P) * stride];
+      k = fma(Kt[P * n + l], t, k);
+      g = fma(Gt[P * n + l], t, g);
+    }
+  }
+  if (hasR) {
+    for (int l = 0; l <= P; ++l) {
+      const double t = base[l * stride];
+      k = fma(Kt[row * n + l], t, k);
+      g = fma(Gt[row * n + l], t, g);
+    }
+  }
+}
+
+template <int P, int TX, int TY, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
+  using C = MCfg<P, TX, TY, NW>;
+  constexpr int n = C::n;
+  __shared__ MSmem<C> sm;
+
+  // Persistent workgroups: each walks a contiguous run of tiles (y fastest), so consecutive
+  // tiles of one workgroup share y-halo lines in its XCD's L2.  The XCD-aware remap gives the
+  // workgroups of one XCD neighbouring runs.
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = nb >> 3, rem = nb & 7;
+  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int ntiles = a.tiles_x * a.tiles_y;
+  const int t_begin = static_cast<int>((static_cast<long long>(L) * ntiles) / nb);
+  const int t_end = static_cast<int>((static_cast<long long>(L + 1) * ntiles) / nb);
+
+  const int lb0 = static_cast<int>(a.line_begin), lb1 = static_cast<int>(a.line_end), NY = static_cast<int>(a.NY);
+  const int nmax = a.n_local32 - 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+
+  // ---- per-lane MFMA coefficient operands: A[i=lr][k=4s+lk] = K_s[lr][k] (0 outside n x n)
+  double aK[C::KS], aG[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) {
+    const int k = 4 * s + lk;
+    const bool ok = lr <= P && k <= P;
+    const int idx = ok ? lr * n + k : 0;
+    const double kv = a.tab[idx], gv = a.tab[n * n + idx];
+    aK[s] = ok ? kv : 0.0;
+    aG[s] = ok ? gv : 0.0;
+  }
+  for (int t = tid; t < n * n; t += C::THREADS) {
+    sm.Kt[t] = a.tab[t];
+    sm.Gt[t] = a.tab[n * n + t];
+  }
+  if (tid < n) sm.ws[tid] = a.tab[2 * n * n + tid];
+
+  // Issue every global load of tile t (staged x window, u and v of this thread's epilogue
+  // nodes) from clamped, always in-bounds addresses; values of clamped entries are never
+  // consumed.  No load is conditional: a "load or zero" select makes hipcc wait per load.
+  double st[C::NSTAGE], pu[C::NMAIN], pv[C::NMAIN];
+  auto issue = [&](int t) {
+    const int tx = t / a.tiles_y, ty = t - tx * a.tiles_y;
+    const int gx0 = (a.ex_begin + tx * TX) * P, gy0 = ty * TY * P;
+#pragma unroll
+    for (int s = 0; s < C::NSTAGE; ++s) {
+      const int idx = min(tid + s * C::THREADS, C::RX * C::RY - 1);
+      const int rr = idx / C::RY, cc = idx - rr * C::RY;
+      const int gx = min(max(gx0 - P + rr, lb0), lb1);
+      const int gy = min(max(gy0 - P + cc, 0), NY - 1);
+      st[s] = a.x[(gx - lb0) * NY + gy];
+    }
+#pragma unroll
+    for (int qn = 0; qn < C::NMAIN; ++qn) {
+      const int idx = tid + qn * C::THREADS;
+      const int rl = idx / C::BY, c = idx - rl * C::BY;
+      const int p = min(max((gx0 + rl - lb0) * NY + gy0 + c, 0), nmax);
+      pu[qn] = a.cu ? a.cu[p] : 1.0;
+      pv[qn] = a.cv ? a.cv[p] : 1.0;
+    }
+  };
+  if (t_begin < t_end) issue(t_begin);
+
+  for (int t = t_begin; t < t_end; ++t) {
+    const int tx = t / a.tiles_y, ty = t - tx * a.tiles_y;
+    const int m0 = a.ex_begin + tx * TX, m1 = min(m0 + TX, a.ex_end);
+    const int n0 = ty * TY, n1 = min(n0 + TY, a.ney);
+    const int gx0 = m0 * P, gy0 = n0 * P;
+
+    __syncthreads();  // the previous tile's epilogue has finished reading Ts
+#pragma unroll
+    for (int s = 0; s < C::NSTAGE; ++s) {
+      const int idx = tid + s * C::THREADS;
+      if (idx < C::RX * C::RY) {
+        const int rr = idx / C::RY, cc = idx - rr * C::RY;
+        sm.Ts[rr * C::PT + cc] = st[s];
+      }
+    }
+    double cu_[C::NMAIN], cv_[C::NMAIN];
+#pragma unroll
+    for (int qn = 0; qn < C::NMAIN; ++qn) {
+      cu_[qn] = pu[qn];
+      cv_[qn] = pv[qn];
+    }
+    __syncthreads();
+    if (t + 1 < t_end) issue(t + 1);  // next tile's loads fly while this tile computes
+
+    // ---- phases A and B: MFMA tasks, round-robin over waves
+#pragma unroll
+    for (int tt = 0; tt < C::TPW; ++tt) {
+      const int task = wave + tt * NW;
+      if (task < C::TA) {
+        const int e = task / C::NCB, cb = task - e * C::NCB;  // element column e (0 = halo), column block
+        dbl4 accK = {0.0, 0.0, 0.0, 0.0}, accG = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) {
+          const int k = 4 * s + lk;
+          double bv = sm.Ts[(e * P + k) * C::PT + P + cb * 16 + lr];
+          if (4 * s + 3 > P) bv = k <= P ? bv : 0.0;  // next element's nodes: keep NaN/Inf out
+          accK = __builtin_amdgcn_mfma_f64_16x16x4f64(aK[s], bv, accK, 0, 0, 0);
+          accG = __builtin_amdgcn_mfma_f64_16x16x4f64(aG[s], bv, accG, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = lk + 4 * r;  // C/D row of an f64 16x16x4 MFMA: (lane>>4) + 4*reg
+          if (i <= P) {
+            sm.EK[(e * n + i) * C::EC + cb * 16 + lr] = accK[r];
+            sm.EG[(e * n + i) * C::EC + cb * 16 + lr] = accG[r];
+          }
+        }
+      } else if (task < C::TA + C::TB) {
+        const int tb = task - C::TA;
+        const int e = tb / C::NLB, lbk = tb - e * C::NLB;  // element row e (0 = halo), line block
+        dbl4 accK = {0.0, 0.0, 0.0, 0.0}, accG = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) {
+          const int k = 4 * s + lk;
+          double av = sm.Ts[(P + lbk * 16 + lr) * C::PT + e * P + k];
+          if (4 * s + 3 > P) av = k <= P ? av : 0.0;
+          accK = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aK[s], accK, 0, 0, 0);
+          accG = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aG[s], accG, 0, 0, 0);
+        }
+        if (lr <= P) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int line = lbk * 16 + lk + 4 * r;
+            sm.FK[(e * C::FL + line) * n + lr] = accK[r];
+            sm.FG[(e * C::FL + line) * n + lr] = accG[r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- epilogue: one owned node per item, lanes along columns (coalesced global I/O)
+    const int BXo = (m1 - m0) * P, BYo = (n1 - n0) * P;  // owned without closing line / column
+    const bool lastx = m1 == a.ex_end, lasty = n1 == a.ney;
+    auto node = [&](int rl, int c, double uu, double vv) {
+      const int gx = gx0 + rl, gy = gy0 + c;
+      const int p = (gx - lb0) * NY + gy;
+      const double xv = sm.Ts[(P + rl) * C::PT + P + c];
+      // x-direction: element column of this line (right) and, at a shared line, the left one
+      const int i = rl % P, ex = rl / P;
+      const int mR = m0 + ex;
+      const bool hasR = mR < a.ex_end, hasLx = i == 0 && mR - 1 >= a.ex_begin;
+      double XK = 0.0, XG = 0.0;
+      if (c < C::EC) {
+        if (hasLx) {
+          XK = sm.EK[(ex * n + P) * C::EC + c];
+          XG = sm.EG[(ex * n + P) * C::EC + c];
+        }
+        if (hasR) {
+          XK += sm.EK[((ex + 1) * n + i) * C::EC + c];
+          XG += sm.EG[((ex + 1) * n + i) * C::EC + c];
+        }
+      } else {
+        contract_generic<P>(sm.Kt, sm.Gt, &sm.Ts[(P + rl - i) * C::PT + P + c], C::PT, i, hasR, hasLx, XK, XG);
+      }
+      // y-direction
+      const int j = c % P, ey = c / P;
+      const int nR = n0 + ey;
+      const bool hasRy = nR < a.ney, hasLy = j == 0 && nR - 1 >= 0;
+      double YK = 0.0, YG = 0.0;
+      if (rl < C::FL) {
+        if (hasLy) {
+          YK = sm.FK[(ey * C::FL + rl) * n + P];
+          YG = sm.FG[(ey * C::FL + rl) * n + P];
+        }
+        if (hasRy) {
+          YK += sm.FK[((ey + 1) * C::FL + rl) * n + j];
+          YG += sm.FG[((ey + 1) * C::FL + rl) * n + j];
+        }
+      } else {
+        contract_generic<P>(sm.Kt, sm.Gt, &sm.Ts[(P + rl) * C::PT + P + c - j], 1, j, hasRy, hasLy, YK, YG);
+      }
+      const double mx = weight_sum(gx, P, a.ex_begin, a.ex_end, sm.ws);
+      const double my = weight_sum(gy, P, 0, a.ney, sm.ws);
+      double z = 0.0;
+      if (a.cK != 0.0) z = a.cK * fma(a.sx * my, XK, a.sy * mx * YK);
+      if (a.cM != 0.0) z = fma(a.cM * a.hxy * mx * my, xv, z);
+      if (a.cX != 0.0) z = fma(a.cX * uu, a.hy * my * XG, z);
+      if (a.cY != 0.0) z = fma(a.cY * vv, a.hx * mx * YG, z);
+      if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
+      if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
+      if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
+      if (a.dir_mode != SEM_DIR_NONE) {
+        const bool isd = a.mask ? (a.mask[p] != 0)
+                                : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
+                                   ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
+        if (isd) {
+          // an interface line's Dirichlet row is written by its owner (the right strip) only
+          const bool owner = !(gx == lb1 && a.ex_end < a.nex);
+          if (!owner)
+            z = 0.0;
+          else if (a.dir_mode == SEM_DIR_IDENTITY)
+            z = xv - (a.dval ? a.dval[p] : 0.0);
+          else
+            z = a.dval[p];
+        }
+      }
+      a.y[p] = z;
+    };
+#pragma unroll
+    for (int qn = 0; qn < C::NMAIN; ++qn) {
+      const int idx = tid + qn * C::THREADS;
+      const int rl = idx / C::BY, c = idx - rl * C::BY;
+      if (idx < C::BX * C::BY && rl < BXo && c < BYo) node(rl, c, cu_[qn], cv_[qn]);
+    }
+    auto edge = [&](int rl, int c) {
+      const int p = (gx0 + rl - lb0) * NY + gy0 + c;
+      node(rl, c, a.cu ? a.cu[p] : 1.0, a.cv ? a.cv[p] : 1.0);
+    };
+    if (lastx)  // closing line of the local lines
+      for (int c = tid; c < BYo + (lasty ? 1 : 0); c += C::THREADS) edge(BXo, c);
+    if (lasty)  // closing column of the domain
+      for (int rl = tid; rl < BXo; rl += C::THREADS) edge(rl, BYo);
+  }
+}
+
+template <int P, int TX, int TY, int NW>
+static int launch_apply_mfma(const ApplyArgs& args_in, const sem_handle* h, hipStream_t s) {
+  using C = MCfg<P, TX, TY, NW>;
+  ApplyArgs args = args_in;
+  const int ncols = h->ex_end - h->ex_begin;
+  args.tiles_x = (ncols + TX - 1) / TX;
+  args.tiles_y = (h->ney + TY - 1) / TY;
+  const long long ntiles = static_cast<long long>(args.tiles_x) * args.tiles_y;
+  if (ntiles <= 0 || ntiles > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
+  // persistent grid: the resident workgroups of every CU, never more than the tiles
+  static int resident = [] {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, apply_tp_mfma<P, TX, TY, NW>, C::THREADS, 0) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus < 1)
+      cus = 256;
+    return per_cu * cus;
+  }();
+  static const int oversub = [] {
+    const char* e = std::getenv("SEM_MFMA_OVERSUB");  // tuning override: grid = resident x this
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  const long long grid = std::min<long long>(ntiles, static_cast<long long>(resident) * oversub);
+  hipLaunchKernelGGL((apply_tp_mfma<P, TX, TY, NW>), dim3(static_cast<unsigned>(grid)), dim3(C::THREADS), 0, s,
+                     args);
+  return hip_check(hipGetLastError(), "apply (mfma) launch");
+}
+
+// Tile shapes: element tiles of ~32 x 32 nodes (4 waves) for large meshes, ~16 x 16 nodes
+// (2 waves) when the mesh is too small to give every CU several workgroups.
+template <int P>
+static int launch_apply_mfma_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
+  constexpr int TL = (32 / P) > 0 ? 32 / P : 1;
+  constexpr int TS = (16 / P) > 0 ? 16 / P : 1;
+  const long long big_tiles = static_cast<long long>((h->ex_end - h->ex_begin + TL - 1) / TL) * ((h->ney + TL - 1) / TL);
+  static const int force = [] {
+    const char* e = std::getenv("SEM_MFMA_TILE");  // tuning override: 1 = small, 2 = large
+    return e ? std::atoi(e) : 0;
+  }();
+  if (force == 2 || (force == 0 && big_tiles >= 4 * 256)) return launch_apply_mfma<P, TL, TL, 4>(args, h, s);
+  return launch_apply_mfma<P, TS, TS, 2>(args, h, s);
+}
+
+// =========================================================================== column kernel
+//
+// Single-phase VALU kernel.  Thread = (element column e of the tile, row split s, column c);
+// lanes run along columns (coalesced global I/O), so within a wave the element-local row i
+// is uniform: the x-direction coefficients K_s[i][.] / G_s[i][.] are instruction immediates
+// and the x-window T[eP-P .. eP+P][c] is loaded once into registers and reused by every row.
+// The y-direction needs the coefficient row of the column's local index j = gy mod P, which
+// differs per lane but is fixed for the thread: it is loaded once into registers.  No
+// intermediate buffers, one barrier per tile.
+template <int P, int TX, int BY, int RS>
+struct CCfg {
+  static constexpr int n = P + 1;
+  static constexpr int RP = P / RS;                   // rows per thread
+  static constexpr int THREADS = TX * RS * BY;
+  static constexpr int BX = TX * P;
+  static constexpr int RX = BX + P + 1;               // staged lines   [gx0-P, gx0+BX]
+  static constexpr int RY = BY + 2 * P + 1;           // staged columns [gy0-P, gy0+BY+P]
+  static constexpr int PT = RY;                       // lanes read along a row: any pitch is conflict-free
+  static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
+  static_assert(P % RS == 0, "row splits must divide P");
+  static_assert((BY * RS) % 64 == 0, "a wave must hold one (element column, split)");
+  static_assert(THREADS <= 1024, "workgroup too large");
+};
+
+template <int P, int TX, int BY, int RS>
+__global__ __launch_bounds__((CCfg<P, TX, BY, RS>::THREADS)) void apply_tp_col(const ApplyArgs a) {
+  using C = CCfg<P, TX, BY, RS>;
+  constexpr int n = C::n, RP = C::RP;
+  __shared__ double Ts[C::RX * C::PT];
+  __shared__ double ws[n];
+
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = nb >> 3, rem = nb & 7;
+  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tx = L / a.tiles_y, ty = L - tx * a.tiles_y;
+  const int lb0 = static_cast<int>(a.line_begin), lb1 = static_cast<int>(a.line_end), NY = static_cast<int>(a.NY);
+  const int m0 = a.ex_begin + tx * TX, m1 = min(m0 + TX, a.ex_end);
+  const int gx0 = m0 * P, gy0 = ty * BY;
+  const int BYo = min(BY, NY - 1 - gy0);     // owned columns without the domain's closing one
+  const bool lasty = gy0 + BY >= NY - 1;
+  const int tid = threadIdx.x;
+  const int c = tid % BY, s = (tid / BY) % RS, e = tid / (BY * RS);
+  const int me = m0 + e;                      // this thread's element column
+  const bool hasE = me < m1;
+
+  const double wreg = a.tab[2 * n * n + min(tid, n - 1)];
+  // ---- stage x (clamped, unconditional loads)
+  double st[C::NSTAGE];
+#pragma unroll
+  for (int k = 0; k < C::NSTAGE; ++k) {
+    const int idx = min(tid + k * C::THREADS, C::RX * C::RY - 1);
+    const int rr = idx / C::RY, cc = idx - rr * C::RY;
+    const int gx = min(max(gx0 - P + rr, lb0), lb1);
+    const int gy = min(max(gy0 - P + cc, 0), NY - 1);
+    st[k] = a.x[(gx - lb0) * NY + gy];
+  }
+  // ---- this thread's rows: u, v prefetch (clamped addresses)
+  const int nmax = a.n_local32 - 1;
+  double pu[RP + 1], pv[RP + 1];
+#pragma unroll
+  for (int ii = 0; ii <= RP; ++ii) {
+    const int p = min((me * P + s * RP + ii - lb0) * NY + gy0 + c, nmax);
+    pu[ii] = a.cu ? a.cu[p] : 1.0;
+    pv[ii] = a.cv ? a.cv[p] : 1.0;
+  }
+  if (tid < n) ws[tid] = wreg;
+#pragma unroll
+  for (int k = 0; k < C::NSTAGE; ++k) {
+    const int idx = tid + k * C::THREADS;
+    if (idx < C::RX * C::RY) {
+      const int rr = idx / C::RY, cc = idx - rr * C::RY;
+      Ts[rr * C::PT + cc] = st[k];
+    }
+  }
+  __syncthreads();
+
+  // per-column (per-lane) y data: local index j, right/left element flags, coefficient rows
+  auto column = [&](int cc, double (&uu)[RP + 1], double (&vv)[RP + 1]) {
+    const int gy = gy0 + cc;
+    const int j = gy % P, ne = gy / P;
+    const bool hasRy = ne < a.ney, hasLy = j == 0 && ne > 0;
+    double rK[n], rG[n];
+#pragma unroll
+    for (int l = 0; l <= P; ++l) {
+      const int idx = (hasRy ? j : 0) * n + l;
+      const double kv = a.tab[idx], gv = a.tab[n * n + idx];
+      rK[l] = hasRy ? kv : 0.0;
+      rG[l] = hasRy ? gv : 0.0;
+    }
+    const double my = weight_sum(gy, P, 0, a.ney, ws);
+    // x-window of this element column along column cc: T[meP-P+k][gy], k = 0..2P
+    double xt[2 * P + 1];
+#pragma unroll
+    for (int k = 0; k <= 2 * P; ++k) xt[k] = Ts[(e * P + k) * C::PT + P + cc];
+    const bool hasLx = me - 1 >= a.ex_begin, lastE = me == a.ex_end - 1;
+    const double* trow0 = &Ts[P + cc - j];  // y-window base of the right element (row offset added below)
+    auto row = [&](auto I, double uval, double vval) {
+      constexpr int i = decltype(I)::value;
+      const int rl = e * P + i;  // line index within the tile
+      const int gx = gx0 + rl;
+      double kx, gxv;
+      contract_row<P, i>(xt, hasLx, kx, gxv);
+      // y-direction for line gx
+      const double* tr = trow0 + (P + rl) * C::PT;
+      double ky = 0.0, gyv = 0.0;
+      if (hasLy) row_dot<P, P>(tr - P, ky, gyv, std::make_integer_sequence<int, P + 1>{});  // left element, row P
+#pragma unroll
+      for (int l = 0; l <= P; ++l) {
+        const double t = tr[l];
+        ky = fma(rK[l], t, ky);
+        gyv = fma(rG[l], t, gyv);
+      }
+      const int p = (gx - lb0) * NY + gy;
+      const double xv = xt[P + i];
+      const double mx = weight_sum(gx, P, a.ex_begin, a.ex_end, ws);
+      double z = 0.0;
+      if (a.cK != 0.0) z = a.cK * fma(a.sx * my, kx, a.sy * mx * ky);
+      if (a.cM != 0.0) z = fma(a.cM * a.hxy * mx * my, xv, z);
+      if (a.cX != 0.0) z = fma(a.cX * uval, a.hy * my * gxv, z);
+      if (a.cY != 0.0) z = fma(a.cY * vval, a.hx * mx * gyv, z);
+      if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
+      if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
+      if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
+      if (a.dir_mode != SEM_DIR_NONE) {
+        const bool isd = a.mask ? (a.mask[p] != 0)
+                                : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
+                                   ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
+        if (isd) {
+          const bool owner = !(gx == lb1 && a.ex_end < a.nex);
+          if (!owner)
+            z = 0.0;
+          else if (a.dir_mode == SEM_DIR_IDENTITY)
+            z = xv - (a.dval ? a.dval[p] : 0.0);
+          else
+            z = a.dval[p];
+        }
+      }
+      a.y[p] = z;
+    };
+    // rows of this split (wave-uniform split -> compile-time rows), plus the closing line
+    auto rows = [&](auto S) {
+      constexpr int s0 = decltype(S)::value * RP;
+      for_rows(std::make_integer_sequence<int, RP>{}, [&](auto II) {
+        constexpr int ii = decltype(II)::value;
+        row(std::integral_constant<int, s0 + ii>{}, uu[ii], vv[ii]);
+      });
+      if constexpr (decltype(S)::value == RS - 1) {
+        if (lastE) row(std::integral_constant<int, P>{}, uu[RP], vv[RP]);
+      }
+    };
+    for_rows(std::make_integer_sequence<int, RS>{}, [&](auto S) {
+      if (s == decltype(S)::value) rows(S);
+    });
+  };
+  if (hasE && c < BYo) column(c, pu, pv);
+  if (hasE && lasty && c == 0) {  // the domain's closing column
+    double qu[RP + 1], qv[RP + 1];
+#pragma unroll
+    for (int ii = 0; ii <= RP; ++ii) {
+      const int p = min((me * P + s * RP + ii - lb0) * NY + gy0 + BYo, nmax);
+      qu[ii] = a.cu ? a.cu[p] : 1.0;
+      qv[ii] = a.cv ? a.cv[p] : 1.0;
+    }
+    column(BYo, qu, qv);
+  }
+}
+
+template <int P, int TX, int BY, int RS>
+static int launch_apply_col(const ApplyArgs& args_in, const sem_handle* h, hipStream_t s) {
+  using C = CCfg<P, TX, BY, RS>;
+  ApplyArgs args = args_in;
+  const int ncols = h->ex_end - h->ex_begin;
+  args.tiles_x = (ncols + TX - 1) / TX;
+  args.tiles_y = static_cast<int>((h->NY - 1 + BY - 1) / BY);
+  const long long nblk = static_cast<long long>(args.tiles_x) * args.tiles_y;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
+  hipLaunchKernelGGL((apply_tp_col<P, TX, BY, RS>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0, s, args);
+  return hip_check(hipGetLastError(), "apply (column) launch");
+}
+
+template <int P>
+static int launch_apply_col_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
+  static const int force = [] {
+    const char* e = std::getenv("SEM_COL_TILE");  // tuning override
+    return e ? std::atoi(e) : 0;
+  }();
+  constexpr int RS = (P % 4 == 0) ? 4 : (P % 2 == 0 ? 2 : 1);
+  constexpr int BYs = 64 / RS > 16 ? 64 / RS : 16;
+  const long long n = h->n_local;
+  if (force == 2 || (force == 0 && n >= (1LL << 23))) return launch_apply_col<P, 4, 64, 1>(args, h, s);
+  if (force == 3) return launch_apply_col<P, 2, 64, 1>(args, h, s);
+  return launch_apply_col<P, 2, BYs, RS>(args, h, s);
 }
 
 // --------------------------------------------------------------------------- gather / DSS
@@ -346,7 +958,7 @@ using namespace sem;
 extern "C" {
 
 int sem_abi_version(void) { return SEM_ABI_VERSION; }
-const char* sem_last_error(void) { return g_last_error.c_str(); }
+const char* sem_last_error(void) { return last_error(); }
 int sem_max_order(void) { return kMaxOrder; }
 
 int sem_gll_nodes(int P, double* xi, double* w, double* V) { return gll_nodes(P, xi, w, V); }
@@ -457,7 +1069,8 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   if (x == y) return set_error(SEM_EINVAL, "x and y must not alias");
   if (d->dir_mode < SEM_DIR_NONE || d->dir_mode > SEM_DIR_REPLACE) return set_error(SEM_EINVAL, "bad dir_mode");
   if (d->dir_mode == SEM_DIR_REPLACE && !d->dir_val) return set_error(SEM_EINVAL, "SEM_DIR_REPLACE needs dir_val");
-  if (d->algo == SEM_ALGO_MFMA) return set_error(SEM_EUNSUPPORTED, "MFMA algorithm not built in this version");
+  if (d->algo < SEM_ALGO_AUTO || d->algo > 3) return set_error(SEM_EINVAL, "bad algo");
+  if (d->algo == SEM_ALGO_MFMA && h->P > 15) return set_error(SEM_EUNSUPPORTED, "MFMA path needs P <= 15");
   ApplyArgs a{};
   a.x = x;
   a.y = y;
@@ -493,7 +1106,34 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   a.ex_end = h->ex_end;
   a.dir_mode = d->dir_mode;
   a.sides = d->dir_sides;
+  a.n_local32 = static_cast<int>(std::min<int64_t>(h->n_local, 0x7fffffff));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (d->algo == 3) {
+    switch (h->P) {
+#define SEM_CCASE(PP) \
+  case PP:            \
+    return launch_apply_col_auto<PP>(a, h, s);
+      SEM_CCASE(1) SEM_CCASE(2) SEM_CCASE(3) SEM_CCASE(4) SEM_CCASE(5) SEM_CCASE(6) SEM_CCASE(7) SEM_CCASE(8)
+      SEM_CCASE(9) SEM_CCASE(10) SEM_CCASE(11) SEM_CCASE(12) SEM_CCASE(13) SEM_CCASE(14) SEM_CCASE(15) SEM_CCASE(16)
+#undef SEM_CCASE
+      default:
+        break;
+    }
+  }
+  const bool mfma = d->algo == SEM_ALGO_MFMA || (d->algo == SEM_ALGO_AUTO && h->P <= 15);
+  if (mfma && h->n_local >= (int64_t(1) << 31)) return set_error(SEM_EUNSUPPORTED, "MFMA path needs n_local < 2^31");
+  if (mfma) {
+    switch (h->P) {
+#define SEM_MCASE(PP) \
+  case PP:            \
+    return launch_apply_mfma_auto<PP>(a, h, s);
+      SEM_MCASE(1) SEM_MCASE(2) SEM_MCASE(3) SEM_MCASE(4) SEM_MCASE(5) SEM_MCASE(6) SEM_MCASE(7) SEM_MCASE(8)
+      SEM_MCASE(9) SEM_MCASE(10) SEM_MCASE(11) SEM_MCASE(12) SEM_MCASE(13) SEM_MCASE(14) SEM_MCASE(15)
+#undef SEM_MCASE
+      default:
+        break;
+    }
+  }
   switch (h->P) {
 #define SEM_CASE(PP) \
   case PP:           \

@@ -158,30 +158,42 @@ class SEMOperator:
 
     def tocsr(self):
         """Materialise as SciPy CSR for SciPy-only consumers (bmat / splu).  Not used by any
-        apply; the pattern is the reference's (zero element entries dropped, SEM.py:134)."""
+        apply.  Built like SEM.assemble (SEM.py:113-146): the nonzero element entries of every
+        term as unsummed (row, col, value) triplets, summed by one COO->CSR conversion, so the
+        sparsity pattern -- including entries that cancel to an explicit 0 -- is the reference's."""
         m = self.mesh
         w, Ks, Gs = self._tables()
-        mx, my = m.weights_1d()
-        Kx = _assembled_1d(Ks, m.P, m.ex_begin, m.ex_end, m.line_begin, m.line_end)
-        Ky = _assembled_1d(Ks, m.P, 0, m.ney, 0, m.NY - 1)
-        Gx = _assembled_1d(Gs, m.P, m.ex_begin, m.ex_end, m.line_begin, m.line_end)
-        Gy = _assembled_1d(Gs, m.P, 0, m.ney, 0, m.NY - 1)
-        Mx, My = sp.diags(mx), sp.diags(my)
-        A = sp.csr_matrix(self.shape)
-        if self.cM:
-            A = A + self.cM * (m.dx / 2) * (m.dy / 2) * sp.kron(Mx, My)
-        if self.cK:
-            A = A + self.cK * ((m.dy / m.dx) * sp.kron(Kx, My) + (m.dx / m.dy) * sp.kron(Mx, Ky))
+        P, NY = m.P, m.NY
+        xr = (m.ex_begin, m.ex_end, m.line_begin)
+        yr = (0, m.ney, 0)
+        W = np.diag(w)
         cX, cu, cY, cv, d = self._coeffs()
+        terms = []  # (coef, x-table, x-scale, y-table, y-scale, row weights)
+        if self.cM:
+            terms.append((self.cM, W, m.dx / 2, W, m.dy / 2, None))
+        if self.cK:
+            terms.append((self.cK, Ks, 2 / m.dx, W, m.dy / 2, None))
+            terms.append((self.cK, W, m.dx / 2, Ks, 2 / m.dy, None))
         if cX:
-            GX = (m.dy / 2) * sp.kron(Gx, My)
-            A = A + cX * (GX if cu is None else sp.diags(self._host(cu)) @ GX)
+            terms.append((cX, Gs, 1.0, W, m.dy / 2, cu))
         if cY:
-            GY = (m.dx / 2) * sp.kron(Mx, Gy)
-            A = A + cY * (GY if cv is None else sp.diags(self._host(cv)) @ GY)
+            terms.append((cY, W, m.dx / 2, Gs, 1.0, cv))
+        R, Cc, V = [], [], []
+        for coef, tx, sx, ty, sy, rw in terms:
+            ar, ac, av = _element_triplets(sx * tx, P, *xr)
+            br, bc, bv = _element_triplets(sy * ty, P, *yr)
+            rows = (ar[:, None] * NY + br[None, :]).ravel()
+            cols = (ac[:, None] * NY + bc[None, :]).ravel()
+            vals = coef * (av[:, None] * bv[None, :]).ravel()
+            if rw is not None:
+                vals = vals * self._host(rw)[rows]
+            R.append(rows), Cc.append(cols), V.append(vals)
         if d is not None:
-            A = A + sp.diags(self._host(d))
-        A = sp.csr_matrix(A)
+            idx = np.arange(self.shape[0])
+            R.append(idx), Cc.append(idx), V.append(self._host(d))
+        if not R:
+            return sp.csr_matrix(self.shape)
+        A = sp.coo_matrix((np.concatenate(V), (np.concatenate(R), np.concatenate(Cc))), shape=self.shape).tocsr()
         A.sum_duplicates()
         return A
 
@@ -193,16 +205,12 @@ class SEMOperator:
                 f"cK={self.cK} gx_terms={len(self.gx)} gy_terms={len(self.gy)} diag_terms={len(self.dg)}>")
 
 
-def _assembled_1d(table, P, e_lo, e_hi, g_lo, g_hi):
-    """1-D assembled matrix sum_e table over elements [e_lo, e_hi), zero table entries dropped."""
-    n = P + 1
+def _element_triplets(table, P, e_lo, e_hi, g_lo):
+    """Unsummed 1-D element entries (row, col, value) of `table` over elements [e_lo, e_hi),
+    zero table entries dropped as np.nonzero does in SEM.assemble (SEM.py:134)."""
     ii, kk = np.nonzero(table)
-    rows = np.concatenate([e * P + ii - g_lo for e in range(e_lo, e_hi)])
-    cols = np.concatenate([e * P + kk - g_lo for e in range(e_lo, e_hi)])
-    vals = np.tile(table[ii, kk], e_hi - e_lo)
-    size = g_hi - g_lo + 1
-    del n
-    return sp.coo_matrix((vals, (rows, cols)), shape=(size, size)).tocsr()
+    base = np.arange(e_lo, e_hi)[:, None] * P - g_lo
+    return (base + ii).ravel(), (base + kk).ravel(), np.tile(table[ii, kk], e_hi - e_lo)
 
 
 class RowRestricted:

@@ -70,8 +70,14 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
          (8, 17, 5), (9, 3, 4), (10, 2, 2), (11, 3, 1), (12, 5, 3), (13, 2, 3), (14, 1, 2), (15, 2, 2), (16, 3, 2)]
 
 
+ALGOS = [1, 2, 3]  # VALU two-phase, MFMA, VALU single-phase column kernel
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", CASES)
-def test_fused_apply_vs_oracle(gpu, P, nex, ney):
+def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo):
+    if algo == 2 and P > 15:
+        pytest.skip("MFMA path covers P <= 15")
     from sem_amd.device import get_mesh
     Lx, Ly = 1.3, 0.7
     dx, dy = Lx / nex, Ly / ney
@@ -82,21 +88,22 @@ def test_fused_apply_vs_oracle(gpu, P, nex, ney):
     X, U, V, A, B = (mesh.to_device(t) for t in (x, u, v, a, b))
     ref = {k: O.apply_matrix_free(P, nex, ney, dx, dy, x, **kw) for k, kw in
            {"M": dict(c_mass=1.0), "K": dict(c_stiff=1.0), "Gx": dict(c_gradx=1.0), "Gy": dict(c_grady=1.0)}.items()}
-    assert rel(mesh.apply(X, c_mass=1.0), ref["M"]) < TOL
-    assert rel(mesh.apply(X, c_stiff=1.0), ref["K"]) < TOL
-    assert rel(mesh.apply(X, c_gradx=1.0), ref["Gx"]) < TOL
-    assert rel(mesh.apply(X, c_grady=1.0), ref["Gy"]) < TOL
+    assert rel(mesh.apply(X, c_mass=1.0, algo=algo), ref["M"]) < TOL
+    assert rel(mesh.apply(X, c_stiff=1.0, algo=algo), ref["K"]) < TOL
+    assert rel(mesh.apply(X, c_gradx=1.0, algo=algo), ref["Gx"]) < TOL
+    assert rel(mesh.apply(X, c_grady=1.0, algo=algo), ref["Gy"]) < TOL
     # everything at once: 0.5 M + K + 40 u.Gx + 40 v.Gy + 3 (a.b + u.v) + 2 y_in
     yin = r.uniform(-1, 1, N)
     Y = mesh.to_device(yin)
     mesh.apply(X, Y, c_mass=0.5, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, c_extra=3.0, ea=A, eb=B,
-               ec=U, ed=V, c_acc=2.0)
+               ec=U, ed=V, c_acc=2.0, algo=algo)
     want = 0.5 * ref["M"] + ref["K"] + 40 * u * ref["Gx"] + 40 * v * ref["Gy"] + 3 * (a * b + u * v) + 2 * yin
     assert rel(Y, want) < TOL
 
 
-@pytest.mark.parametrize("P,nex,ney", [(4, 4, 4), (8, 6, 5), (12, 3, 4)])
-def test_dirichlet_rows(gpu, P, nex, ney):
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("P,nex,ney", [(4, 4, 4), (8, 6, 5), (12, 3, 4), (8, 40, 33)])
+def test_dirichlet_rows(gpu, P, nex, ney, algo):
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.0 / ney)
@@ -111,19 +118,36 @@ def test_dirichlet_rows(gpu, P, nex, ney):
                        (15, (gx == 0) | (gx == NX - 1) | (gy == 0) | (gy == NY - 1))):
         want = base.copy()
         want[sel] = x[sel] - g[sel]
-        y1 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides, dir_val=G)
+        y1 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides, dir_val=G, algo=algo)
         y2 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_IDENTITY,
-                        dir_mask=torch.as_tensor(sel.astype(np.uint8), device=mesh.device), dir_val=G)
+                        dir_mask=torch.as_tensor(sel.astype(np.uint8), device=mesh.device), dir_val=G, algo=algo)
         assert rel(y1, want) < TOL and torch.equal(y1, y2)
         want[sel] = g[sel]
-        y3 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_REPLACE, dir_sides=sides, dir_val=G)
+        y3 = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_REPLACE, dir_sides=sides, dir_val=G, algo=algo)
         assert rel(y3, want) < TOL
     # an irregular mask (as np.isclose could produce) is honoured row by row
     sel = r.uniform(size=N) < 0.1
     want = base.copy()
     want[sel] = x[sel]
     y = mesh.apply(X, c_stiff=1.0, dir_mode=_lib.DIR_IDENTITY,
-                   dir_mask=torch.as_tensor(sel.astype(np.uint8), device=mesh.device))
+                   dir_mask=torch.as_tensor(sel.astype(np.uint8), device=mesh.device), algo=algo)
+    assert rel(y, want) < TOL
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("P,nex,ney", [(8, 130, 67), (12, 70, 45), (4, 300, 211)])
+def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo):
+    """Meshes big enough for the large-tile / persistent launch configurations."""
+    from sem_amd.device import get_mesh
+    dx, dy = 1.0 / nex, 2.0 / ney
+    mesh = get_mesh(P, nex, ney, dx, dy)
+    N = mesh.n_local
+    r = np.random.default_rng(nex + ney)
+    x, u, v = (r.uniform(-1, 1, N) for _ in range(3))
+    want = (O.apply_matrix_free(P, nex, ney, dx, dy, x, c_stiff=1.0)
+            + 40 * O.apply_matrix_free(P, nex, ney, dx, dy, x, c_gradx=1.0, c_grady=1.0, cu=u, cv=v))
+    X, U, V = (mesh.to_device(t) for t in (x, u, v))
+    y = mesh.apply(X, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, algo=algo)
     assert rel(y, want) < TOL
 
 
@@ -179,10 +203,13 @@ def test_full_size_properties(gpu, P, ne):
     assert abs(torch.dot(z, Kx).item() - torch.dot(x, Kz).item()) < 1e-11 * scale * N ** 0.5  # symmetry
     M1 = mesh.apply(ones, c_mass=1.0)
     assert abs(M1.sum().item() - 1.0) < 1e-12                                         # area of [0,1]^2
-    xs = torch.as_tensor(np.repeat(np.asarray(__import__("sem_amd").SEM.global_nodes_1d(P, ne, d)), mesh.NY),
-                         device=mesh.device)
-    assert (mesh.apply(xs, c_gradx=1.0) - M1).abs().max().item() < 1e-13 * M1.abs().max().item()  # d(x)/dx = 1
-    assert mesh.apply(xs, c_grady=1.0).abs().max().item() < 1e-13 * M1.abs().max().item()          # d(x)/dy = 0
+    from sem_amd import GLL, SEM
+    xs = torch.as_tensor(np.repeat(SEM.global_nodes_1d(P, ne, d), mesh.NY), device=mesh.device)
+    # rounding scale of G applied to O(1) data: (d/2) * max w * max_i sum_k |G_s[i,k]| * 2 (shared lines)
+    w = GLL.standard_nodes(P)[1]
+    gscale = d / 2 * w.max() * 2 * np.abs(GLL.standard_gradient_matrix(P)).sum(axis=1).max()
+    assert (mesh.apply(xs, c_gradx=1.0) - M1).abs().max().item() < 1e-14 * gscale     # d(x)/dx = 1
+    assert mesh.apply(xs, c_grady=1.0).abs().max().item() < 1e-14 * gscale            # d(x)/dy = 0
     lin = mesh.apply(2.0 * x - 3.0 * z, c_stiff=1.0)
     assert (lin - (2.0 * Kx - 3.0 * Kz)).abs().max().item() < 1e-12 * scale            # linearity
     assert torch.equal(Kx, mesh.apply(x, c_stiff=1.0))                                # deterministic
