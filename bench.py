@@ -229,7 +229,7 @@ def main():
                                                                                          world == 1)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
-                     "kernel": "sem::apply_tp_valu<8>", "bytes_per_launch": bytes_launch,
+                     "kernel": mesh.kernel_name(), "bytes_per_launch": bytes_launch,
                      "flops_per_launch": flops_launch, "kernel_us": kern_s * 1e6, "kernel_us_isolated": iso_us,
                      "fp64_tflops": flops_launch / kern_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
     }
@@ -244,7 +244,8 @@ def main():
         kb = sb / 20
         bb = 32.0 * big.n_local
         wl = f"cd_matvec_{args.hbm_ne}x{args.hbm_ne}_P{P}"
-        out["roofline_hbm"] = {"workload": wl, "dofs": big.n_local, "value": big.n_local / kb, "unit": "DOF-updates/s",
+        out["roofline_hbm"] = {"workload": wl, "kernel": big.kernel_name(), "dofs": big.n_local,
+                               "value": big.n_local / kb, "unit": "DOF-updates/s",
                                "bound": "hbm", "achieved": bb / kb / 1e9, "peak": HBM_PEAK_GBS, "unit_bw": "GB/s",
                                "frac": bb / kb / 1e9 / HBM_PEAK_GBS, "traffic": load_pmc(wl), "kernel_us": kb * 1e6}
         del Tb, ub, vb, yb

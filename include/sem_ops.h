@@ -55,7 +55,14 @@ enum sem_dir_mode {
   SEM_DIR_REPLACE = 2   /* y[p] = dir_val[p]                                            */
 };
 
-enum sem_algo { SEM_ALGO_AUTO = 0, SEM_ALGO_VALU = 1, SEM_ALGO_MFMA = 2 };
+/* Kernel selection.  All compute the same operator (parity-tested against each other and the
+ * oracle); AUTO picks by mesh size from MI355X measurements. */
+enum sem_algo {
+  SEM_ALGO_AUTO = 0,
+  SEM_ALGO_VALU = 1,   /* two-phase VALU tile kernel (x and y contractions in separate passes)   */
+  SEM_ALGO_MFMA = 2,   /* fp64 MFMA (v_mfma_f64_16x16x4_f64) element-block contractions, P <= 15 */
+  SEM_ALGO_COLUMN = 3  /* single-phase VALU column kernel                                         */
+};
 
 typedef struct sem_handle sem_handle;
 
@@ -137,6 +144,9 @@ int sem_get_info(const sem_handle* h, sem_info* out);
 /* ---- device operators ------------------------------------------------- */
 /* Fused matrix-free operator apply (see sem_apply_desc).  x, y: n_local doubles. */
 int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y, void* stream);
+
+/* Name of the kernel sem_apply launches for this handle and algorithm (for profiles / reports). */
+int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len);
 
 /* SEM.scatter (SEM.py:149-167): u_e[m][n][i][j] = u[global_index(m,n,i,j)] for the
  * local elements; u_e has (ex_end-ex_begin)*ney*(P+1)^2 doubles. */

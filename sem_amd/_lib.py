@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
 DIR_NONE, DIR_IDENTITY, DIR_REPLACE = 0, 1, 2
-ALGO_AUTO, ALGO_VALU, ALGO_MFMA = 0, 1, 2
+ALGO_AUTO, ALGO_VALU, ALGO_MFMA, ALGO_COLUMN = 0, 1, 2, 3
 
 _dp = C.POINTER(C.c_double)
 _i64p = C.POINTER(C.c_int64)
@@ -52,6 +52,7 @@ _SIGS = {
     "sem_destroy": (C.c_int, [C.c_void_p]),
     "sem_get_info": (C.c_int, [C.c_void_p, C.POINTER(SemInfo)]),
     "sem_apply": (C.c_int, [C.c_void_p, C.POINTER(SemApplyDesc), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sem_kernel_name": (C.c_int, [C.c_void_p, C.c_int, C.c_char_p, C.c_int]),
     "sem_gather_elements": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sem_dss": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sem_eval_interpolation": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,

@@ -850,10 +850,9 @@ static int launch_apply_col_auto(const ApplyArgs& args, const sem_handle* h, hip
   }();
   constexpr int RS = (P % 4 == 0) ? 4 : (P % 2 == 0 ? 2 : 1);
   constexpr int BYs = 64 / RS > 16 ? 64 / RS : 16;
-  const long long n = h->n_local;
-  if (force == 2 || (force == 0 && n >= (1LL << 23))) return launch_apply_col<P, 4, 64, 1>(args, h, s);
-  if (force == 3) return launch_apply_col<P, 2, 64, 1>(args, h, s);
-  return launch_apply_col<P, 2, BYs, RS>(args, h, s);
+  if (force == 1) return launch_apply_col<P, 2, BYs, RS>(args, h, s);
+  if (force == 2) return launch_apply_col<P, 4, 64, 1>(args, h, s);
+  return launch_apply_col<P, 2, 64, 1>(args, h, s);
 }
 
 // --------------------------------------------------------------------------- gather / DSS
@@ -1069,7 +1068,7 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   if (x == y) return set_error(SEM_EINVAL, "x and y must not alias");
   if (d->dir_mode < SEM_DIR_NONE || d->dir_mode > SEM_DIR_REPLACE) return set_error(SEM_EINVAL, "bad dir_mode");
   if (d->dir_mode == SEM_DIR_REPLACE && !d->dir_val) return set_error(SEM_EINVAL, "SEM_DIR_REPLACE needs dir_val");
-  if (d->algo < SEM_ALGO_AUTO || d->algo > 3) return set_error(SEM_EINVAL, "bad algo");
+  if (d->algo < SEM_ALGO_AUTO || d->algo > SEM_ALGO_COLUMN) return set_error(SEM_EINVAL, "bad algo");
   if (d->algo == SEM_ALGO_MFMA && h->P > 15) return set_error(SEM_EUNSUPPORTED, "MFMA path needs P <= 15");
   ApplyArgs a{};
   a.x = x;
@@ -1108,7 +1107,11 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   a.sides = d->dir_sides;
   a.n_local32 = static_cast<int>(std::min<int64_t>(h->n_local, 0x7fffffff));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (d->algo == 3) {
+  // AUTO: measured on MI355X (tools/kbench.py) -- the MFMA tile kernel wins on meshes that
+  // leave the chip latency-bound (< 2M DOFs), the single-phase column kernel on larger ones.
+  const bool small = h->n_local < (int64_t(1) << 21);
+  const bool use_col = d->algo == SEM_ALGO_COLUMN || (d->algo == SEM_ALGO_AUTO && !(small && h->P <= 15));
+  if (use_col) {
     switch (h->P) {
 #define SEM_CCASE(PP) \
   case PP:            \
@@ -1120,7 +1123,7 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
         break;
     }
   }
-  const bool mfma = d->algo == SEM_ALGO_MFMA || (d->algo == SEM_ALGO_AUTO && h->P <= 15);
+  const bool mfma = d->algo == SEM_ALGO_MFMA || d->algo == SEM_ALGO_AUTO;
   if (mfma && h->n_local >= (int64_t(1) << 31)) return set_error(SEM_EUNSUPPORTED, "MFMA path needs n_local < 2^31");
   if (mfma) {
     switch (h->P) {
@@ -1144,6 +1147,27 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
     default:
       return set_error(SEM_EUNSUPPORTED, "polynomial order outside compiled range");
   }
+}
+
+int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
+  if (!h || !buf || len < 1) return set_error(SEM_EINVAL, "bad arguments");
+  const bool small = h->n_local < (int64_t(1) << 21);
+  std::string name;
+  const int P = h->P;
+  if (algo == SEM_ALGO_COLUMN || (algo == SEM_ALGO_AUTO && !(small && P <= 15))) {
+    name = "sem::apply_tp_col<" + std::to_string(P) + ", 2, 64, 1>";
+  } else if ((algo == SEM_ALGO_MFMA || algo == SEM_ALGO_AUTO) && P <= 15) {
+    const int TL = std::max(1, 32 / P), TS = std::max(1, 16 / P);
+    const long long big = static_cast<long long>((h->ex_end - h->ex_begin + TL - 1) / TL) * ((h->ney + TL - 1) / TL);
+    name = big >= 4 * 256 ? "sem::apply_tp_mfma<" + std::to_string(P) + ", " + std::to_string(TL) + ", " +
+                                std::to_string(TL) + ", 4>"
+                          : "sem::apply_tp_mfma<" + std::to_string(P) + ", " + std::to_string(TS) + ", " +
+                                std::to_string(TS) + ", 2>";
+  } else {
+    name = "sem::apply_tp_valu<" + std::to_string(P) + ">";
+  }
+  std::snprintf(buf, static_cast<size_t>(len), "%s", name.c_str());
+  return SEM_OK;
 }
 
 int sem_gather_elements(sem_handle* h, const double* u, double* ue, void* stream) {

@@ -96,6 +96,11 @@ class Mesh:
         _lib.check(self._lib.sem_apply(self._h, C.byref(d), _ptr(x), _ptr(y), self.stream_ptr(stream)))
         return y
 
+    def kernel_name(self, algo=_lib.ALGO_AUTO):
+        buf = C.create_string_buffer(128)
+        _lib.check(self._lib.sem_kernel_name(self._h, int(algo), buf, 128))
+        return buf.value.decode()
+
     def gather_elements(self, u, out=None, stream=None):
         """SEM.scatter (SEM.py:149-167) on the device: u[N] -> u_e[m, n, i, j]."""
         u = self._vec(u, "u")

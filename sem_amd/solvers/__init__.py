@@ -1,5 +1,6 @@
 """Solver counterparts (callers of the operator layer): the operator applies of
 Solvers/ConvectionDiffusion_Solver.py and Solvers/NavierStokes_Solver.py on the GPU."""
 from .convection_diffusion import ConvectionDiffusionSolver  # noqa: F401
+from .navier_stokes import NavierStokesSolver  # noqa: F401
 
-__all__ = ["ConvectionDiffusionSolver"]
+__all__ = ["ConvectionDiffusionSolver", "NavierStokesSolver"]

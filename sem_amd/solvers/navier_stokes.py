@@ -1,0 +1,244 @@
+"""Navier-Stokes solver counterpart on the device operators.
+
+Mirrors Solvers/NavierStokes_Solver.py:10-306 (same constructor, same private
+methods the OpenMDAO component calls, same errors).  The operator applies run on
+the GPU as fused launches:
+
+  * `_get_residuals`  (:93-121): res_u = Sys u + G_x p, res_v = Sys v + G_y p - Gr/Re M T,
+    res_cont = G_x u + G_y v, with the reference's Dirichlet / pinned-pressure /
+    artificial-Neumann (`K[mask,:] @ p`) rows -- 7 fused launches, no host round trip.
+  * `_calc_jacobians` (:123-136): Re diag(G_x u) ... as closed-form operators.
+  * `_get_dresiduals` (:138-160): the velocity Jacobian blocks applied matrix-free.
+
+`_get_update` keeps the reference's algorithm: the 2N x 2N velocity Jacobian is
+materialised (`.tocsr()`) and factorised with SuperLU on the host, and the
+pressure Schur complement is solved by LGMRES with the mass-diagonal
+preconditioner (NavierStokes_Solver.py:162-236).  Replacing the direct solver is
+a later step.
+"""
+import time
+
+import numpy as np
+import scipy.sparse as sp_sparse
+import scipy.sparse.linalg as linalg
+import torch
+
+from .. import SEM, _lib
+from ..device import get_mesh
+from .convection_diffusion import DirichletRows
+
+
+class NavierStokesSolver:
+    def __init__(self, L_x: float, L_y: float, Re: float, Gr: float, P: int, N_ex: int, N_ey: int,
+                 v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
+                 mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter']):  # noqa: B006
+        self._iprint = iprint
+        self._Re, self._Gr = Re, Gr
+        if self._Re == 0 and self._Gr != 0:
+            raise ValueError('Cannot have Re == 0 and Gr != 0')
+        self._Gr_over_Re = self._Gr / self._Re if self._Re != 0 else 0.
+        self._mtol, self._mtol_newton = mtol, mtol_newton
+        self._L_x, self._L_y = L_x, L_y
+        self._P, self._N_ex, self._N_ey = P, N_ex, N_ey
+        dx, dy = L_x / N_ex, L_y / N_ey
+        self.points = SEM.global_nodes(P, N_ex, N_ey, L_x / N_ex, L_y / N_ey)
+        self.points_e = SEM.element_nodes(P, N_ex, N_ey, dx, dy)
+        self.N = (N_ex * P + 1) * (N_ey * P + 1)
+        self._mesh = m = get_mesh(P, N_ex, N_ey, dx, dy)
+
+        self._M = SEM.global_mass_matrix(P, N_ex, N_ey, dx, dy)
+        self._K = SEM.global_stiffness_matrix(P, N_ex, N_ey, dx, dy)
+        self._G_x, self._G_y = SEM.global_gradient_matrices(P, N_ex, N_ey, dx, dy)
+        self._C_x, self._C_y = SEM.global_convection_matrices(P, N_ex, N_ey, dx, dy)
+        self._Sys = None
+        self._Jac_u_u = self._Jac_u_v = self._Jac_v_u = self._Jac_v_v = None
+
+        # Dirichlet values and masks, exactly as NavierStokes_Solver.py:78-94 builds them
+        x, y = self.points
+        du, dv, dpp = np.full(self.N, np.nan), np.full(self.N, np.nan), np.full(self.N, np.nan)
+        dv[np.isclose(x, 0)] = v_W
+        du[np.isclose(x, 0)] = 0
+        dv[np.isclose(x, self._L_x)] = v_E
+        du[np.isclose(x, self._L_x)] = 0
+        du[np.isclose(y, 0)] = u_S
+        dv[np.isclose(y, 0)] = 0
+        du[np.isclose(y, self._L_y)] = u_N
+        dv[np.isclose(y, self._L_y)] = 0
+        dpp[int(self.N / 2)] = 0
+        self._dirichlet_u, self._dirichlet_v, self._dirichlet_p = du, dv, dpp
+        self._mask_bound = ~np.isnan(du)
+        self._mask_dir_p = ~np.isnan(dpp)
+        all_sides = _lib.SIDE_W | _lib.SIDE_E | _lib.SIDE_S | _lib.SIDE_N
+        self._dir = DirichletRows(m, self._mask_bound, all_sides)
+        self._dval_u = m.to_device(np.where(self._mask_bound, du, 0.0))
+        self._dval_v = m.to_device(np.where(self._mask_bound, dv, 0.0))
+        self._pidx = torch.as_tensor(np.nonzero(self._mask_dir_p)[0], device=m.device)
+        self._dval_p = m.to_device(np.where(self._mask_dir_p, dpp, 0.0))
+
+    # ------------------------------------------------------------------ helpers
+    def _dev(self, a):
+        return None if a is None else self._mesh.to_device(a)
+
+    @staticmethod
+    def _out(t, like):
+        return t if isinstance(like, torch.Tensor) else t.cpu().numpy()
+
+    def _sys_kw(self, Sys):
+        cX, cu, cY, cv, d = Sys._coeffs()
+        return dict(c_stiff=Sys.cK, c_mass=Sys.cM, c_gradx=cX, cu=cu, c_grady=cY, cv=cv)
+
+    def _continuity(self, u, v, p, pdir=None):
+        """G_x u + G_y v with the artificial Neumann rows (K p)[mask_bound] fused into the launch
+        (SEM_DIR_REPLACE) and the pinned-pressure row; row order as the reference: residual
+        (:119-122) pins first and the Neumann rows win, dres (:160-161) the pinned row wins."""
+        m = self._mesh
+        kp = m.apply(p, c_stiff=1.0)
+        r = m.apply(u, c_gradx=1.0)
+        r = m.apply(v, r, c_grady=1.0, c_acc=1.0, dir_mode=_lib.DIR_REPLACE, dir_val=kp, **self._dir.kw())
+        if pdir is None:
+            r[self._pidx] = p[self._pidx]
+        elif not self._mask_bound[self._pidx.item()]:
+            r[self._pidx] = p[self._pidx] - pdir[self._pidx]
+        return r
+
+    # ------------------------------------------------------------------ reference methods
+    def _get_residuals(self, u, v, p, T):
+        """NavierStokes_Solver.py:93-121."""
+        m = self._mesh
+        U, V, Pp, Tt = self._dev(u), self._dev(v), self._dev(p), self._dev(T)
+        Conv = self._Re * (SEM.tensordot(self._C_x, U, (1, 0)) + SEM.tensordot(self._C_y, V, (1, 0)))
+        self._Sys = self._K + Conv
+        kw = self._sys_kw(self._Sys)
+        # res_u = Sys u + G_x p, Dirichlet rows u - u_dir
+        ru = m.apply(Pp, c_gradx=1.0)
+        ru = m.apply(U, ru, c_acc=1.0, dir_mode=_lib.DIR_IDENTITY, dir_val=self._dval_u, **kw, **self._dir.kw())
+        # res_v = Sys v + G_y p - Gr/Re M T
+        rv = m.apply(Pp, c_grady=1.0)
+        rv = m.apply(Tt, rv, c_mass=-self._Gr_over_Re, c_acc=1.0)
+        rv = m.apply(V, rv, c_acc=1.0, dir_mode=_lib.DIR_IDENTITY, dir_val=self._dval_v, **kw, **self._dir.kw())
+        rc = self._continuity(U, V, Pp, pdir=self._dval_p)
+        return self._out(ru, u), self._out(rv, u), self._out(rc, u)
+
+    def _calc_jacobians(self, u, v):
+        """NavierStokes_Solver.py:123-136."""
+        U, V = self._dev(u), self._dev(v)
+        Re = self._Re
+        self._Jac_u_u = self._Sys + Re * SEM.tensordot(self._C_x, U, (2, 0))
+        self._Jac_v_v = self._Sys + Re * SEM.tensordot(self._C_y, V, (2, 0))
+        self._Jac_u_v = Re * SEM.tensordot(self._C_y, U, (2, 0))
+        self._Jac_v_u = Re * SEM.tensordot(self._C_x, V, (2, 0))
+
+    def _get_dresiduals(self, du, dv, dp, dT=None):
+        """NavierStokes_Solver.py:138-160."""
+        m = self._mesh
+        DU, DV, DP = self._dev(du), self._dev(dv), self._dev(dp)
+        kw = self._sys_kw(self._Sys)
+        juu = self._Jac_u_u._coeffs()[4]   # Re G_x u  (the diagonal part beyond Sys)
+        jvv = self._Jac_v_v._coeffs()[4]   # Re G_y v
+        juv = self._Jac_u_v._coeffs()[4]   # Re G_y u
+        jvu = self._Jac_v_u._coeffs()[4]   # Re G_x v
+        # dres_u = Sys du + (Re G_x u).du + (Re G_y u).dv + G_x dp
+        ru = m.apply(DP, c_gradx=1.0)
+        ru = m.apply(DU, ru, c_acc=1.0, c_extra=1.0, ea=juu, eb=DU, ec=juv, ed=DV, dir_mode=_lib.DIR_IDENTITY,
+                     **kw, **self._dir.kw())
+        # dres_v = (Re G_x v).du + Sys dv + (Re G_y v).dv + G_y dp - Gr/Re M dT
+        rv = m.apply(DP, c_grady=1.0)
+        if dT is not None:
+            rv = m.apply(self._dev(dT), rv, c_mass=-self._Gr_over_Re, c_acc=1.0)
+        rv = m.apply(DV, rv, c_acc=1.0, c_extra=1.0, ea=jvu, eb=DU, ec=jvv, ed=DV, dir_mode=_lib.DIR_IDENTITY,
+                     **kw, **self._dir.kw())
+        # dres_cont = G_x du + G_y dv; [mask_bound] = (K dp)[mask_bound]; [mask_p] = dp[mask_p]
+        rc = self._continuity(DU, DV, DP)
+        return self._out(ru, du), self._out(rv, du), self._out(rc, du)
+
+    def _get_update(self, dres_u, dres_v, dres_cont, du0=None, dv0=None, dp0=None):
+        """Velocity LU + pressure Schur LGMRES (NavierStokes_Solver.py:162-236)."""
+        host = lambda a: a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)  # noqa: E731
+        dres_u, dres_v, dres_cont = host(dres_u), host(dres_v), host(dres_cont)
+        tStart = time.perf_counter()
+        mask = np.hstack((self._mask_bound,) * 2)
+        Jac_velo = sp_sparse.bmat([[self._Jac_u_u.tocsr(), self._Jac_u_v.tocsr()],
+                                   [self._Jac_v_u.tocsr(), self._Jac_v_v.tocsr()]], format='lil')
+        Jac_velo[mask, :] = 0
+        Jac_velo[mask, mask] = 1
+        Jac_velo = Jac_velo.tocsc()
+        Jac_velo_lu = linalg.splu(Jac_velo)
+        if 'LU_suc' in self._iprint:
+            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec '
+                  f'with fill factor {Jac_velo_lu.nnz/Jac_velo.nnz:0.1f}')
+
+        def solve_jac_velo(a, b):
+            return np.split(Jac_velo_lu.solve(np.hstack((a, b))), 2)
+
+        Z = np.zeros(self.N)
+        b_schur = dres_cont - self._get_dresiduals(*solve_jac_velo(dres_u, dres_v), Z)[2]
+
+        def schur_mv(dp):
+            schur_mv.fCount += 1
+            f_x, f_y = solve_jac_velo(*self._get_dresiduals(Z, Z, np.ascontiguousarray(dp).ravel())[:2])
+            return self._get_dresiduals(-f_x, -f_y, np.ascontiguousarray(dp).ravel())[2]
+
+        schur_mv.fCount = 0
+        schur_LO = linalg.LinearOperator((self.N,) * 2, schur_mv, dtype=float)
+        Mdiag = self._M.diagonal()
+
+        def precon_mv(c):
+            z = c / Mdiag
+            z[self._mask_dir_p] = c[self._mask_dir_p]
+            return z
+
+        precon_LO = linalg.LinearOperator((self.N,) * 2, precon_mv, dtype=float)
+
+        def print_res(xk):
+            print_res.iterCount += 1
+            if 'LGMRES_iter' in self._iprint:
+                print(f'NavierStokes LGMRES: {print_res.iterCount}\t{np.linalg.norm(schur_LO.matvec(xk) - b_schur)}')
+
+        print_res.iterCount = 0
+        dp, info = linalg.lgmres(A=schur_LO, b=b_schur, M=precon_LO, x0=dp0, atol=self._mtol * np.sqrt(self.N),
+                                 rtol=0, inner_m=int(self.N * 0.3), callback=print_res)
+        if info != 0:
+            raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {info} iterations')
+        if 'LGMRES_suc' in self._iprint:
+            res = np.linalg.norm(schur_LO.matvec(dp) - b_schur, ord=np.inf)
+            print(f'NavierStokes LGMRES: Converged in {schur_mv.fCount} evaluations with max-norm {res}')
+        b_u, b_v = self._get_dresiduals(Z, Z, dp)[:2]
+        du, dv = solve_jac_velo(dres_u - b_u, dres_v - b_v)
+        return du, dv, dp
+
+    def _get_solution(self, T, u0=None, v0=None, p0=None):
+        """Newton iteration (NavierStokes_Solver.py:238-270)."""
+        u = u0 if u0 is not None else np.zeros(self.N)
+        v = v0 if v0 is not None else np.zeros(self.N)
+        p = p0 if p0 is not None else np.zeros(self.N)
+        self._k = 0
+        while True:
+            res_u, res_v, res_cont = self._get_residuals(u, v, p, T)
+            norm = np.linalg.norm((res_u, res_v, res_cont), ord=2)
+            if 'NEWTON_iter' in self._iprint:
+                print(f'NavierStokes NEWTON: {self._k}\t{norm}')
+            if norm <= self._mtol_newton * np.sqrt(self.N * 3):
+                if 'NEWTON_suc' in self._iprint:
+                    print(f'NavierStokes NEWTON: Converged in {self._k} iterations'
+                          f' with max-norm {np.linalg.norm((res_u, res_v, res_cont), ord=np.inf)}')
+                break
+            self._calc_jacobians(u, v)
+            du, dv, dp = self._get_update(-res_u, -res_v, -res_cont)
+            u = u + du
+            v = v + dv
+            p = p + dp
+            self._k += 1
+        return u, v, p
+
+    def _get_vector(self, f_func):
+        return f_func(self.points[0], self.points[1])
+
+    def _get_interpol(self, f, points_plot):
+        f_e = SEM.scatter(f, self._P, self._N_ex, self._N_ey)
+        return SEM.eval_interpolation(f_e, self.points_e, points_plot)
+
+    def run(self, T_func, points_plot):
+        T = self._get_vector(T_func)
+        u, v, p = self._get_solution(T)
+        return self._get_interpol(u, points_plot), self._get_interpol(v, points_plot), self._get_interpol(p,
+                                                                                                         points_plot)

@@ -1,0 +1,115 @@
+"""World-size-2 gloo test (CPU) of the element-strip decomposition and the interface
+exchange protocol of sem_amd.parallel.InterfaceExchange.
+
+The device kernels cannot run here, so each rank's local apply is the oracle's
+matrix-free apply on its own strip of elements (the same partial sums the kernel
+forms: only local elements contribute, Dirichlet rows of an interface line are
+written by its right-hand owner), and the pack/unpack kernels are replaced by a
+CPU test double with their documented slot semantics.  The product's partition,
+slot assignment and all-reduce protocol run unchanged."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class StripDouble:
+    """CPU stand-in for sem_amd.device.Mesh with the kernels' partition semantics."""
+
+    def __init__(self, P, nex, ney, dx, dy, eb, ee):
+        self.P, self.nex, self.ney, self.dx, self.dy, self.eb, self.ee = P, nex, ney, dx, dy, eb, ee
+        self.NY = ney * P + 1
+        self.line_begin, self.line_end = eb * P, ee * P
+        self.n_local = (self.line_end - self.line_begin + 1) * self.NY
+        self.dof_begin = self.line_begin * self.NY
+        self.device = torch.device("cpu")
+
+    def apply(self, x, sides_mask_global, g):
+        from oracle import sem_oracle as O
+        y = O.apply_matrix_free(self.P, self.ee - self.eb, self.ney, self.dx, self.dy, x, c_stiff=1.0)
+        lines = np.arange(self.line_begin, self.line_end + 1).repeat(self.NY)
+        m = sides_mask_global[self.dof_begin:self.dof_begin + self.n_local]
+        owner = ~((lines == self.line_end) & (self.ee < self.nex))
+        y[m & owner] = x[m & owner] - g[m & owner]
+        y[m & ~owner] = 0.0
+        return torch.from_numpy(y)
+
+    def interface_pack(self, y, bounds, buf):
+        r = bounds.index(self.eb)
+        left, right = (r - 1 if r > 0 else -1), (r if r < len(bounds) - 2 else -1)
+        buf.zero_()
+        if left >= 0:
+            buf[left * self.NY:(left + 1) * self.NY] = y[:self.NY]
+        if right >= 0:
+            buf[right * self.NY:(right + 1) * self.NY] = y[-self.NY:]
+
+    def interface_unpack(self, buf, bounds, y):
+        r = bounds.index(self.eb)
+        left, right = (r - 1 if r > 0 else -1), (r if r < len(bounds) - 2 else -1)
+        if left >= 0:
+            y[:self.NY] = buf[left * self.NY:(left + 1) * self.NY]
+        if right >= 0:
+            y[-self.NY:] = buf[right * self.NY:(right + 1) * self.NY]
+
+
+def _worker(rank, world, port, P, nex, ney, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sem_oracle as O
+        from sem_amd.parallel import StripPartition
+        dx, dy = 1.0 / nex, 1.0 / ney
+        N = (nex * P + 1) * (ney * P + 1)
+        x = np.random.default_rng(3).uniform(-1, 1, N)
+        g = np.random.default_rng(4).uniform(-1, 1, N)
+        NX, NY = nex * P + 1, ney * P + 1
+        gx = np.arange(N) // NY
+        mask = (gx == 0) | (gx == NX - 1)
+        part = StripPartition(nex, world)
+        eb, ee = part.local_range(rank)
+        mesh = StripDouble(P, nex, ney, dx, dy, eb, ee)
+        sl = slice(mesh.dof_begin, mesh.dof_begin + mesh.n_local)
+        y = mesh.apply(x[sl], mask, g[sl])
+        y = part.exchanger(mesh, dist)(y)
+        want = O.apply_matrix_free(P, nex, ney, dx, dy, x, c_stiff=1.0)
+        want[mask] = x[mask] - g[mask]
+        err = np.abs(y.numpy() - want[sl]).max() / np.abs(want).max()
+        q.put((rank, float(err)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,P,nex,ney", [(2, 4, 6, 5), (2, 8, 9, 4), (3, 5, 7, 3)])
+def test_interface_exchange_gloo(world, P, nex, ney):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, nex, ney, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(e < 1e-13 for e in res.values()), res
+
+
+def test_partition_bounds():
+    from sem_amd.parallel import StripPartition
+    p = StripPartition(10, 3)
+    assert p.bounds == [0, 4, 7, 10]
+    assert [p.slots(r) for r in range(3)] == [(-1, 0), (0, 1), (1, -1)]
+    with pytest.raises(ValueError):
+        StripPartition(2, 3)

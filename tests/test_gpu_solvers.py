@@ -1,0 +1,70 @@
+"""Solver counterparts (callers of the operator layer) against the reference's own
+solver outputs (tests/golden/cd.npz, ns.npz)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-13
+CD_KEYS = {"P4_4x4": (4, 4, 4), "P4_3x2": (4, 3, 2), "P8_8x8": (8, 8, 8)}
+
+
+def rel(a, b):
+    return np.abs(np.asarray(a) - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+@pytest.mark.parametrize("key", list(CD_KEYS))
+def test_cd_residuals_and_jacobians(gpu, key):
+    from sem_amd.solvers import ConvectionDiffusionSolver
+    g = golden("cd.npz")
+    P, nex, ney = CD_KEYS[key]
+    Lx, Ly = g[key + "_LxLy"]
+    bc = {k: float(v) for k, v in zip(("T_W", "T_E", "T_S", "T_N"), g[key + "_bc"]) if not np.isnan(v)}
+    cd = ConvectionDiffusionSolver(float(Lx), float(Ly), 40.0, P, nex, ney, **bc)
+    assert np.array_equal(cd._mask_dir, g[key + "_mask_dir"])
+    assert rel(cd._get_residuals(g[key + "_T"], g[key + "_u"], g[key + "_v"]), g[key + "_res"]) < TOL
+    cd._calc_jacobians(g[key + "_T"])
+    assert rel(cd._get_dresiduals(g[key + "_dT"]), g[key + "_dres"]) < TOL
+    assert rel(cd._get_dresiduals(g[key + "_dT"], g[key + "_du"], g[key + "_dv"]), g[key + "_dres_full"]) < TOL
+
+
+def test_cd_cfg1_solution_and_interpolation(gpu):
+    """BASELINE configs[0]: Examples/ConvectionDiffusion_Example.py physics on 4x4, P=4."""
+    from sem_amd.solvers import ConvectionDiffusionSolver
+    g = golden("cd.npz")
+    cd = ConvectionDiffusionSolver(1.0, 1.0, 40.0, 4, 4, 4, T_E=-0.5, T_W=0.5)
+    u = cd._get_vector(lambda x, y: y - 0.5)
+    v = cd._get_vector(lambda x, y: 0.5 - x)
+    T = cd._get_solution(u, v)
+    assert np.abs(T - g["cfg1_T"]).max() < 1e-6          # LGMRES to atol = mtol*sqrt(N), as the reference
+    assert np.abs(cd._get_residuals(T, u, v)).max() < 1e-6
+    Tp = cd._get_interpol(T, (g["cfg1_plot_x"], g["cfg1_plot_y"]))
+    assert np.abs(Tp - g["cfg1_T_plot"]).max() < 1e-6
+
+
+def test_ns_residuals_and_jacobians(gpu):
+    from sem_amd.solvers import NavierStokesSolver
+    g = golden("ns.npz")
+    k = "P4_4x4_"
+    ns = NavierStokesSolver(1.0, 1.0, 100.0, 50.0, 4, 4, 4, u_N=1.0, iprint=[])
+    assert np.array_equal(ns._mask_bound, g[k + "mask_bound"])
+    ru, rv, rc = ns._get_residuals(g[k + "u"], g[k + "v"], g[k + "p"], g[k + "T"])
+    assert rel(ru, g[k + "ru"]) < TOL and rel(rv, g[k + "rv"]) < TOL and rel(rc, g[k + "rc"]) < TOL
+    ns._calc_jacobians(g[k + "u"], g[k + "v"])
+    du, dv, dp = ns._get_dresiduals(g[k + "du"], g[k + "dv"], g[k + "dp"], g[k + "dT"])
+    assert rel(du, g[k + "dru"]) < TOL and rel(dv, g[k + "drv"]) < TOL and rel(dp, g[k + "drc"]) < TOL
+    # the materialised velocity Jacobian blocks equal the matrix-free ones
+    w = np.random.default_rng(9).uniform(-1, 1, ns.N)
+    for J in (ns._Jac_u_u, ns._Jac_u_v, ns._Jac_v_u, ns._Jac_v_v):
+        assert rel(J.tocsr() @ w, J @ w) < 1e-12
+
+
+def test_ns_lid_driven_solve(gpu):
+    from sem_amd.solvers import NavierStokesSolver
+    g = golden("ns.npz")
+    ns = NavierStokesSolver(1.0, 1.0, 100.0, 0.0, 4, 4, 4, u_N=1.0, iprint=[])
+    u, v, p = ns._get_solution(np.zeros(ns.N))
+    assert ns._k == int(g["lid_newton_iters"])
+    assert np.abs(u - g["lid_u"]).max() < 1e-5 and np.abs(v - g["lid_v"]).max() < 1e-5
+    assert np.abs(p - g["lid_p"]).max() < 1e-4 * max(1.0, np.abs(g["lid_p"]).max())
