@@ -121,6 +121,9 @@ class SEMOperator:
     dot = __matmul__
 
     def matvec(self, x):
+        """SciPy LinearOperator protocol (accepts (N,) or (N, 1))."""
+        if isinstance(x, np.ndarray) and x.ndim == 2 and x.shape[1] == 1:
+            return (self @ x[:, 0])[:, None]
         return self @ x
 
     def __getitem__(self, key):

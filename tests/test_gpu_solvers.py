@@ -68,3 +68,26 @@ def test_ns_lid_driven_solve(gpu):
     assert ns._k == int(g["lid_newton_iters"])
     assert np.abs(u - g["lid_u"]).max() < 1e-5 and np.abs(v - g["lid_v"]).max() < 1e-5
     assert np.abs(p - g["lid_p"]).max() < 1e-4 * max(1.0, np.abs(g["lid_p"]).max())
+
+
+def test_readme_helmholtz_with_scipy_cg(gpu):
+    """Solvers/README.md:60-96: H = lam M + K, g = M f, u = cg(H, g) -- with the matrix-free
+    operators handed straight to SciPy."""
+    import scipy.sparse.linalg as linalg
+    from oracle import sem_oracle as O
+    from sem_amd import SEM
+    L_x, L_y, lam, P, N_ex, N_ey = 2, 1, 1, 4, 2, 3
+    f = lambda x, y: np.cos(np.pi * x / L_x) * np.cos(np.pi * y / L_y)  # noqa: E731
+    dx, dy = L_x / N_ex, L_y / N_ey
+    points = SEM.global_nodes(P, N_ex, N_ey, dx, dy)
+    M = SEM.global_mass_matrix(P, N_ex, N_ey, dx, dy)
+    K = SEM.global_stiffness_matrix(P, N_ex, N_ey, dx, dy)
+    H = lam * M + K
+    g = M @ f(points[0], points[1])
+    u = linalg.cg(H, g, rtol=1e-12)[0]
+    Mo, Ko = O.global_mass_matrix(P, N_ex, N_ey, dx, dy), O.global_stiffness_matrix(P, N_ex, N_ey, dx, dy)
+    uo = linalg.cg(lam * Mo + Ko, Mo @ f(points[0], points[1]), rtol=1e-12)[0]
+    assert np.abs(u - uo).max() < 1e-9
+    # the exact solution is f / (lam + pi^2/L_x^2 + pi^2/L_y^2)
+    exact = f(points[0], points[1]) / (lam + np.pi ** 2 / L_x ** 2 + np.pi ** 2 / L_y ** 2)
+    assert np.abs(u - exact).max() < 1e-3
