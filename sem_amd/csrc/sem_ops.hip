@@ -65,6 +65,7 @@ struct ApplyArgs {
   unsigned sides;
   int has_e1, has_e2;
   int n_local32;  // local vector length (MFMA path: < 2^31)
+  int diag;       // ablation bits for performance diagnosis (SEM_DIAG env); 0 in production
 };
 
 template <int P>
@@ -341,9 +342,10 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int pitch18(int w) { return w + ((18 - (w % 32)) + 32) % 32; }  // >= w, == 18 (mod 32)
 
-template <int P, int TX_, int TY_, int NW_>
+template <int P, int TX_, int TY_, int NW_, bool SPLIT_>
 struct MCfg {
   static constexpr int n = P + 1, TX = TX_, TY = TY_, NW = NW_, THREADS = 64 * NW_;
+  static constexpr bool SPLIT = SPLIT_;                   // K and G chains as separate wave tasks
   static constexpr int BX = TX * P, BY = TY * P;          // owned lines / columns (w/o closing ones)
   static constexpr int NLB = (BX + 15) / 16, NCB = (BY + 15) / 16;  // 16-wide MFMA blocks
   static constexpr int KS = (n + 3) / 4;                  // k-steps of 4
@@ -353,7 +355,8 @@ struct MCfg {
   static constexpr int EC = 16 * NCB;   // E (x-results) column pitch
   static constexpr int FL = 16 * NLB;   // F (y-results) lines per element row
   static constexpr int TA = (TX + 1) * NCB, TB = (TY + 1) * NLB;
-  static constexpr int TPW = (TA + TB + NW - 1) / NW;     // MFMA tasks per wave
+  static constexpr int NT = (TA + TB) * (SPLIT ? 2 : 1);  // MFMA wave tasks per tile
+  static constexpr int TPW = (NT + NW - 1) / NW;          // tasks per wave
   static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
   static constexpr int NMAIN = (BX * BY + THREADS - 1) / THREADS;  // epilogue nodes per thread
   static_assert(n <= 16, "MFMA path needs P+1 <= 16");
@@ -366,10 +369,16 @@ struct MSmem {
   double EG[(C::TX + 1) * C::n * C::EC];
   double FK[(C::TY + 1) * C::FL * C::n];
   double FG[(C::TY + 1) * C::FL * C::n];
-  double Kt[C::n * C::n];  // coefficient tables for the closing-line / closing-column path
-  double Gt[C::n * C::n];
   double ws[C::n];
 };
+
+// Sum of GLL weights of the elements in [e_lo, e_hi) that hold 1-D node g (32-bit, P compile-time).
+template <int P>
+__device__ __forceinline__ double wsum(int g, int e_lo, int e_hi, const double* w) {
+  const int e = g / P, i = g - e * P;
+  if (i != 0) return w[i];
+  return (e - 1 >= e_lo && e - 1 < e_hi ? w[P] : 0.0) + (e >= e_lo && e < e_hi ? w[0] : 0.0);
+}
 
 // Generic (VALU) contraction along one staged direction for nodes the MFMA blocks do not
 // cover (the domain's closing line / column): `base` points at the element's node 0 in the
@@ -396,43 +405,25 @@ __device__ __forceinline__ void contract_generic(const double* Kt, const double*
   }
 }
 
-template <int P, int TX, int TY, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
-  using C = MCfg<P, TX, TY, NW>;
+template <int P, int TX, int TY, int NW, bool PERSIST, bool SPLIT>
+__global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void apply_tp_mfma(const ApplyArgs a) {
+  using C = MCfg<P, TX, TY, NW, SPLIT>;
   constexpr int n = C::n;
   __shared__ MSmem<C> sm;
 
-  // Persistent workgroups: each walks a contiguous run of tiles (y fastest), so consecutive
-  // tiles of one workgroup share y-halo lines in its XCD's L2.  The XCD-aware remap gives the
-  // workgroups of one XCD neighbouring runs.
+  // Workgroups walk contiguous runs of tiles (y fastest); the XCD-aware remap gives the
+  // workgroups of one XCD neighbouring runs (halo lines shared through that XCD's L2).
   const int nb = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q = nb >> 3, rem = nb & 7;
   const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
   const int ntiles = a.tiles_x * a.tiles_y;
-  const int t_begin = static_cast<int>((static_cast<long long>(L) * ntiles) / nb);
-  const int t_end = static_cast<int>((static_cast<long long>(L + 1) * ntiles) / nb);
+  const int t_begin = PERSIST ? static_cast<int>((static_cast<long long>(L) * ntiles) / nb) : L;
+  const int t_end = PERSIST ? static_cast<int>((static_cast<long long>(L + 1) * ntiles) / nb) : L + 1;
 
   const int lb0 = static_cast<int>(a.line_begin), lb1 = static_cast<int>(a.line_end), NY = static_cast<int>(a.NY);
   const int nmax = a.n_local32 - 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
-
-  // ---- per-lane MFMA coefficient operands: A[i=lr][k=4s+lk] = K_s[lr][k] (0 outside n x n)
-  double aK[C::KS], aG[C::KS];
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s) {
-    const int k = 4 * s + lk;
-    const bool ok = lr <= P && k <= P;
-    const int idx = ok ? lr * n + k : 0;
-    const double kv = a.tab[idx], gv = a.tab[n * n + idx];
-    aK[s] = ok ? kv : 0.0;
-    aG[s] = ok ? gv : 0.0;
-  }
-  for (int t = tid; t < n * n; t += C::THREADS) {
-    sm.Kt[t] = a.tab[t];
-    sm.Gt[t] = a.tab[n * n + t];
-  }
-  if (tid < n) sm.ws[tid] = a.tab[2 * n * n + tid];
 
   // Issue every global load of tile t (staged x window, u and v of this thread's epilogue
   // nodes) from clamped, always in-bounds addresses; values of clamped entries are never
@@ -460,13 +451,28 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
   };
   if (t_begin < t_end) issue(t_begin);
 
+  // Per-lane MFMA coefficient operands A[i=lr][k=4s+lk] = K_s[lr][k] (0 outside n x n) and the
+  // GLL weights, loaded AFTER the tile's loads so nothing waits for them before staging starts.
+  double aK[C::KS], aG[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) {
+    const int k = 4 * s + lk;
+    const bool ok = lr <= P && k <= P;
+    const int idx = ok ? lr * n + k : 0;
+    const double kv = a.tab[idx], gv = a.tab[n * n + idx];
+    aK[s] = ok ? kv : 0.0;
+    aG[s] = ok ? gv : 0.0;
+  }
+  const double wreg = a.tab[2 * n * n + min(tid, n - 1)];
+  bool ws_done = false;
+
   for (int t = t_begin; t < t_end; ++t) {
     const int tx = t / a.tiles_y, ty = t - tx * a.tiles_y;
     const int m0 = a.ex_begin + tx * TX, m1 = min(m0 + TX, a.ex_end);
     const int n0 = ty * TY, n1 = min(n0 + TY, a.ney);
     const int gx0 = m0 * P, gy0 = n0 * P;
 
-    __syncthreads();  // the previous tile's epilogue has finished reading Ts
+    if (PERSIST) __syncthreads();  // the previous tile's epilogue has finished reading Ts
 #pragma unroll
     for (int s = 0; s < C::NSTAGE; ++s) {
       const int idx = tid + s * C::THREADS;
@@ -475,6 +481,10 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
         sm.Ts[rr * C::PT + cc] = st[s];
       }
     }
+    if (!ws_done) {
+      if (tid < n) sm.ws[tid] = wreg;
+      ws_done = true;
+    }
     double cu_[C::NMAIN], cv_[C::NMAIN];
 #pragma unroll
     for (int qn = 0; qn < C::NMAIN; ++qn) {
@@ -482,12 +492,16 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
       cv_[qn] = pv[qn];
     }
     __syncthreads();
-    if (t + 1 < t_end) issue(t + 1);  // next tile's loads fly while this tile computes
+    if (PERSIST && t + 1 < t_end) issue(t + 1);  // next tile's loads fly while this tile computes
 
-    // ---- phases A and B: MFMA tasks, round-robin over waves
+    // ---- phases A and B: MFMA wave tasks (K and G chains fused, or split when SPLIT)
 #pragma unroll
     for (int tt = 0; tt < C::TPW; ++tt) {
-      const int task = wave + tt * NW;
+      if (a.diag & 1) break;
+      const int task0 = wave + tt * NW;
+      const int task = SPLIT ? task0 >> 1 : task0;
+      const int part = SPLIT ? (task0 & 1) : 2;  // 0: K only, 1: G only, 2: both
+      if (task0 >= C::NT) continue;
       if (task < C::TA) {
         const int e = task / C::NCB, cb = task - e * C::NCB;  // element column e (0 = halo), column block
         dbl4 accK = {0.0, 0.0, 0.0, 0.0}, accG = {0.0, 0.0, 0.0, 0.0};
@@ -496,18 +510,18 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
           const int k = 4 * s + lk;
           double bv = sm.Ts[(e * P + k) * C::PT + P + cb * 16 + lr];
           if (4 * s + 3 > P) bv = k <= P ? bv : 0.0;  // next element's nodes: keep NaN/Inf out
-          accK = __builtin_amdgcn_mfma_f64_16x16x4f64(aK[s], bv, accK, 0, 0, 0);
-          accG = __builtin_amdgcn_mfma_f64_16x16x4f64(aG[s], bv, accG, 0, 0, 0);
+          if (part != 1) accK = __builtin_amdgcn_mfma_f64_16x16x4f64(aK[s], bv, accK, 0, 0, 0);
+          if (part != 0) accG = __builtin_amdgcn_mfma_f64_16x16x4f64(aG[s], bv, accG, 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = lk + 4 * r;  // C/D row of an f64 16x16x4 MFMA: (lane>>4) + 4*reg
           if (i <= P) {
-            sm.EK[(e * n + i) * C::EC + cb * 16 + lr] = accK[r];
-            sm.EG[(e * n + i) * C::EC + cb * 16 + lr] = accG[r];
+            if (part != 1) sm.EK[(e * n + i) * C::EC + cb * 16 + lr] = accK[r];
+            if (part != 0) sm.EG[(e * n + i) * C::EC + cb * 16 + lr] = accG[r];
           }
         }
-      } else if (task < C::TA + C::TB) {
+      } else {
         const int tb = task - C::TA;
         const int e = tb / C::NLB, lbk = tb - e * C::NLB;  // element row e (0 = halo), line block
         dbl4 accK = {0.0, 0.0, 0.0, 0.0}, accG = {0.0, 0.0, 0.0, 0.0};
@@ -516,15 +530,15 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
           const int k = 4 * s + lk;
           double av = sm.Ts[(P + lbk * 16 + lr) * C::PT + e * P + k];
           if (4 * s + 3 > P) av = k <= P ? av : 0.0;
-          accK = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aK[s], accK, 0, 0, 0);
-          accG = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aG[s], accG, 0, 0, 0);
+          if (part != 1) accK = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aK[s], accK, 0, 0, 0);
+          if (part != 0) accG = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aG[s], accG, 0, 0, 0);
         }
         if (lr <= P) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int line = lbk * 16 + lk + 4 * r;
-            sm.FK[(e * C::FL + line) * n + lr] = accK[r];
-            sm.FG[(e * C::FL + line) * n + lr] = accG[r];
+            if (part != 1) sm.FK[(e * C::FL + line) * n + lr] = accK[r];
+            if (part != 0) sm.FG[(e * C::FL + line) * n + lr] = accG[r];
           }
         }
       }
@@ -534,16 +548,21 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
     // ---- epilogue: one owned node per item, lanes along columns (coalesced global I/O)
     const int BXo = (m1 - m0) * P, BYo = (n1 - n0) * P;  // owned without closing line / column
     const bool lastx = m1 == a.ex_end, lasty = n1 == a.ney;
-    auto node = [&](int rl, int c, double uu, double vv) {
+    auto node = [&](auto EDGE, int rl, int c, double uu, double vv) {
+      constexpr bool edge = decltype(EDGE)::value;
       const int gx = gx0 + rl, gy = gy0 + c;
       const int p = (gx - lb0) * NY + gy;
       const double xv = sm.Ts[(P + rl) * C::PT + P + c];
+      if (a.diag & 2) {
+        a.y[p] = xv * uu + vv;
+        return;
+      }
       // x-direction: element column of this line (right) and, at a shared line, the left one
       const int i = rl % P, ex = rl / P;
       const int mR = m0 + ex;
       const bool hasR = mR < a.ex_end, hasLx = i == 0 && mR - 1 >= a.ex_begin;
       double XK = 0.0, XG = 0.0;
-      if (c < C::EC) {
+      if (!edge || c < C::EC) {
         if (hasLx) {
           XK = sm.EK[(ex * n + P) * C::EC + c];
           XG = sm.EG[(ex * n + P) * C::EC + c];
@@ -553,14 +572,15 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
           XG += sm.EG[((ex + 1) * n + i) * C::EC + c];
         }
       } else {
-        contract_generic<P>(sm.Kt, sm.Gt, &sm.Ts[(P + rl - i) * C::PT + P + c], C::PT, i, hasR, hasLx, XK, XG);
+        contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl - i) * C::PT + P + c], C::PT, i, hasR, hasLx, XK,
+                            XG);
       }
       // y-direction
       const int j = c % P, ey = c / P;
       const int nR = n0 + ey;
       const bool hasRy = nR < a.ney, hasLy = j == 0 && nR - 1 >= 0;
       double YK = 0.0, YG = 0.0;
-      if (rl < C::FL) {
+      if (!edge || rl < C::FL) {
         if (hasLy) {
           YK = sm.FK[(ey * C::FL + rl) * n + P];
           YG = sm.FG[(ey * C::FL + rl) * n + P];
@@ -570,10 +590,11 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
           YG += sm.FG[((ey + 1) * C::FL + rl) * n + j];
         }
       } else {
-        contract_generic<P>(sm.Kt, sm.Gt, &sm.Ts[(P + rl) * C::PT + P + c - j], 1, j, hasRy, hasLy, YK, YG);
+        contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl) * C::PT + P + c - j], 1, j, hasRy, hasLy, YK,
+                            YG);
       }
-      const double mx = weight_sum(gx, P, a.ex_begin, a.ex_end, sm.ws);
-      const double my = weight_sum(gy, P, 0, a.ney, sm.ws);
+      const double mx = wsum<P>(gx, a.ex_begin, a.ex_end, sm.ws);
+      const double my = wsum<P>(gy, 0, a.ney, sm.ws);
       double z = 0.0;
       if (a.cK != 0.0) z = a.cK * fma(a.sx * my, XK, a.sy * mx * YK);
       if (a.cM != 0.0) z = fma(a.cM * a.hxy * mx * my, xv, z);
@@ -603,11 +624,11 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
     for (int qn = 0; qn < C::NMAIN; ++qn) {
       const int idx = tid + qn * C::THREADS;
       const int rl = idx / C::BY, c = idx - rl * C::BY;
-      if (idx < C::BX * C::BY && rl < BXo && c < BYo) node(rl, c, cu_[qn], cv_[qn]);
+      if (idx < C::BX * C::BY && rl < BXo && c < BYo) node(std::false_type{}, rl, c, cu_[qn], cv_[qn]);
     }
     auto edge = [&](int rl, int c) {
       const int p = (gx0 + rl - lb0) * NY + gy0 + c;
-      node(rl, c, a.cu ? a.cu[p] : 1.0, a.cv ? a.cv[p] : 1.0);
+      node(std::true_type{}, rl, c, a.cu ? a.cu[p] : 1.0, a.cv ? a.cv[p] : 1.0);
     };
     if (lastx)  // closing line of the local lines
       for (int c = tid; c < BYo + (lasty ? 1 : 0); c += C::THREADS) edge(BXo, c);
@@ -616,50 +637,50 @@ __global__ __launch_bounds__(64 * NW, 2) void apply_tp_mfma(const ApplyArgs a) {
   }
 }
 
-template <int P, int TX, int TY, int NW>
+template <int P, int TX, int TY, int NW, bool PERSIST, bool SPLIT>
 static int launch_apply_mfma(const ApplyArgs& args_in, const sem_handle* h, hipStream_t s) {
-  using C = MCfg<P, TX, TY, NW>;
+  using C = MCfg<P, TX, TY, NW, SPLIT>;
   ApplyArgs args = args_in;
   const int ncols = h->ex_end - h->ex_begin;
   args.tiles_x = (ncols + TX - 1) / TX;
   args.tiles_y = (h->ney + TY - 1) / TY;
   const long long ntiles = static_cast<long long>(args.tiles_x) * args.tiles_y;
   if (ntiles <= 0 || ntiles > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
-  // persistent grid: the resident workgroups of every CU, never more than the tiles
-  static int resident = [] {
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, apply_tp_mfma<P, TX, TY, NW>, C::THREADS, 0) !=
-            hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || cus < 1)
-      cus = 256;
-    return per_cu * cus;
-  }();
-  static const int oversub = [] {
-    const char* e = std::getenv("SEM_MFMA_OVERSUB");  // tuning override: grid = resident x this
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
-  const long long grid = std::min<long long>(ntiles, static_cast<long long>(resident) * oversub);
-  hipLaunchKernelGGL((apply_tp_mfma<P, TX, TY, NW>), dim3(static_cast<unsigned>(grid)), dim3(C::THREADS), 0, s,
-                     args);
+  long long grid = ntiles;
+  if (PERSIST) {  // persistent grid: the resident workgroups of every CU, never more than the tiles
+    static int resident = [] {
+      int per_cu = 0, dev = 0, cus = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, apply_tp_mfma<P, TX, TY, NW, PERSIST, SPLIT>,
+                                                       C::THREADS, 0) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+      return per_cu * cus;
+    }();
+    grid = std::min<long long>(ntiles, resident);
+  }
+  hipLaunchKernelGGL((apply_tp_mfma<P, TX, TY, NW, PERSIST, SPLIT>), dim3(static_cast<unsigned>(grid)),
+                     dim3(C::THREADS), 0, s, args);
   return hip_check(hipGetLastError(), "apply (mfma) launch");
 }
 
-// Tile shapes: element tiles of ~32 x 32 nodes (4 waves) for large meshes, ~16 x 16 nodes
-// (2 waves) when the mesh is too small to give every CU several workgroups.
+// Tile shapes: element tiles of ~32 x 32 nodes (4 waves, persistent) for large meshes; ~16 x 16
+// nodes for meshes too small to give every CU several workgroups (4 waves with the K and G
+// chains as separate tasks; SEM_MFMA_TILE=1 selects the earlier 2-wave variant).
 template <int P>
 static int launch_apply_mfma_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
   constexpr int TL = (32 / P) > 0 ? 32 / P : 1;
   constexpr int TS = (16 / P) > 0 ? 16 / P : 1;
   const long long big_tiles = static_cast<long long>((h->ex_end - h->ex_begin + TL - 1) / TL) * ((h->ney + TL - 1) / TL);
   static const int force = [] {
-    const char* e = std::getenv("SEM_MFMA_TILE");  // tuning override: 1 = small, 2 = large
+    const char* e = std::getenv("SEM_MFMA_TILE");  // tuning override: 1 = small 2-wave, 2 = large, 3 = small 4-wave
     return e ? std::atoi(e) : 0;
   }();
-  if (force == 2 || (force == 0 && big_tiles >= 4 * 256)) return launch_apply_mfma<P, TL, TL, 4>(args, h, s);
-  return launch_apply_mfma<P, TS, TS, 2>(args, h, s);
+  if (force == 2 || (force == 0 && big_tiles >= 4 * 256)) return launch_apply_mfma<P, TL, TL, 4, true, false>(args, h, s);
+  if (force == 1) return launch_apply_mfma<P, TS, TS, 2, false, false>(args, h, s);
+  return launch_apply_mfma<P, TS, TS, 4, false, true>(args, h, s);
 }
 
 // =========================================================================== column kernel
@@ -703,7 +724,11 @@ __global__ __launch_bounds__((CCfg<P, TX, BY, RS>::THREADS)) void apply_tp_col(c
   const int BYo = min(BY, NY - 1 - gy0);     // owned columns without the domain's closing one
   const bool lasty = gy0 + BY >= NY - 1;
   const int tid = threadIdx.x;
-  const int c = tid % BY, s = (tid / BY) % RS, e = tid / (BY * RS);
+  const int c = tid % BY;
+  // (element column, split) are wave-uniform by construction (BY*RS is a multiple of 64):
+  // readfirstlane puts them and everything derived per row (line, weights, flags) in SGPRs
+  const int s = __builtin_amdgcn_readfirstlane((tid / BY) % RS);
+  const int e = __builtin_amdgcn_readfirstlane(tid / (BY * RS));
   const int me = m0 + e;                      // this thread's element column
   const bool hasE = me < m1;
 
@@ -727,6 +752,21 @@ __global__ __launch_bounds__((CCfg<P, TX, BY, RS>::THREADS)) void apply_tp_col(c
     pu[ii] = a.cu ? a.cu[p] : 1.0;
     pv[ii] = a.cv ? a.cv[p] : 1.0;
   }
+  // the y coefficient rows of this thread's column, loaded with the tile (no wait before staging)
+  double rK0[n], rG0[n];
+  auto coef_rows = [&](int cc, double (&rK)[n], double (&rG)[n]) {
+    const int gy = gy0 + cc;
+    const int j = gy % P;
+    const bool hasRy = gy / P < a.ney;
+#pragma unroll
+    for (int l = 0; l <= P; ++l) {
+      const int idx = (hasRy ? j : 0) * n + l;
+      const double kv = a.tab[idx], gv = a.tab[n * n + idx];
+      rK[l] = hasRy ? kv : 0.0;
+      rG[l] = hasRy ? gv : 0.0;
+    }
+  };
+  coef_rows(c, rK0, rG0);
   if (tid < n) ws[tid] = wreg;
 #pragma unroll
   for (int k = 0; k < C::NSTAGE; ++k) {
@@ -739,19 +779,11 @@ __global__ __launch_bounds__((CCfg<P, TX, BY, RS>::THREADS)) void apply_tp_col(c
   __syncthreads();
 
   // per-column (per-lane) y data: local index j, right/left element flags, coefficient rows
-  auto column = [&](int cc, double (&uu)[RP + 1], double (&vv)[RP + 1]) {
+  auto column = [&](int cc, double (&uu)[RP + 1], double (&vv)[RP + 1], const double (&rK)[n], const double (&rG)[n]) {
     const int gy = gy0 + cc;
     const int j = gy % P, ne = gy / P;
-    const bool hasRy = ne < a.ney, hasLy = j == 0 && ne > 0;
-    double rK[n], rG[n];
-#pragma unroll
-    for (int l = 0; l <= P; ++l) {
-      const int idx = (hasRy ? j : 0) * n + l;
-      const double kv = a.tab[idx], gv = a.tab[n * n + idx];
-      rK[l] = hasRy ? kv : 0.0;
-      rG[l] = hasRy ? gv : 0.0;
-    }
-    const double my = weight_sum(gy, P, 0, a.ney, ws);
+    const bool hasLy = j == 0 && ne > 0;
+    const double my = wsum<P>(gy, 0, a.ney, ws);
     // x-window of this element column along column cc: T[meP-P+k][gy], k = 0..2P
     double xt[2 * P + 1];
 #pragma unroll
@@ -776,7 +808,7 @@ __global__ __launch_bounds__((CCfg<P, TX, BY, RS>::THREADS)) void apply_tp_col(c
       }
       const int p = (gx - lb0) * NY + gy;
       const double xv = xt[P + i];
-      const double mx = weight_sum(gx, P, a.ex_begin, a.ex_end, ws);
+      const double mx = wsum<P>(gx, a.ex_begin, a.ex_end, ws);
       double z = 0.0;
       if (a.cK != 0.0) z = a.cK * fma(a.sx * my, kx, a.sy * mx * ky);
       if (a.cM != 0.0) z = fma(a.cM * a.hxy * mx * my, xv, z);
@@ -816,16 +848,17 @@ __global__ __launch_bounds__((CCfg<P, TX, BY, RS>::THREADS)) void apply_tp_col(c
       if (s == decltype(S)::value) rows(S);
     });
   };
-  if (hasE && c < BYo) column(c, pu, pv);
+  if (hasE && c < BYo) column(c, pu, pv, rK0, rG0);
   if (hasE && lasty && c == 0) {  // the domain's closing column
-    double qu[RP + 1], qv[RP + 1];
+    double qu[RP + 1], qv[RP + 1], rK1[n], rG1[n];
+    coef_rows(BYo, rK1, rG1);
 #pragma unroll
     for (int ii = 0; ii <= RP; ++ii) {
       const int p = min((me * P + s * RP + ii - lb0) * NY + gy0 + BYo, nmax);
       qu[ii] = a.cu ? a.cu[p] : 1.0;
       qv[ii] = a.cv ? a.cv[p] : 1.0;
     }
-    column(BYo, qu, qv);
+    column(BYo, qu, qv, rK1, rG1);
   }
 }
 
@@ -852,6 +885,12 @@ static int launch_apply_col_auto(const ApplyArgs& args, const sem_handle* h, hip
   constexpr int BYs = 64 / RS > 16 ? 64 / RS : 16;
   if (force == 1) return launch_apply_col<P, 2, BYs, RS>(args, h, s);
   if (force == 2) return launch_apply_col<P, 4, 64, 1>(args, h, s);
+  if constexpr (RS > 1) {
+    if (force == 4) return launch_apply_col<P, 2, 64, RS>(args, h, s);
+    if (force == 5) return launch_apply_col<P, 1, 64, RS>(args, h, s);
+    if (force == 6) return launch_apply_col<P, 1, 64, 2>(args, h, s);
+    if (force == 7) return launch_apply_col<P, 2, 64, 2>(args, h, s);
+  }
   return launch_apply_col<P, 2, 64, 1>(args, h, s);
 }
 
@@ -1106,6 +1145,11 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   a.dir_mode = d->dir_mode;
   a.sides = d->dir_sides;
   a.n_local32 = static_cast<int>(std::min<int64_t>(h->n_local, 0x7fffffff));
+  static const int diag = [] {
+    const char* e = std::getenv("SEM_DIAG");  // ablation for profiling only: results are wrong when set
+    return e ? std::atoi(e) : 0;
+  }();
+  a.diag = diag;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // AUTO: measured on MI355X (tools/kbench.py) -- the MFMA tile kernel wins on meshes that
   // leave the chip latency-bound (< 2M DOFs), the single-phase column kernel on larger ones.
@@ -1160,9 +1204,9 @@ int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
     const int TL = std::max(1, 32 / P), TS = std::max(1, 16 / P);
     const long long big = static_cast<long long>((h->ex_end - h->ex_begin + TL - 1) / TL) * ((h->ney + TL - 1) / TL);
     name = big >= 4 * 256 ? "sem::apply_tp_mfma<" + std::to_string(P) + ", " + std::to_string(TL) + ", " +
-                                std::to_string(TL) + ", 4>"
+                                std::to_string(TL) + ", 4, true, false>"
                           : "sem::apply_tp_mfma<" + std::to_string(P) + ", " + std::to_string(TS) + ", " +
-                                std::to_string(TS) + ", 2>";
+                                std::to_string(TS) + ", 4, false, true>";
   } else {
     name = "sem::apply_tp_valu<" + std::to_string(P) + ">";
   }

@@ -14,8 +14,10 @@ Vectors may be NumPy arrays (returned as NumPy, like the reference) or float64
 device tensors (kept on the device).  The Dirichlet mask is built exactly as the
 reference builds it (np.isclose on the node coordinates, :62-71); when it is the
 plain boundary-line set the kernel derives it from geometry (no mask traffic).
-`_get_update` keeps the reference's LGMRES (SciPy, host Arnoldi) around device
-matvecs; a device-resident Krylov solver is the next step.
+`_get_update` runs a device-resident GMRES (sem_amd/krylov.py: Krylov basis in
+HBM, CGS2 orthogonalisation as GEMVs, same stopping rule atol = mtol*sqrt(N) as
+the reference's LGMRES); `krylov="scipy"` keeps the reference's host LGMRES
+around device matvecs.
 """
 import typing
 
@@ -25,6 +27,7 @@ import torch
 
 from .. import SEM, _lib
 from ..device import get_mesh
+from ..krylov import gmres
 
 
 def side_mask(points, L_x, L_y, sides):
@@ -74,7 +77,10 @@ class DirichletRows:
 class ConvectionDiffusionSolver:
     def __init__(self, L_x: float, L_y: float, Pe: float, P: int, N_ex: int, N_ey: int,
                  T_W: float = None, T_E: float = None, T_S: float = None, T_N: float = None,
-                 mtol=1e-7, iprint: list = []):  # noqa: B006 - reference signature
+                 mtol=1e-7, iprint: list = [], krylov: str = "device", max_basis: int = 2000):  # noqa: B006
+        if krylov not in ("device", "scipy"):
+            raise ValueError("krylov must be 'device' or 'scipy'")
+        self._krylov, self._max_basis = krylov, max_basis
         self._iprint = iprint
         self._Pe = Pe
         self._mtol = mtol
@@ -140,7 +146,34 @@ class ConvectionDiffusionSolver:
         return self._out(y, dT)
 
     def _get_update(self, dres, dT0=None):
-        """LGMRES on the device matvec (ConvectionDiffusion_Solver.py:123-156)."""
+        """Newton update: solve dres_op(dT) = dres (ConvectionDiffusion_Solver.py:123-156)."""
+        if self._krylov == "device":
+            return self._get_update_device(dres, dT0)
+        return self._get_update_scipy(dres, dT0)
+
+    def _get_update_device(self, dres, dT0=None):
+        """GMRES with the Krylov basis in HBM; restart = min(int(0.3 N), max_basis) (the
+        reference's inner_m, capped so the basis fits device memory)."""
+        b = self._dev(dres)
+        x0 = self._dev(dT0)
+        it = [0]
+
+        def cb(est):
+            it[0] += 1
+            if "LGMRES_iter" in self._iprint:
+                print(f"ConvectionDiffusion GMRES: {it[0]}\t{est}")
+
+        r = gmres(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
+                  restart=max(1, min(int(self.N * 0.3), self._max_basis)), callback=cb)
+        if r.info != 0:
+            raise RuntimeError(f"ConvectionDiffusion LGMRES: Failed to converge in {r.info} iterations")
+        if "LGMRES_suc" in self._iprint:
+            res = (self._get_dresiduals(r.x) - b).abs().max().item()
+            print(f"ConvectionDiffusion GMRES: Converged in {r.matvecs} evaluations with max-norm {res}")
+        return self._out(r.x, dres)
+
+    def _get_update_scipy(self, dres, dT0=None):
+        """The reference's LGMRES on the host around device matvecs."""
 
         def lhs_mv(dT):
             lhs_mv.fCount += 1

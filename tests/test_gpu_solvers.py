@@ -29,11 +29,12 @@ def test_cd_residuals_and_jacobians(gpu, key):
     assert rel(cd._get_dresiduals(g[key + "_dT"], g[key + "_du"], g[key + "_dv"]), g[key + "_dres_full"]) < TOL
 
 
-def test_cd_cfg1_solution_and_interpolation(gpu):
+@pytest.mark.parametrize("krylov", ["device", "scipy"])
+def test_cd_cfg1_solution_and_interpolation(gpu, krylov):
     """BASELINE configs[0]: Examples/ConvectionDiffusion_Example.py physics on 4x4, P=4."""
     from sem_amd.solvers import ConvectionDiffusionSolver
     g = golden("cd.npz")
-    cd = ConvectionDiffusionSolver(1.0, 1.0, 40.0, 4, 4, 4, T_E=-0.5, T_W=0.5)
+    cd = ConvectionDiffusionSolver(1.0, 1.0, 40.0, 4, 4, 4, T_E=-0.5, T_W=0.5, krylov=krylov)
     u = cd._get_vector(lambda x, y: y - 0.5)
     v = cd._get_vector(lambda x, y: 0.5 - x)
     T = cd._get_solution(u, v)
@@ -91,3 +92,23 @@ def test_readme_helmholtz_with_scipy_cg(gpu):
     # the exact solution is f / (lam + pi^2/L_x^2 + pi^2/L_y^2)
     exact = f(points[0], points[1]) / (lam + np.pi ** 2 / L_x ** 2 + np.pi ** 2 / L_y ** 2)
     assert np.abs(u - exact).max() < 1e-3
+
+
+def test_cd_device_solve_cfg2_against_oracle(gpu):
+    """cfg2 mesh (64x64, P=8) circular-flow CD solve fully on the device vs the oracle's
+    SciPy LGMRES on the assembled CSR (looser mtol to keep the oracle run short)."""
+    import time
+    from oracle import sem_oracle as O
+    from sem_amd.solvers import ConvectionDiffusionSolver
+    P, ne = 8, 16
+    cd = ConvectionDiffusionSolver(1.0, 1.0, 40.0, P, ne, ne, T_W=0.5, T_E=-0.5, mtol=1e-9)
+    u = cd._get_vector(lambda x, y: y - 0.5)
+    v = cd._get_vector(lambda x, y: 0.5 - x)
+    t0 = time.perf_counter()
+    T = cd._get_solution(u, v)
+    t_dev = time.perf_counter() - t0
+    ref = O.CDOracle(1.0, 1.0, 40.0, P, ne, ne, T_W=0.5, T_E=-0.5)
+    Tref = ref.solution(u, v, mtol=1e-9)
+    assert np.abs(T - Tref).max() < 1e-6
+    assert np.abs(cd._get_residuals(T, u, v)).max() < 1e-7
+    print(f"device CD solve {ne}x{ne} P={P}: {t_dev:.3f} s")

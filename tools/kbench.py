@@ -12,15 +12,51 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def time_graph(fn, reps):
+    for _ in range(3):
+        fn()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        for _ in range(reps):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / reps * 1e3)
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--algo", type=int, default=0)
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--meshes", default="8:64,12:128,8:256,8:1024,4:512")
+    ap.add_argument("--floor", action="store_true", help="also time torch.addcmul (same 32 B/DOF traffic)")
+    ap.add_argument("--dss", type=int, default=0,
+                    help="FETCH_SIZE calibration: time sem_dss on an ne x ne, P=8 element array (8-byte loads, "
+                         "reads exactly ne^2*81*8 bytes)")
     a = ap.parse_args()
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     dev = torch.device("cuda", 0)
+    if a.dss:
+        m = get_mesh(8, a.dss, a.dss, 1.0 / a.dss, 1.0 / a.dss)
+        ae = torch.rand((a.dss, a.dss, 9, 9), dtype=torch.float64, device=dev)
+        out = torch.empty(m.n_local, dtype=torch.float64, device=dev)
+        t = time_graph(lambda: m.dss(ae, out), 20)
+        rb, wb = ae.numel() * 8, out.numel() * 8
+        print(f"dss ne={a.dss}: {t:9.2f} us  reads {rb / 1e6:.1f} MB  writes {wb / 1e6:.1f} MB  "
+              f"{(rb + wb) / (t * 1e-6) / 1e9:7.1f} GB/s", flush=True)
+        return
     for spec in a.meshes.split(","):
         P, ne = map(int, spec.split(":"))
         m = get_mesh(P, ne, ne, 1.0 / ne, 1.0 / ne)
@@ -52,6 +88,10 @@ def main():
         gbs = 32.0 * N / (best * 1e-6) / 1e9
         print(f"P={P:2d} ne={ne:5d} N={N:10d} algo={a.algo}: {best:9.2f} us/apply  {N / best / 1e3:9.3f} GDOF/s"
               f"  {gbs:7.1f} GB/s ({gbs / 8000 * 100:5.1f}% of 8 TB/s)", flush=True)
+        if a.floor:
+            fl = time_graph(lambda: torch.addcmul(v, T, u, out=y), reps)
+            print(f"    floor (torch.addcmul, 3 reads + 1 write): {fl:9.2f} us  {32.0 * N / (fl * 1e-6) / 1e9:7.1f} GB/s",
+                  flush=True)
         del T, u, v, y, g
 
 
