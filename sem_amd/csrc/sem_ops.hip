@@ -66,6 +66,7 @@ struct ApplyArgs {
   int has_e1, has_e2;
   int n_local32;  // local vector length (MFMA path: < 2^31)
   int diag;       // ablation bits for performance diagnosis (SEM_DIAG env); 0 in production
+  unsigned long long* stamps;  // SEM_DIAG bit 8: per-wave s_memtime phase stamps (diagnostic builds only)
 };
 
 template <int P>
@@ -355,8 +356,9 @@ struct MCfg {
   static constexpr int EC = 16 * NCB;   // E (x-results) column pitch
   static constexpr int FL = 16 * NLB;   // F (y-results) lines per element row
   static constexpr int TA = (TX + 1) * NCB, TB = (TY + 1) * NLB;
-  static constexpr int NT = (TA + TB) * (SPLIT ? 2 : 1);  // MFMA wave tasks per tile
-  static constexpr int TPW = (NT + NW - 1) / NW;          // tasks per wave
+  static constexpr int NWA = NW > 1 ? NW / 2 : 1;         // waves running phase A (the rest: phase B)
+  static_assert(NW >= 2, "phase A and B run on separate waves");
+  static constexpr int MAXG = 4;                          // tasks batched per wave (register bound)
   static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
   static constexpr int NMAIN = (BX * BY + THREADS - 1) / THREADS;  // epilogue nodes per thread
   static_assert(n <= 16, "MFMA path needs P+1 <= 16");
@@ -372,12 +374,24 @@ struct MSmem {
   double ws[C::n];
 };
 
+// Diagnostic phase stamp (SEM_DIAG bit 8): lane 0 of each wave records s_memtime.
+#define SEM_STAMP(k)                                                                      \
+  do {                                                                                    \
+    if (a.stamps) {                                                                       \
+      unsigned long long t_;                                                              \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if ((threadIdx.x & 63) == 0) a.stamps[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+    }                                                                                     \
+  } while (0)
+
 // Sum of GLL weights of the elements in [e_lo, e_hi) that hold 1-D node g (32-bit, P compile-time).
 template <int P>
 __device__ __forceinline__ double wsum(int g, int e_lo, int e_hi, const double* w) {
   const int e = g / P, i = g - e * P;
-  if (i != 0) return w[i];
-  return (e - 1 >= e_lo && e - 1 < e_hi ? w[P] : 0.0) + (e >= e_lo && e < e_hi ? w[0] : 0.0);
+  const double wi = w[i], wP = w[P], w0 = w[0];  // unconditional reads: no per-lane branch
+  return i != 0 ? wi : (e - 1 >= e_lo && e - 1 < e_hi ? wP : 0.0) + (e >= e_lo && e < e_hi ? w0 : 0.0);
 }
 
 // Generic (VALU) contraction along one staged direction for nodes the MFMA blocks do not
@@ -405,6 +419,20 @@ __device__ __forceinline__ void contract_generic(const double* Kt, const double*
   }
 }
 
+// Buffer resource over `bytes` bytes at p (wave-uniform inputs only).  Loads at offsets outside
+// [0, bytes) -- including "negative" offsets, which wrap to huge unsigned values -- return 0
+// without touching memory, so halo staging needs no clamps.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v),
+                                        r, off, 0, 0);
+}
+
 template <int P, int TX, int TY, int NW, bool PERSIST, bool SPLIT>
 __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void apply_tp_mfma(const ApplyArgs a) {
   using C = MCfg<P, TX, TY, NW, SPLIT>;
@@ -421,32 +449,49 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
   const int t_end = PERSIST ? static_cast<int>((static_cast<long long>(L + 1) * ntiles) / nb) : L + 1;
 
   const int lb0 = static_cast<int>(a.line_begin), lb1 = static_cast<int>(a.line_end), NY = static_cast<int>(a.NY);
-  const int nmax = a.n_local32 - 1;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lk = lane >> 4;
+  SEM_STAMP(0);
+  if (a.stamps && lane == 0) {  // slot 7: the XCD this wave runs on (stamps are per-XCD clocks)
+    unsigned xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)" : "=s"(xcc), "=s"(hw));
+    a.stamps[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 7] =
+        (static_cast<unsigned long long>(hw) << 8) | (xcc & 0xf);
+  }
 
-  // Issue every global load of tile t (staged x window, u and v of this thread's epilogue
-  // nodes) from clamped, always in-bounds addresses; values of clamped entries are never
-  // consumed.  No load is conditional: a "load or zero" select makes hipcc wait per load.
+  const int nbytes = a.n_local32 * 8;
+  const auto rx = brsrc(a.x, nbytes), ru = brsrc(a.cu, a.cu ? nbytes : 0), rv = brsrc(a.cv, a.cv ? nbytes : 0);
+
+  // Tile-invariant per-thread byte offsets of the staged window entries and epilogue nodes.
+  int soff[C::NSTAGE], noff[C::NMAIN];
+#pragma unroll
+  for (int s = 0; s < C::NSTAGE; ++s) {
+    const int idx = tid + s * C::THREADS;
+    const int rr = idx / C::RY, cc = idx - rr * C::RY;
+    soff[s] = (rr * NY + cc) * 8;
+  }
+#pragma unroll
+  for (int qn = 0; qn < C::NMAIN; ++qn) {
+    const int idx = tid + qn * C::THREADS;
+    const int rl = idx / C::BY, c = idx - rl * C::BY;
+    noff[qn] = (rl * NY + c) * 8;
+  }
+
+  // Issue every global load of tile t (staged x window, u and v of this thread's epilogue nodes).
+  // Entries outside the local lines read 0 (buffer bounds check); entries past the domain's
+  // y-ends wrap into neighbouring lines.  Neither is ever consumed.
   double st[C::NSTAGE], pu[C::NMAIN], pv[C::NMAIN];
   auto issue = [&](int t) {
     const int tx = t / a.tiles_y, ty = t - tx * a.tiles_y;
     const int gx0 = (a.ex_begin + tx * TX) * P, gy0 = ty * TY * P;
+    const int sbase = ((gx0 - P - lb0) * NY + gy0 - P) * 8, nbase = ((gx0 - lb0) * NY + gy0) * 8;
 #pragma unroll
-    for (int s = 0; s < C::NSTAGE; ++s) {
-      const int idx = min(tid + s * C::THREADS, C::RX * C::RY - 1);
-      const int rr = idx / C::RY, cc = idx - rr * C::RY;
-      const int gx = min(max(gx0 - P + rr, lb0), lb1);
-      const int gy = min(max(gy0 - P + cc, 0), NY - 1);
-      st[s] = a.x[(gx - lb0) * NY + gy];
-    }
+    for (int s = 0; s < C::NSTAGE; ++s) st[s] = bload(rx, sbase + soff[s]);
 #pragma unroll
     for (int qn = 0; qn < C::NMAIN; ++qn) {
-      const int idx = tid + qn * C::THREADS;
-      const int rl = idx / C::BY, c = idx - rl * C::BY;
-      const int p = min(max((gx0 + rl - lb0) * NY + gy0 + c, 0), nmax);
-      pu[qn] = a.cu ? a.cu[p] : 1.0;
-      pv[qn] = a.cv ? a.cv[p] : 1.0;
+      pu[qn] = bload(ru, nbase + noff[qn]);
+      pv[qn] = bload(rv, nbase + noff[qn]);
     }
   };
   if (t_begin < t_end) issue(t_begin);
@@ -465,6 +510,10 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
   }
   const double wreg = a.tab[2 * n * n + min(tid, n - 1)];
   bool ws_done = false;
+  // Uniform epilogue factors (absent terms have coefficient 0 and contribute exact zeros).
+  const double fKx = a.cK * a.sx, fKy = a.cK * a.sy, fM = a.cM * a.hxy, fX = a.cX * a.hy, fY = a.cY * a.hx;
+  const bool has_u = a.cu != nullptr, has_v = a.cv != nullptr;
+  SEM_STAMP(1);
 
   for (int t = t_begin; t < t_end; ++t) {
     const int tx = t / a.tiles_y, ty = t - tx * a.tiles_y;
@@ -476,7 +525,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
 #pragma unroll
     for (int s = 0; s < C::NSTAGE; ++s) {
       const int idx = tid + s * C::THREADS;
-      if (idx < C::RX * C::RY) {
+      if ((s + 1) * C::THREADS <= C::RX * C::RY || idx < C::RX * C::RY) {
         const int rr = idx / C::RY, cc = idx - rr * C::RY;
         sm.Ts[rr * C::PT + cc] = st[s];
       }
@@ -488,153 +537,232 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
     double cu_[C::NMAIN], cv_[C::NMAIN];
 #pragma unroll
     for (int qn = 0; qn < C::NMAIN; ++qn) {
-      cu_[qn] = pu[qn];
-      cv_[qn] = pv[qn];
+      cu_[qn] = has_u ? pu[qn] : 1.0;
+      cv_[qn] = has_v ? pv[qn] : 1.0;
     }
+    SEM_STAMP(2);
     __syncthreads();
+    SEM_STAMP(3);
     if (PERSIST && t + 1 < t_end) issue(t + 1);  // next tile's loads fly while this tile computes
 
-    // ---- phases A and B: MFMA wave tasks (K and G chains fused, or split when SPLIT)
+    // ---- phases A and B: each wave owns a homogeneous list of tasks (the first half of the
+    // waves phase A, the rest phase B); it issues every operand read of its tasks first, then
+    // all MFMAs with one independent K and one G accumulator chain per task, then the writes.
+    if (!(a.diag & 1)) {
+      constexpr int NWA = C::NWA, NWB = NW - C::NWA;
+      if (wave < NWA) {
+        constexpr int TW = (C::TA + NWA - 1) / NWA, TG = TW < C::MAXG ? TW : C::MAXG;
 #pragma unroll
-    for (int tt = 0; tt < C::TPW; ++tt) {
-      if (a.diag & 1) break;
-      const int task0 = wave + tt * NW;
-      const int task = SPLIT ? task0 >> 1 : task0;
-      const int part = SPLIT ? (task0 & 1) : 2;  // 0: K only, 1: G only, 2: both
-      if (task0 >= C::NT) continue;
-      if (task < C::TA) {
-        const int e = task / C::NCB, cb = task - e * C::NCB;  // element column e (0 = halo), column block
-        dbl4 accK = {0.0, 0.0, 0.0, 0.0}, accG = {0.0, 0.0, 0.0, 0.0};
+        for (int g0 = 0; g0 < TW; g0 += TG) {
+          double bv[TG][C::KS];
 #pragma unroll
-        for (int s = 0; s < C::KS; ++s) {
-          const int k = 4 * s + lk;
-          double bv = sm.Ts[(e * P + k) * C::PT + P + cb * 16 + lr];
-          if (4 * s + 3 > P) bv = k <= P ? bv : 0.0;  // next element's nodes: keep NaN/Inf out
-          if (part != 1) accK = __builtin_amdgcn_mfma_f64_16x16x4f64(aK[s], bv, accK, 0, 0, 0);
-          if (part != 0) accG = __builtin_amdgcn_mfma_f64_16x16x4f64(aG[s], bv, accG, 0, 0, 0);
-        }
+          for (int tt = 0; tt < TG; ++tt) {
+            const int task = min(wave + (g0 + tt) * NWA, C::TA - 1);
+            const int e = task / C::NCB, cb = task - e * C::NCB;  // element line e (0 = halo), column block
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = lk + 4 * r;  // C/D row of an f64 16x16x4 MFMA: (lane>>4) + 4*reg
-          if (i <= P) {
-            if (part != 1) sm.EK[(e * n + i) * C::EC + cb * 16 + lr] = accK[r];
-            if (part != 0) sm.EG[(e * n + i) * C::EC + cb * 16 + lr] = accG[r];
+            for (int s = 0; s < C::KS; ++s) {
+              const int k = 4 * s + lk;
+              const double v = sm.Ts[(e * P + k) * C::PT + P + cb * 16 + lr];
+              bv[tt][s] = (4 * s + 3 > P && k > P) ? 0.0 : v;  // next element's nodes: keep NaN/Inf out
+            }
+          }
+          dbl4 accK[TG], accG[TG];
+#pragma unroll
+          for (int tt = 0; tt < TG; ++tt) accK[tt] = accG[tt] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+            for (int tt = 0; tt < TG; ++tt) {
+              accK[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(aK[s], bv[tt][s], accK[tt], 0, 0, 0);
+              accG[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(aG[s], bv[tt][s], accG[tt], 0, 0, 0);
+            }
+#pragma unroll
+          for (int tt = 0; tt < TG; ++tt) {
+            const int task = wave + (g0 + tt) * NWA;
+            if (g0 + tt < TW && task < C::TA) {
+              const int e = task / C::NCB, cb = task - e * C::NCB;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int i = lk + 4 * r;  // C/D row of an f64 16x16x4 MFMA: (lane>>4) + 4*reg
+                if (i <= P) {
+                  sm.EK[(e * n + i) * C::EC + cb * 16 + lr] = accK[tt][r];
+                  sm.EG[(e * n + i) * C::EC + cb * 16 + lr] = accG[tt][r];
+                }
+              }
+            }
           }
         }
       } else {
-        const int tb = task - C::TA;
-        const int e = tb / C::NLB, lbk = tb - e * C::NLB;  // element row e (0 = halo), line block
-        dbl4 accK = {0.0, 0.0, 0.0, 0.0}, accG = {0.0, 0.0, 0.0, 0.0};
+        constexpr int TW = (C::TB + NWB - 1) / NWB, TG = TW < C::MAXG ? TW : C::MAXG;
+        const int wb = wave - NWA;
 #pragma unroll
-        for (int s = 0; s < C::KS; ++s) {
-          const int k = 4 * s + lk;
-          double av = sm.Ts[(P + lbk * 16 + lr) * C::PT + e * P + k];
-          if (4 * s + 3 > P) av = k <= P ? av : 0.0;
-          if (part != 1) accK = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aK[s], accK, 0, 0, 0);
-          if (part != 0) accG = __builtin_amdgcn_mfma_f64_16x16x4f64(av, aG[s], accG, 0, 0, 0);
-        }
-        if (lr <= P) {
+        for (int g0 = 0; g0 < TW; g0 += TG) {
+          double av[TG][C::KS];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int line = lbk * 16 + lk + 4 * r;
-            if (part != 1) sm.FK[(e * C::FL + line) * n + lr] = accK[r];
-            if (part != 0) sm.FG[(e * C::FL + line) * n + lr] = accG[r];
+          for (int tt = 0; tt < TG; ++tt) {
+            const int task = min(wb + (g0 + tt) * NWB, C::TB - 1);
+            const int e = task / C::NLB, lbk = task - e * C::NLB;  // element column e (0 = halo), line block
+#pragma unroll
+            for (int s = 0; s < C::KS; ++s) {
+              const int k = 4 * s + lk;
+              const double v = sm.Ts[(P + lbk * 16 + lr) * C::PT + e * P + k];
+              av[tt][s] = (4 * s + 3 > P && k > P) ? 0.0 : v;
+            }
+          }
+          dbl4 accK[TG], accG[TG];
+#pragma unroll
+          for (int tt = 0; tt < TG; ++tt) accK[tt] = accG[tt] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+            for (int tt = 0; tt < TG; ++tt) {
+              accK[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tt][s], aK[s], accK[tt], 0, 0, 0);
+              accG[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tt][s], aG[s], accG[tt], 0, 0, 0);
+            }
+#pragma unroll
+          for (int tt = 0; tt < TG; ++tt) {
+            const int task = wb + (g0 + tt) * NWB;
+            if (g0 + tt < TW && task < C::TB && lr <= P) {
+              const int e = task / C::NLB, lbk = task - e * C::NLB;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int line = lbk * 16 + lk + 4 * r;
+                sm.FK[(e * C::FL + line) * n + lr] = accK[tt][r];
+                sm.FG[(e * C::FL + line) * n + lr] = accG[tt][r];
+              }
+            }
           }
         }
       }
     }
+    SEM_STAMP(4);
     __syncthreads();
+    SEM_STAMP(5);
 
-    // ---- epilogue: one owned node per item, lanes along columns (coalesced global I/O)
+    // ---- epilogue, interior nodes: one node per item, lanes along columns.  For these the
+    // right/upper element always exists and the line is never the partition's closing line.
     const int BXo = (m1 - m0) * P, BYo = (n1 - n0) * P;  // owned without closing line / column
-    const bool lastx = m1 == a.ex_end, lasty = n1 == a.ney;
-    auto node = [&](auto EDGE, int rl, int c, double uu, double vv) {
-      constexpr bool edge = decltype(EDGE)::value;
-      const int gx = gx0 + rl, gy = gy0 + c;
-      const int p = (gx - lb0) * NY + gy;
-      const double xv = sm.Ts[(P + rl) * C::PT + P + c];
-      if (a.diag & 2) {
-        a.y[p] = xv * uu + vv;
-        return;
-      }
-      // x-direction: element column of this line (right) and, at a shared line, the left one
-      const int i = rl % P, ex = rl / P;
-      const int mR = m0 + ex;
-      const bool hasR = mR < a.ex_end, hasLx = i == 0 && mR - 1 >= a.ex_begin;
-      double XK = 0.0, XG = 0.0;
-      if (!edge || c < C::EC) {
-        if (hasLx) {
-          XK = sm.EK[(ex * n + P) * C::EC + c];
-          XG = sm.EG[(ex * n + P) * C::EC + c];
-        }
-        if (hasR) {
-          XK += sm.EK[((ex + 1) * n + i) * C::EC + c];
-          XG += sm.EG[((ex + 1) * n + i) * C::EC + c];
-        }
-      } else {
-        contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl - i) * C::PT + P + c], C::PT, i, hasR, hasLx, XK,
-                            XG);
-      }
-      // y-direction
-      const int j = c % P, ey = c / P;
-      const int nR = n0 + ey;
-      const bool hasRy = nR < a.ney, hasLy = j == 0 && nR - 1 >= 0;
-      double YK = 0.0, YG = 0.0;
-      if (!edge || rl < C::FL) {
-        if (hasLy) {
-          YK = sm.FK[(ey * C::FL + rl) * n + P];
-          YG = sm.FG[(ey * C::FL + rl) * n + P];
-        }
-        if (hasRy) {
-          YK += sm.FK[((ey + 1) * C::FL + rl) * n + j];
-          YG += sm.FG[((ey + 1) * C::FL + rl) * n + j];
-        }
-      } else {
-        contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl) * C::PT + P + c - j], 1, j, hasRy, hasLy, YK,
-                            YG);
-      }
-      const double mx = wsum<P>(gx, a.ex_begin, a.ex_end, sm.ws);
-      const double my = wsum<P>(gy, 0, a.ney, sm.ws);
-      double z = 0.0;
-      if (a.cK != 0.0) z = a.cK * fma(a.sx * my, XK, a.sy * mx * YK);
-      if (a.cM != 0.0) z = fma(a.cM * a.hxy * mx * my, xv, z);
-      if (a.cX != 0.0) z = fma(a.cX * uu, a.hy * my * XG, z);
-      if (a.cY != 0.0) z = fma(a.cY * vv, a.hx * mx * YG, z);
-      if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
-      if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
-      if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
-      if (a.dir_mode != SEM_DIR_NONE) {
-        const bool isd = a.mask ? (a.mask[p] != 0)
-                                : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
-                                   ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
-        if (isd) {
-          // an interface line's Dirichlet row is written by its owner (the right strip) only
-          const bool owner = !(gx == lb1 && a.ex_end < a.nex);
-          if (!owner)
-            z = 0.0;
-          else if (a.dir_mode == SEM_DIR_IDENTITY)
-            z = xv - (a.dval ? a.dval[p] : 0.0);
-          else
-            z = a.dval[p];
-        }
-      }
-      a.y[p] = z;
-    };
+    const int nbase = ((gx0 - lb0) * NY + gy0) * 8;
+    const auto ry = brsrc(a.y, nbytes);
+    const bool leftx = m0 > a.ex_begin, lefty = n0 > 0;
+    const double wP = sm.ws[P];
 #pragma unroll
     for (int qn = 0; qn < C::NMAIN; ++qn) {
       const int idx = tid + qn * C::THREADS;
       const int rl = idx / C::BY, c = idx - rl * C::BY;
-      if (idx < C::BX * C::BY && rl < BXo && c < BYo) node(std::false_type{}, rl, c, cu_[qn], cv_[qn]);
+      if (!((qn + 1) * C::THREADS <= C::BX * C::BY || idx < C::BX * C::BY) || rl >= BXo || c >= BYo) continue;
+      const int off = nbase + noff[qn];
+      const int i = rl % P, ex = rl / P, j = c % P, ey = c / P;
+      const bool hasLx = i == 0 && (ex > 0 || leftx), hasLy = j == 0 && (ey > 0 || lefty);
+      const double xv = sm.Ts[(P + rl) * C::PT + P + c];
+      const double kl = sm.EK[(ex * n + P) * C::EC + c], gl = sm.EG[(ex * n + P) * C::EC + c];
+      const double kr = sm.EK[((ex + 1) * n + i) * C::EC + c], gr = sm.EG[((ex + 1) * n + i) * C::EC + c];
+      const double fkl = sm.FK[(ey * C::FL + rl) * n + P], fgl = sm.FG[(ey * C::FL + rl) * n + P];
+      const double fkr = sm.FK[((ey + 1) * C::FL + rl) * n + j], fgr = sm.FG[((ey + 1) * C::FL + rl) * n + j];
+      const double wi = sm.ws[i], wj = sm.ws[j];
+      if (a.diag & 2) {
+        bstore(ry, off, xv * cu_[qn] + cv_[qn]);
+        continue;
+      }
+      const double XK = hasLx ? kl + kr : kr, XG = hasLx ? gl + gr : gr;
+      const double YK = hasLy ? fkl + fkr : fkr, YG = hasLy ? fgl + fgr : fgr;
+      const double mx = hasLx ? wP + wi : wi, my = hasLy ? wP + wj : wj;
+      double z = fma(fKx * my, XK, fKy * mx * YK);
+      z = fma(fM * mx * my, xv, z);
+      z = fma(fX * cu_[qn], my * XG, z);
+      z = fma(fY * cv_[qn], mx * YG, z);
+      if (a.has_e1) z = fma(a.cE * a.ea[off >> 3], a.eb[off >> 3], z);
+      if (a.has_e2) z = fma(a.cE * a.ec[off >> 3], a.ed[off >> 3], z);
+      if (a.cA != 0.0) z = fma(a.cA, bload(ry, off), z);
+      if (a.dir_mode != SEM_DIR_NONE) {
+        const int gx = gx0 + rl, gy = gy0 + c;
+        const bool isd = a.mask ? (a.mask[off >> 3] != 0)
+                                : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
+                                   ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
+        if (isd) z = a.dir_mode == SEM_DIR_IDENTITY ? xv - (a.dval ? a.dval[off >> 3] : 0.0) : a.dval[off >> 3];
+      }
+      bstore(ry, off, z);
     }
-    auto edge = [&](int rl, int c) {
-      const int p = (gx0 + rl - lb0) * NY + gy0 + c;
-      node(std::true_type{}, rl, c, a.cu ? a.cu[p] : 1.0, a.cv ? a.cv[p] : 1.0);
-    };
-    if (lastx)  // closing line of the local lines
-      for (int c = tid; c < BYo + (lasty ? 1 : 0); c += C::THREADS) edge(BXo, c);
-    if (lasty)  // closing column of the domain
-      for (int rl = tid; rl < BXo; rl += C::THREADS) edge(rl, BYo);
+
+    // ---- epilogue, closing line / column of the local domain (edge tiles only): general path
+    const bool lastx = m1 == a.ex_end, lasty = n1 == a.ney;
+    if (lastx || lasty) {
+      auto edge = [&](int rl, int c) {
+        const int gx = gx0 + rl, gy = gy0 + c;
+        const int p = (gx - lb0) * NY + gy;
+        const double uu = a.cu ? a.cu[p] : 1.0, vv = a.cv ? a.cv[p] : 1.0;
+        const double xv = sm.Ts[(P + rl) * C::PT + P + c];
+        if (a.diag & 2) {
+          a.y[p] = xv * uu + vv;
+          return;
+        }
+        const int i = rl % P, ex = rl / P;
+        const int mR = m0 + ex;
+        const bool hasR = mR < a.ex_end, hasLx = i == 0 && mR - 1 >= a.ex_begin;
+        double XK = 0.0, XG = 0.0;
+        if (c < C::EC) {
+          if (hasLx) {
+            XK = sm.EK[(ex * n + P) * C::EC + c];
+            XG = sm.EG[(ex * n + P) * C::EC + c];
+          }
+          if (hasR) {
+            XK += sm.EK[((ex + 1) * n + i) * C::EC + c];
+            XG += sm.EG[((ex + 1) * n + i) * C::EC + c];
+          }
+        } else {
+          contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl - i) * C::PT + P + c], C::PT, i, hasR, hasLx, XK,
+                              XG);
+        }
+        const int j = c % P, ey = c / P;
+        const int nR = n0 + ey;
+        const bool hasRy = nR < a.ney, hasLy = j == 0 && nR - 1 >= 0;
+        double YK = 0.0, YG = 0.0;
+        if (rl < C::FL) {
+          if (hasLy) {
+            YK = sm.FK[(ey * C::FL + rl) * n + P];
+            YG = sm.FG[(ey * C::FL + rl) * n + P];
+          }
+          if (hasRy) {
+            YK += sm.FK[((ey + 1) * C::FL + rl) * n + j];
+            YG += sm.FG[((ey + 1) * C::FL + rl) * n + j];
+          }
+        } else {
+          contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl) * C::PT + P + c - j], 1, j, hasRy, hasLy, YK,
+                              YG);
+        }
+        const double mx = wsum<P>(gx, a.ex_begin, a.ex_end, sm.ws);
+        const double my = wsum<P>(gy, 0, a.ney, sm.ws);
+        double z = fma(fKx * my, XK, fKy * mx * YK);
+        z = fma(fM * mx * my, xv, z);
+        z = fma(fX * uu, my * XG, z);
+        z = fma(fY * vv, mx * YG, z);
+        if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
+        if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
+        if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
+        if (a.dir_mode != SEM_DIR_NONE) {
+          const bool isd = a.mask ? (a.mask[p] != 0)
+                                  : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
+                                     ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
+          if (isd) {
+            // an interface line's Dirichlet row is written by its owner (the right strip) only
+            const bool owner = !(gx == lb1 && a.ex_end < a.nex);
+            if (!owner)
+              z = 0.0;
+            else if (a.dir_mode == SEM_DIR_IDENTITY)
+              z = xv - (a.dval ? a.dval[p] : 0.0);
+            else
+              z = a.dval[p];
+          }
+        }
+        a.y[p] = z;
+      };
+      if (lastx)  // closing line of the local lines
+        for (int c = tid; c < BYo + (lasty ? 1 : 0); c += C::THREADS) edge(BXo, c);
+      if (lasty)  // closing column of the domain
+        for (int rl = tid; rl < BXo; rl += C::THREADS) edge(rl, BYo);
+    }
   }
+  SEM_STAMP(6);
 }
 
 template <int P, int TX, int TY, int NW, bool PERSIST, bool SPLIT>
@@ -1150,6 +1278,11 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
     return e ? std::atoi(e) : 0;
   }();
   a.diag = diag;
+  static unsigned long long* stamps = [] {
+    const char* e = std::getenv("SEM_DIAG_BUF");  // device address of a stamp buffer (diagnostics)
+    return e ? reinterpret_cast<unsigned long long*>(std::strtoull(e, nullptr, 0)) : nullptr;
+  }();
+  a.stamps = (diag & 8) ? stamps : nullptr;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // AUTO: measured on MI355X (tools/kbench.py) -- the MFMA tile kernel wins on meshes that
   // leave the chip latency-bound (< 2M DOFs), the single-phase column kernel on larger ones.

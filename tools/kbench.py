@@ -35,12 +35,20 @@ def time_graph(fn, reps):
     return best
 
 
+STAMP_BUF = None
+if os.environ.get("SEM_DIAG_BUF") == "auto":  # allocate the stamp buffer before libsemops reads the variable
+    STAMP_BUF = torch.zeros(1 << 22, dtype=torch.int64, device="cuda")
+    os.environ["SEM_DIAG_BUF"] = str(STAMP_BUF.data_ptr())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--algo", type=int, default=0)
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--meshes", default="8:64,12:128,8:256,8:1024,4:512")
     ap.add_argument("--floor", action="store_true", help="also time torch.addcmul (same 32 B/DOF traffic)")
+    ap.add_argument("--stamps", action="store_true",
+                    help="diagnostic: per-wave phase stamps of one apply (needs SEM_DIAG=8 and SEM_DIAG_BUF)")
     ap.add_argument("--dss", type=int, default=0,
                     help="FETCH_SIZE calibration: time sem_dss on an ne x ne, P=8 element array (8-byte loads, "
                          "reads exactly ne^2*81*8 bytes)")
@@ -48,6 +56,49 @@ def main():
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     dev = torch.device("cuda", 0)
+    if a.stamps:
+        import numpy as np
+        buf = STAMP_BUF
+        P, ne = map(int, a.meshes.split(",")[0].split(":"))
+        m = get_mesh(P, ne, ne, 1.0 / ne, 1.0 / ne)
+        T, u, v = (torch.rand(m.n_local, dtype=torch.float64, device=dev) for _ in range(3))
+        y = torch.empty_like(T)
+        kw = dict(c_stiff=1.0, c_gradx=40.0, cu=u, c_grady=40.0, cv=v, dir_mode=_lib.DIR_IDENTITY,
+                  dir_sides=_lib.SIDE_W | _lib.SIDE_E, algo=a.algo)
+        for _ in range(20):
+            m.apply(T, y, **kw)
+        buf.zero_()
+        torch.cuda.synchronize()
+        m.apply(T, y, **kw)
+        torch.cuda.synchronize()
+        st = buf.cpu().numpy().reshape(-1, 8).astype(np.int64)
+        st = st[st[:, 0] > 0]
+        t0 = st[:, 0].min()
+        names = ["start", "loads issued", "staged->LDS", "barrier1", "mfma done", "barrier2", "end"]
+        print(f"{m.kernel_name(a.algo)}: {len(st)} waves; times in shader cycles relative to the first wave start")
+        for k in range(7):
+            col = st[:, k] - t0
+            print(f"  {names[k]:14s} min {col.min():8d} med {int(np.median(col)):8d} max {col.max():8d}")
+        for k in range(1, 7):
+            d = st[:, k] - st[:, k - 1]
+            print(f"  phase {names[k-1]:>14s} -> {names[k]:14s}: med {int(np.median(d)):7d}  p90 {int(np.percentile(d, 90)):7d}")
+        # per-XCD view (each XCD has its own clock): dispatch ramp, wave span, active window
+        xcc = st[:, 7] & 0xF
+        hw = st[:, 7] >> 8  # HW_ID: cu_id [11:8], sh_id [12], se_id [15:13]
+        cu = (xcc << 8) | ((hw >> 8) & 0xFF)
+        win, ramp = [], []
+        for c in sorted(set(cu.tolist())):
+            sc = st[cu == c]
+            win.append(sc[:, 6].max() - sc[:, 0].min())
+            ramp.append(sc[:, 0].max() - sc[:, 0].min())
+        print(f"  per CU ({len(win)} CUs): active window med {int(np.median(win))} max {int(np.max(win))}; "
+              f"start ramp med {int(np.median(ramp))} max {int(np.max(ramp))}; waves/CU {len(st) / len(win):.1f}")
+        for x in sorted(set(xcc.tolist())):
+            sx = st[xcc == x]
+            s0 = sx[:, 0].min()
+            print(f"  xcd {x}: waves {len(sx):5d}  last start {sx[:, 0].max() - s0:7d}  first end {sx[:, 6].min() - s0:7d}"
+                  f"  last end {sx[:, 6].max() - s0:7d}  med span {int(np.median(sx[:, 6] - sx[:, 0])):6d}")
+        return
     if a.dss:
         m = get_mesh(8, a.dss, a.dss, 1.0 / a.dss, 1.0 / a.dss)
         ae = torch.rand((a.dss, a.dss, 9, 9), dtype=torch.float64, device=dev)
