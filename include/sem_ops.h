@@ -61,7 +61,9 @@ enum sem_algo {
   SEM_ALGO_AUTO = 0,
   SEM_ALGO_VALU = 1,   /* two-phase VALU tile kernel (x and y contractions in separate passes)   */
   SEM_ALGO_MFMA = 2,   /* fp64 MFMA (v_mfma_f64_16x16x4_f64) element-block contractions, P <= 15 */
-  SEM_ALGO_COLUMN = 3  /* single-phase VALU column kernel                                         */
+  SEM_ALGO_COLUMN = 3, /* single-phase VALU column kernel                                         */
+  SEM_ALGO_BAND = 4    /* assembled-band VALU kernel: one banded dot product per node and direction,
+                          x / y roles on separate waves, wave-uniform compile-time coefficients   */
 };
 
 typedef struct sem_handle sem_handle;

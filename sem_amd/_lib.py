@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
 DIR_NONE, DIR_IDENTITY, DIR_REPLACE = 0, 1, 2
-ALGO_AUTO, ALGO_VALU, ALGO_MFMA, ALGO_COLUMN = 0, 1, 2, 3
+ALGO_AUTO, ALGO_VALU, ALGO_MFMA, ALGO_COLUMN, ALGO_BAND = 0, 1, 2, 3, 4
 
 _dp = C.POINTER(C.c_double)
 _i64p = C.POINTER(C.c_int64)

@@ -15,8 +15,8 @@ LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libsemops.so")
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["sem_ops.hip", "gll_tables.cpp"]
-HEADERS = ["sem_internal.h", "gll_consts.h", os.path.join("..", "..", "include", "sem_ops.h")]
+SOURCES = ["sem_ops.hip", "apply_band.hip", "gll_tables.cpp"]
+HEADERS = ["sem_internal.h", "gll_consts.h", "apply_common.h", os.path.join("..", "..", "include", "sem_ops.h")]
 
 
 def _hipcc():
@@ -59,11 +59,27 @@ def build(force=False, verbose=False):
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     gen_consts(verbose)
+    hipcc = _hipcc()
+    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-I", os.path.join(ROOT, "include")]
+    objs, procs = [], []
+    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS + [os.path.join("..", "build.py")])
+    for src in SOURCES:  # one hipcc per translation unit, in parallel; unchanged objects are reused
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        if (not force and os.path.exists(obj)
+                and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, src)))):
+            continue
+        cmd = [hipcc] + flags + ["-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((src, subprocess.Popen(cmd)))
+    bad = [src for src, pr in procs if pr.wait() != 0]
+    if bad:
+        raise RuntimeError(f"hipcc failed on {bad}")
     tmp = LIB + ".tmp"
-    cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     return LIB

@@ -1,0 +1,615 @@
+// Banded-assembly apply kernel for gfx950 (SEM_ALGO_BAND).
+//
+// Same operator as the other apply kernels -- the assembled global operators of
+// Solvers/SEM.py (mass :170-183, stiffness :186-203, gradient :206-223, convection
+// :226-245 as contracted at ConvectionDiffusion_Solver.py:82-87,112-119) -- but written
+// against the *assembled* 1-D operators instead of per-element blocks:
+//
+//     (K x)[gx,gy] = (dy/dx) My[gy] sum_k Kx[gx][k] x[k][gy] + (dx/dy) Mx[gx] sum_l Ky[gy][l] x[gx][l]
+//
+// where Kx (resp. Gx) is the 1-D direct-stiffness sum of K_s (G_s) over the element
+// columns holding a line (SEM.py:196-202): row gx of an element-interior node is one row
+// of K_s over that element's P+1 nodes; the row of a node shared by two elements is
+// K_s[P][.] over the left element plus K_s[0][.] over the right one.  Every owned node's
+// result is therefore one banded dot product per direction -- no element halo is
+// recomputed and no element-local results are summed afterwards.
+//
+// One workgroup = one tile of TXE x TYE elements (BX = TXE*P lines, BY = TYE*P columns).
+// Waves have fixed roles, chosen so that every coefficient is wave-uniform (compile-time
+// constants, gll_consts.h) and every global access is coalesced along y:
+//   X waves    lane = column c, wave = (element column a, row split s): the x-direction
+//              rows of element a at column c from a (2P+1)-node window held in registers;
+//              afterwards the epilogue of those nodes (coalesced loads / stores).
+//   Y waves    lane = (line r, element b), wave = column split h: the y-direction rows of
+//              element b on line r from a (2P+1)-node window; results (scaled) -> LDS.
+// The local domain's closing line (x = line_end) and column (y = NY-1) are row / column 0 of a
+// *ghost* element past the last one: tiles run over ncols+1 x ney+1 element positions, and a
+// ghost element contributes only its row / column 0 (left element only).  Every node therefore
+// goes through the same wave-uniform fast path, and the ghost tiles are light.
+// Barriers: staged tile in LDS -> X and Y contractions run concurrently -> X epilogue.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <string>
+
+#include "apply_common.h"
+
+namespace sem {
+
+
+// ---- Even-odd (centro-symmetric) form of one element's rows.
+// G_s is exactly centro-antisymmetric (G[P-i][P-l] = -G[i][l], GLL.py:62-70); K_s is
+// centro-symmetric to rounding (|K[i][l] - K[P-i][P-l]| <= 1.5 ulp), and is used in its symmetrised
+// form Ks = (K + centro(K))/2, a change far below the 1e-13 parity tolerance.  With e_m =
+// t_m + t_{P-m}, o_m = t_m - t_{P-m} (m < (P+1)/2) the rows i and P-i of an element share
+//     E_i = sum_m S_i[m] e_m (+ A[i][P/2] t_{P/2}),  O_i = sum_m D_i[m] o_m,
+//     S_i[m] = (A[i][m] + A[i][P-m])/2,  D_i[m] = (A[i][m] - A[i][P-m])/2,
+// and y_i = E_i + O_i, y_{P-i} = E_i - O_i (K), O_i - E_i (G): about half the multiply-adds and
+// half the coefficient constants of the direct rows.  The shared-node row 0 folds the left
+// element's row P onto row 0 the same way: Ks[0][m] (t_{P+m} + t_{P-m}), G[0][m] (t_{P+m} - t_{P-m}).
+template <int P>
+struct EOC {
+  static constexpr int n = P + 1, H = (P + 1) / 2, c = P / 2, NP = (P - 1) / 2;
+  static constexpr bool EVEN = P % 2 == 0;
+  static constexpr double K(int i, int l) { return GllConst<P>::K[i * n + l]; }
+  static constexpr double G(int i, int l) { return GllConst<P>::G[i * n + l]; }
+  static constexpr double Ks(int i, int l) { return 0.5 * (K(i, l) + K(P - i, P - l)); }
+  static constexpr double SK(int i, int m) { return 0.5 * (Ks(i, m) + Ks(i, P - m)); }
+  static constexpr double DK(int i, int m) { return 0.5 * (Ks(i, m) - Ks(i, P - m)); }
+  static constexpr double SG(int i, int m) { return 0.5 * (G(i, m) + G(i, P - m)); }
+  static constexpr double DG(int i, int m) { return 0.5 * (G(i, m) - G(i, P - m)); }
+};
+
+// Work items of an element's rows, split over NS threads: item 0 = row 0, item i in [1, NP] =
+// the mirror pair (i, P-i), item -1 = the centre row P/2 (even P).  Split 0 takes row 0 and the
+// even pairs, split 1 the odd pairs and the centre (NS = 2); NS = 1 takes everything.
+template <int P, int NS>
+struct EPlan {
+  static constexpr int NP = EOC<P>::NP;
+  static constexpr bool EVEN = EOC<P>::EVEN;
+  static constexpr bool in_split(int it, int s) {
+    return NS == 1 ? true : (it == 0 ? s == 0 : it < 0 ? s == 1 : (it % 2 == 0) == (s == 0));
+  }
+  static constexpr int code(int k) { return k == 0 ? 0 : (k <= NP ? k : -1); }  // k-th item overall
+  static constexpr int NITEMS = 1 + NP + (EVEN ? 1 : 0);
+  static constexpr int size(int it) { return it > 0 ? 2 : 1; }
+  static constexpr int nrows(int s) {
+    int r = 0;
+    for (int k = 0; k < NITEMS; ++k)
+      if (in_split(code(k), s)) r += size(code(k));
+    return r;
+  }
+  // first slot of item k within split s
+  static constexpr int slot(int s, int k) {
+    int r = 0;
+    for (int q = 0; q < k; ++q)
+      if (in_split(code(q), s)) r += size(code(q));
+    return r;
+  }
+  static constexpr int row(int s, int sl) {  // element-local row of slot sl of split s
+    for (int k = 0; k < NITEMS; ++k) {
+      const int it = code(k);
+      if (!in_split(it, s)) continue;
+      const int f = slot(s, k);
+      if (sl == f) return it == 0 ? 0 : (it < 0 ? P / 2 : it);
+      if (it > 0 && sl == f + 1) return P - it;
+    }
+    return 0;
+  }
+  static constexpr int NRMAX = nrows(0) > nrows(NS - 1) ? nrows(0) : nrows(NS - 1);
+  static constexpr bool needs_left(int s) { return in_split(0, s); }
+  static constexpr bool needs_eo(int s) {
+    for (int k = 1; k < NITEMS; ++k)
+      if (in_split(code(k), s)) return true;
+    return false;
+  }
+};
+
+// Rows of split S of one element from a (2P+1)-node window t (t[P..2P] = the element, t[0..P] = the
+// left neighbour; absent elements are zero in the staged tile).  fk = hasL + hasR and
+// fg = hasR - hasL weight the shared node t[P] in row 0.  Results go to slots (EPlan order).
+template <int P, int NS, int S, int NR>
+__device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk, double fg, double (&k)[NR],
+                                        double (&g)[NR]) {
+  using E = EOC<P>;
+  using L = EPlan<P, NS>;
+  constexpr int H = E::H;
+  double e[H], o[H];
+  if constexpr (L::needs_eo(S)) {
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+      e[m] = t[P + m] + t[2 * P - m];
+      o[m] = t[P + m] - t[2 * P - m];
+    }
+  }
+  for_rows(std::make_integer_sequence<int, L::NITEMS>{}, [&](auto KI) {
+    constexpr int kk = decltype(KI)::value;
+    constexpr int it = L::code(kk);
+    if constexpr (L::in_split(it, S)) {
+      constexpr int sl = L::slot(S, kk);
+      if constexpr (it == 0) {  // shared-node row 0 (+ the left element's row P)
+        constexpr double k00 = E::Ks(0, 0), g00 = E::G(0, 0);
+        double kv = (k00 * fk) * t[P], gv = (g00 * fg) * t[P];
+        for_rows(std::make_integer_sequence<int, P>{}, [&](auto MI) {
+          constexpr int m = decltype(MI)::value + 1;
+          constexpr double km = E::Ks(0, m), gm = E::G(0, m);
+          kv = fma(km, t[P + m] + t[P - m], kv);
+          gv = fma(gm, t[P + m] - t[P - m], gv);
+        });
+        k[sl] = kv;
+        g[sl] = gv;
+      } else if constexpr (it > 0) {  // mirror pair (it, P-it)
+        double Ek = 0.0, Ok = 0.0, Eg = 0.0, Og = 0.0;
+        for_rows(std::make_integer_sequence<int, H>{}, [&](auto MI) {
+          constexpr int m = decltype(MI)::value;
+          constexpr double sk = E::SK(it, m), dk = E::DK(it, m), sg = E::SG(it, m), dg = E::DG(it, m);
+          Ek = fma(sk, e[m], Ek);
+          Ok = fma(dk, o[m], Ok);
+          Eg = fma(sg, e[m], Eg);
+          Og = fma(dg, o[m], Og);
+        });
+        if constexpr (E::EVEN) {
+          constexpr double kc_ = E::Ks(it, E::c), gc_ = E::G(it, E::c);
+          Ek = fma(kc_, t[P + E::c], Ek);
+          Eg = fma(gc_, t[P + E::c], Eg);
+        }
+        k[sl] = Ek + Ok;
+        k[sl + 1] = Ek - Ok;
+        g[sl] = Eg + Og;
+        g[sl + 1] = Og - Eg;
+      } else {  // centre row P/2: Ks symmetric, G antisymmetric about it
+        double kv = 0.0, gv = 0.0;
+        for_rows(std::make_integer_sequence<int, H>{}, [&](auto MI) {
+          constexpr int m = decltype(MI)::value;
+          constexpr double sk = E::SK(E::c, m), dg = E::DG(E::c, m);
+          kv = fma(sk, e[m], kv);
+          gv = fma(dg, o[m], gv);
+        });
+        constexpr double kcc = E::Ks(E::c, E::c), gcc = E::G(E::c, E::c);
+        kv = fma(kcc, t[P + E::c], kv);
+        if constexpr (gcc != 0.0) gv = fma(gcc, t[P + E::c], gv);
+        k[sl] = kv;
+        g[sl] = gv;
+      }
+    }
+  });
+}
+
+template <int P, int TXE, int TYE, int RS, int YS>
+struct BCfg {
+  static constexpr int n = P + 1;
+  static constexpr int BX = TXE * P, BY = TYE * P;      // lines / columns of the tile's element positions
+  static constexpr int XW = (BY + 63) / 64;             // waves per X group (a, s)
+  static constexpr int RP = EPlan<P, RS>::NRMAX;        // rows per X thread (at most)
+  static constexpr int NXW = TXE * RS * XW;             // X waves
+  static constexpr int YL = BX * TYE;                   // Y lanes per column split
+  static constexpr int YW = (YL + 63) / 64;
+  static constexpr int JP = EPlan<P, YS>::NRMAX;        // columns per Y thread (at most)
+  static constexpr int NYW = YS * YW;                   // Y waves
+  static constexpr int NW = NXW + NYW;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int RX = BX + P + 1, RY = BY + P + 1;  // staged lines [gx0-P, gx0+BX] x cols [gy0-P, gy0+BY]
+  static constexpr int PT = RY | 1;                     // odd pitch
+  static constexpr int PY = BY | 1;
+  static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
+  static_assert(RS >= 1 && RS <= 2 && YS >= 1 && YS <= 2 && (P >= 2 || (RS == 1 && YS == 1)), "1 or 2 splits");
+  static_assert(THREADS <= 1024, "workgroup too large");
+};
+
+// Kernel arguments of the band kernel: compact, the fields every wave needs first at the
+// front (two s_load_dwordx16 fetch them), all epilogue factors fused on the host.  Every field
+// is read once at kernel entry; a kernarg load sunk into a later phase is a full memory round
+// trip on that phase's critical path.
+struct BandArgs {
+  const double* x;
+  double* y;
+  const double* cu;
+  const double* cv;
+  double fKx, fKy, fM, fX, fY;  // cK*dy/dx, cK*dx/dy, cM*dx*dy/4, cX*dy/2, cY*dx/2
+  int NY, lb0, lb1, ex_begin, ex_end, ney, nex, NXg, tiles_y, nbytes, dir_mode, diag;
+  unsigned sides, flags;  // flags: 1 = cu given, 2 = cv given
+  int nblk, pad_;         // grid size (gridDim would be a second, dependent kernarg fetch)
+  // FULL kernels only
+  const double* ea;
+  const double* eb;
+  const double* ec;
+  const double* ed;
+  const double* dval;
+  const uint8_t* mask;
+  double cE, cA;
+  int has_e1, has_e2;
+  unsigned long long* stamps;  // SEM_DIAG bit 8
+};
+
+// Pin a kernel argument to kernel entry (an empty asm use keeps the compiler from sinking
+// or rematerialising its s_load into a later phase).
+#define BPIN(v) asm volatile("" ::"s"(v))
+
+// Per-node operands of the optional terms (extra pairs, accumulate, Dirichlet mask / values).
+// FULL kernels load them in the prologue with the tile, so the epilogue issues no load: on
+// gfx950 vmcnt counts stores too, and a load-dependent wait between the epilogue's stores would
+// serialise them behind the stores' completion.
+struct NodeOps {
+  double ea, eb, ec, ed, ya, dv;
+  unsigned mk;
+};
+
+__device__ __forceinline__ NodeOps load_node_ops(const BandArgs& a, int p) {
+  const int nb = a.nbytes;
+  NodeOps o;
+  o.ea = bload(brsrc(a.ea, a.has_e1 ? nb : 0), p * 8);
+  o.eb = bload(brsrc(a.eb, a.has_e1 ? nb : 0), p * 8);
+  o.ec = bload(brsrc(a.ec, a.has_e2 ? nb : 0), p * 8);
+  o.ed = bload(brsrc(a.ed, a.has_e2 ? nb : 0), p * 8);
+  o.ya = bload(brsrc(a.y, a.cA != 0.0 ? nb : 0), p * 8);
+  o.dv = bload(brsrc(a.dval, a.dval ? nb : 0), p * 8);
+  o.mk = __builtin_amdgcn_raw_buffer_load_b8(brsrc(a.mask, a.mask ? nb / 8 : 0), p, 0, 0);
+  return o;
+}
+
+// Operator value z of one node -> + extra / accumulate terms, Dirichlet rows (no memory access).
+template <bool FULL>
+__device__ __forceinline__ double finish_node(const BandArgs& a, const NodeOps& o, int gx, int gy, double xv,
+                                              double z) {
+  if constexpr (FULL) {
+    if (a.has_e1) z = fma(a.cE * o.ea, o.eb, z);
+    if (a.has_e2) z = fma(a.cE * o.ec, o.ed, z);
+    if (a.cA != 0.0) z = fma(a.cA, o.ya, z);
+  }
+  if (a.dir_mode != SEM_DIR_NONE) {
+    const bool side = ((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
+                      ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1);
+    bool isd = side;
+    if constexpr (FULL) isd = a.mask ? (o.mk & 0xff) != 0 : side;
+    if (isd) {
+      // an interface line's Dirichlet row is written by its owner (the right strip) only
+      const bool owner = !(gx == a.lb1 && a.ex_end < a.nex);
+      const double dv = FULL ? o.dv : 0.0;
+      if (!owner)
+        z = 0.0;
+      else if (a.dir_mode == SEM_DIR_IDENTITY)
+        z = xv - dv;
+      else
+        z = dv;
+    }
+  }
+  return z;
+}
+
+// GLL weight w_J of order P for a runtime J (compile-time constants, no memory access).
+template <int P>
+__device__ __forceinline__ double gll_w(int J) {
+  double r = 0.0;
+  for_rows(std::make_integer_sequence<int, P + 1>{}, [&](auto K) {
+    constexpr int k = decltype(K)::value;
+    if (J == k) r = GllConst<P>::w[k];
+  });
+  return r;
+}
+
+// FULL = false: no extra / accumulate terms, no Dirichlet mask or values (side bits only).
+template <int P, int TXE, int TYE, int RS, int YS, bool FULL>
+__global__ __launch_bounds__((BCfg<P, TXE, TYE, RS, YS>::THREADS)) void apply_band(const BandArgs a) {
+  using C = BCfg<P, TXE, TYE, RS, YS>;
+  constexpr int n = C::n, BX = C::BX, BY = C::BY, PT = C::PT, PY = C::PY;
+  __shared__ double Ts[C::RX * PT];
+  __shared__ double YK[BX * PY];
+  __shared__ double YG[BX * PY];
+  __shared__ double ws[n];
+
+  BPIN(a.x);
+  BPIN(a.y);
+  BPIN(a.cu);
+  BPIN(a.cv);
+  BPIN(a.fKx);
+  BPIN(a.fKy);
+  BPIN(a.fM);
+  BPIN(a.fX);
+  BPIN(a.fY);
+  BPIN(a.NY);
+  BPIN(a.lb0);
+  BPIN(a.lb1);
+  BPIN(a.ex_begin);
+  BPIN(a.ex_end);
+  BPIN(a.ney);
+  BPIN(a.nex);
+  BPIN(a.NXg);
+  BPIN(a.tiles_y);
+  BPIN(a.nbytes);
+  BPIN(a.dir_mode);
+  BPIN(a.diag);
+  BPIN(a.sides);
+  BPIN(a.flags);
+  BPIN(a.stamps);
+  BPIN(a.nblk);
+
+  // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
+  // tiles (y fastest) and neighbouring tiles share their halo lines through that XCD's L2.
+  const int nb = a.nblk, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nb >> 3, rem = nb & 7;
+  const int L = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (bid >> 3);
+  const int tx = L / a.tiles_y, ty = L - tx * a.tiles_y;
+
+  const int lb0 = a.lb0, NY = a.NY;
+  // element positions [m0, m1) x [n0, n1); position ex_end (ney) is the ghost holding the closing line (column)
+  const int m0 = a.ex_begin + tx * TXE, m1 = min(m0 + TXE, a.ex_end + 1);
+  const int n0 = ty * TYE, n1 = min(n0 + TYE, a.ney + 1);
+  const int gx0 = m0 * P, gy0 = n0 * P;
+  const int rows_ok = (min(m1, a.ex_end) - m0) * P + (m1 > a.ex_end ? 1 : 0);  // valid lines of the tile
+  const int cols_ok = (min(n1, a.ney) - n0) * P + (n1 > a.ney ? 1 : 0);       // valid columns
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // Diagnostics (SEM_DIAG bit 8): s_memtime phase stamps held in SGPRs, written at the very end
+  // so that no diagnostic store sits in the vmcnt queue of the measured phases.
+  unsigned long long stv[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0, rt1 = 0;
+  if (a.stamps) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
+#define BSTAMP(k)                                                                      \
+  do {                                                                                 \
+    if (a.stamps) {                                                                    \
+      __builtin_amdgcn_sched_barrier(0);                                               \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stv[k])::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                               \
+    }                                                                                  \
+  } while (0)
+  BSTAMP(0);
+
+  const int nbytes = a.nbytes;
+  const bool has_u = a.flags & 1, has_v = a.flags & 2;
+  const auto rx = brsrc(a.x, nbytes), ru = brsrc(a.cu, has_u ? nbytes : 0), rv = brsrc(a.cv, has_v ? nbytes : 0);
+  const auto ry = brsrc(a.y, nbytes);
+  const int nodeb = (gx0 - lb0) * NY + gy0;  // local DOF index of the tile's first node
+
+  // ---- issue every global load first, in the order they are consumed (vmcnt retires in order):
+  // the staged x window, then u, v of this thread's epilogue nodes.  Buffer bounds make lines
+  // outside the local range read 0; columns past the domain's y-ends wrap into neighbouring
+  // lines.  Neither is ever consumed.
+  const int sbase = (a.diag & 64) ? -(1 << 30) : ((gx0 - P - lb0) * NY + gy0 - P) * 8;  // diag 64: no staging loads
+  double st[C::NSTAGE];
+#pragma unroll
+  for (int s = 0; s < C::NSTAGE; ++s) {
+    const int idx = min(tid + s * C::THREADS, C::RX * C::RY - 1);
+    const int rr = idx / C::RY, cc = idx - rr * C::RY;
+    st[s] = bload(rx, sbase + (rr * NY + cc) * 8);
+  }
+  // X role: (element position xa, row split xs, column xc)
+  const int xg = w / C::XW;
+  const int xa = xg / RS, xs = xg - xa * RS;
+  const int xc = (w - xg * C::XW) * 64 + lane;
+  const bool xghost = m0 + xa == a.ex_end;                       // wave-uniform
+  const bool xact = w < C::NXW && xa < m1 - m0 && xc < cols_ok && (!xghost || xs == 0);
+  // Issued by every wave (uniform vmcnt bookkeeping, so the staging writes below wait for the
+  // staging loads only); the Y waves' offsets are out of bounds and touch no memory.
+  using XPlan = EPlan<P, RS>;
+  double pu[C::RP], pv[C::RP];
+  int prow[C::RP];  // element-local row of each slot (wave-uniform)
+  NodeOps ops[C::RP] = {};
+  const int pbase = w < C::NXW && !(a.diag & 32) ? nodeb + xa * P * NY + xc : -(1 << 28);
+#pragma unroll
+  for (int k = 0; k < C::RP; ++k) {
+    prow[k] = xs == 0 ? XPlan::row(0, k) : XPlan::row(RS - 1, k);
+    pu[k] = bload(ru, (pbase + prow[k] * NY) * 8);
+    pv[k] = bload(rv, (pbase + prow[k] * NY) * 8);
+  }
+  if constexpr (FULL) {
+#pragma unroll
+    for (int k = 0; k < C::RP; ++k) ops[k] = load_node_ops(a, pbase + prow[k] * NY);
+  }
+
+  // ---- LDS: staged window, weights
+  if (tid < n) ws[tid] = gll_w<P>(tid);
+#pragma unroll
+  for (int s = 0; s < C::NSTAGE; ++s) {
+    const int idx = tid + s * C::THREADS;
+    if ((s + 1) * C::THREADS <= C::RX * C::RY || idx < C::RX * C::RY) {
+      const int rr = idx / C::RY, cc = idx - rr * C::RY;
+      const int gy = gy0 - P + cc;  // columns outside the domain are staged as 0 (absent elements)
+      Ts[rr * PT + cc] = (gy >= 0 && gy < NY) ? st[s] : 0.0;
+    }
+  }
+  BSTAMP(1);
+  __syncthreads();
+  BSTAMP(2);
+
+  constexpr double w0 = GllConst<P>::w[0], wP = GllConst<P>::w[P];
+  const bool hasLx = m0 + xa - 1 >= a.ex_begin;  // X role: left element of position xa (wave-uniform)
+
+  double XK[C::RP], XG[C::RP], XV[C::RP];
+  if (w < C::NXW) {
+    // ---- X contractions: the rows of split xs of element position xa at column xc.  Lines
+    // outside the local range are staged as 0, so absent elements contribute nothing.
+    const double fk = (hasLx ? 1.0 : 0.0) + (xghost ? 0.0 : 1.0), fg = (xghost ? 0.0 : 1.0) - (hasLx ? 1.0 : 0.0);
+    for_rows(std::make_integer_sequence<int, RS>{}, [&](auto S) {
+      constexpr int s = decltype(S)::value;
+      if (xs != s) return;
+      double t[2 * P + 1];
+      constexpr int q0 = XPlan::needs_left(s) ? 0 : P;  // only row 0 reads the left element
+#pragma unroll
+      for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[(xa * P + qq) * PT + P + xc];
+#pragma unroll
+      for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
+      eo_rows<P, RS, s>(t, fk, fg, XK, XG);
+#pragma unroll
+      for (int k = 0; k < C::RP; ++k) XV[k] = t[P + XPlan::row(s, k)];
+    });
+  } else {
+    // ---- Y contractions: the columns of split h of element position b on line r -> LDS,
+    // scaled by Mx of the line.  Columns outside the domain are staged as 0.
+    using YPlan = EPlan<P, YS>;
+    const int wy = w - C::NXW;
+    const int h = wy / C::YW;
+    const int t2 = (wy - h * C::YW) * 64 + lane;
+    const int r = t2 % BX, b = t2 / BX;
+    if (t2 < C::YL && r < rows_ok && b < n1 - n0) {
+      const bool hasLy = n0 + b - 1 >= 0, hasRy = n0 + b < a.ney;
+      const double fk = (hasLy ? 1.0 : 0.0) + (hasRy ? 1.0 : 0.0), fg = (hasRy ? 1.0 : 0.0) - (hasLy ? 1.0 : 0.0);
+      const int i = r % P, ex = m0 + r / P;
+      const double mx = i != 0 ? ws[i] : (ex - 1 >= a.ex_begin ? wP : 0.0) + (ex < a.ex_end ? w0 : 0.0);
+      const double sk = a.fKy * mx, sg = a.fY * mx;
+      for_rows(std::make_integer_sequence<int, YS>{}, [&](auto H) {
+        constexpr int hh = decltype(H)::value;
+        if (h != hh) return;
+        double t[2 * P + 1];
+        constexpr int q0 = YPlan::needs_left(hh) ? 0 : P;
+#pragma unroll
+        for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[(P + r) * PT + b * P + qq];
+#pragma unroll
+        for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
+        double k[C::JP], g[C::JP];
+        eo_rows<P, YS, hh>(t, fk, fg, k, g);
+#pragma unroll
+        for (int q = 0; q < YPlan::nrows(hh); ++q) {
+          const int j = YPlan::row(hh, q);
+          YK[r * PY + b * P + j] = sk * k[q];
+          YG[r * PY + b * P + j] = sg * g[q];
+        }
+      });
+    }
+  }
+  BSTAMP(3);
+  __syncthreads();
+  BSTAMP(4);
+
+  // ---- X epilogue: combine with the y-direction results, pointwise terms, store (coalesced)
+  if (xact) {
+    const int j = xc % P, ey = n0 + xc / P;
+    const double my = j != 0 ? ws[j] : (ey - 1 >= 0 ? wP : 0.0) + (ey < a.ney ? w0 : 0.0);
+    const int nr = xghost ? 1 : (xs == 0 ? XPlan::nrows(0) : XPlan::nrows(RS - 1));  // a ghost holds row 0 only
+    double zz[C::RP];
+#pragma unroll
+    for (int k = 0; k < C::RP; ++k) {
+      const int i = prow[k];  // element-local row (wave-uniform)
+      const int rl = xa * P + i;
+      const double mx = i != 0 ? ws[i] : (hasLx ? wP : 0.0) + (xghost ? 0.0 : w0);
+      const double u_ = has_u ? pu[k] : 1.0, v_ = has_v ? pv[k] : 1.0;
+      double z = fma(a.fKx * my, XK[k], YK[rl * PY + xc]);
+      z = fma(a.fM * mx * my, XV[k], z);
+      z = fma(a.fX * u_, my * XG[k], z);
+      z = fma(v_, YG[rl * PY + xc], z);
+      zz[k] = finish_node<FULL>(a, ops[k], gx0 + rl, gy0 + xc, XV[k], z);
+    }
+#pragma unroll
+    for (int k = 0; k < C::RP; ++k)
+      if (k < nr && !(a.diag & 16)) bstore(ry, (pbase + prow[k] * NY) * 8, zz[k]);  // diag 16: no stores (timing)
+  }
+  BSTAMP(5);
+  if (a.stamps) {
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1)::"memory");
+    unsigned xcc_, hw_;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)" : "=s"(xcc_), "=s"(hw_));
+    if (lane == 0) {  // 16 slots per wave: 0-5 s_memtime phases, 6 tile, 7 hw id, 8-9 s_memrealtime start/end
+      unsigned long long* o = a.stamps + (blockIdx.x * C::NW + w) * 16;
+      for (int k = 0; k < 6; ++k) o[k] = stv[k];
+      o[6] = L;
+      o[7] = (static_cast<unsigned long long>(hw_) << 8) | (xcc_ & 0xf);
+      o[8] = rt0;
+      o[9] = rt1;
+    }
+  }
+#undef BSTAMP
+}
+
+static int hip_check_b(hipError_t e, const char* what) {
+  if (e == hipSuccess) return SEM_OK;
+  return set_error(SEM_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <int P, int TXE, int TYE, int RS, int YS>
+static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
+  using C = BCfg<P, TXE, TYE, RS, YS>;
+  const int ncols = h->ex_end - h->ex_begin;
+  const int tiles_x = (ncols + 1 + TXE - 1) / TXE;  // + the ghost position of the closing line
+  const int tiles_y = (h->ney + 1 + TYE - 1) / TYE;
+  const long long nblk = static_cast<long long>(tiles_x) * tiles_y;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
+  BandArgs b{};
+  b.x = g.x;
+  b.y = g.y;
+  b.cu = g.cu;
+  b.cv = g.cv;
+  b.fKx = g.cK * g.sx;
+  b.fKy = g.cK * g.sy;
+  b.fM = g.cM * g.hxy;
+  b.fX = g.cX * g.hy;
+  b.fY = g.cY * g.hx;
+  b.NY = static_cast<int>(g.NY);
+  b.lb0 = static_cast<int>(g.line_begin);
+  b.lb1 = static_cast<int>(g.line_end);
+  b.ex_begin = g.ex_begin;
+  b.ex_end = g.ex_end;
+  b.ney = g.ney;
+  b.nex = g.nex;
+  b.NXg = static_cast<int>(g.NXg);
+  b.tiles_y = tiles_y;
+  b.nbytes = g.n_local32 * 8;
+  b.dir_mode = g.dir_mode;
+  b.diag = g.diag;
+  b.sides = g.sides;
+  b.flags = (g.cu ? 1u : 0u) | (g.cv ? 2u : 0u);
+  b.ea = g.ea;
+  b.eb = g.eb;
+  b.ec = g.ec;
+  b.ed = g.ed;
+  b.dval = g.dval;
+  b.mask = g.mask;
+  b.cE = g.cE;
+  b.cA = g.cA;
+  b.has_e1 = g.has_e1;
+  b.has_e2 = g.has_e2;
+  b.stamps = g.stamps;
+  b.nblk = static_cast<int>(nblk);
+  const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
+  if (full)
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, RS, YS, true>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
+                       s, b);
+  else
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, RS, YS, false>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
+                       s, b);
+  return hip_check_b(hipGetLastError(), "apply (band) launch");
+}
+
+// Tile shape per order: ~64 columns (TYE = 64/P elements) so an X wave spans one tile row;
+// TXE element columns so a tile holds ~1024 nodes; row / column splits of 2 for even P.
+template <int P>
+struct BandShape {
+  static constexpr int TYE = (64 / P) > 0 ? 64 / P : 1;
+  static constexpr int TXE = (8 / P) > 4 ? 4 : ((8 / P) > 0 ? 8 / P : 1);
+  static constexpr int RS = P >= 2 ? 2 : 1;
+  static constexpr int YS = RS;
+};
+
+template <int P>
+static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
+  using S = BandShape<P>;
+  static const int force = [] {
+    const char* e = std::getenv("SEM_BAND_TILE");  // tuning override
+    return e ? std::atoi(e) : 0;
+  }();
+  if constexpr (P == 8) {
+    if (force == 1) return launch_band<P, 2, S::TYE, S::RS, S::YS>(args, h, s);
+    if (force == 2) return launch_band<P, 1, S::TYE, 1, 1>(args, h, s);
+  }
+  return launch_band<P, S::TXE, S::TYE, S::RS, S::YS>(args, h, s);
+}
+
+std::string band_kernel_name(int P) {
+  const int TYE = std::max(1, 64 / P), TXE = std::min(4, std::max(1, 8 / P));
+  const int RS = P >= 2 ? 2 : 1;
+  return "sem::apply_band<" + std::to_string(P) + ", " + std::to_string(TXE) + ", " + std::to_string(TYE) + ", " +
+         std::to_string(RS) + ", " + std::to_string(RS) + ">";
+}
+
+int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s) {
+  switch (h->P) {
+#define SEM_BCASE(PP) \
+  case PP:            \
+    return launch_band_auto<PP>(a, h, s);
+    SEM_BCASE(1) SEM_BCASE(2) SEM_BCASE(3) SEM_BCASE(4) SEM_BCASE(5) SEM_BCASE(6) SEM_BCASE(7) SEM_BCASE(8)
+    SEM_BCASE(9) SEM_BCASE(10) SEM_BCASE(11) SEM_BCASE(12) SEM_BCASE(13) SEM_BCASE(14) SEM_BCASE(15) SEM_BCASE(16)
+#undef SEM_BCASE
+    default:
+      return set_error(SEM_EUNSUPPORTED, "polynomial order outside compiled range");
+  }
+}
+
+}  // namespace sem

@@ -33,10 +33,12 @@
 #include <string>
 #include <vector>
 
-#include "gll_consts.h"
-#include "sem_internal.h"
+#include "apply_common.h"
 
 namespace sem {
+
+int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s);  // apply_band.hip
+std::string band_kernel_name(int P);
 
 static int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) return SEM_OK;
@@ -44,30 +46,6 @@ static int hip_check(hipError_t e, const char* what) {
 }
 
 // --------------------------------------------------------------------------- apply kernel
-
-struct ApplyArgs {
-  const double* x;
-  double* y;
-  const double* cu;
-  const double* cv;
-  const double* ea;
-  const double* eb;
-  const double* ec;
-  const double* ed;
-  const uint8_t* mask;
-  const double* dval;
-  const double* tab;  // K_s | G_s | w
-  double cM, cK, cX, cY, cE, cA;
-  double sx, sy, hx, hy, hxy;  // dy/dx, dx/dy, dx/2, dy/2, dx*dy/4
-  int64_t NY, NXg, line_begin, line_end;
-  int nex, ney, ex_begin, ex_end;
-  int tiles_x, tiles_y, dir_mode;
-  unsigned sides;
-  int has_e1, has_e2;
-  int n_local32;  // local vector length (MFMA path: < 2^31)
-  int diag;       // ablation bits for performance diagnosis (SEM_DIAG env); 0 in production
-  unsigned long long* stamps;  // SEM_DIAG bit 8: per-wave s_memtime phase stamps (diagnostic builds only)
-};
 
 template <int P>
 struct TileCfg {
@@ -84,57 +62,6 @@ struct TileCfg {
   static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;  // staging loads per thread
   static_assert(TX * BY <= THREADS && TY * BX <= THREADS, "one phase item per thread");
 };
-
-// Sum of GLL weights of the elements in [e_lo, e_hi) that hold 1-D node g.
-__device__ __forceinline__ double weight_sum(int64_t g, int P, int e_lo, int e_hi, const double* w) {
-  const int64_t e = g / P;
-  const int i = static_cast<int>(g - e * P);
-  if (i != 0) return w[i];
-  double s = 0.0;
-  if (e - 1 >= e_lo && e - 1 < e_hi) s += w[P];
-  if (e >= e_lo && e < e_hi) s += w[0];
-  return s;
-}
-
-// One element's K_s / G_s contraction for output row `row` from a (2P+1)-window t
-// (t[P..2P] = this element's nodes, t[0..P] = the left neighbour's, used at row 0).
-// The K_s / G_s coefficients are compile-time constants (gll_consts.h, generated from the same
-// host code that builds each handle's tables).  They are read through template indices into
-// constexpr locals, so every coefficient is folded into the instruction stream: the
-// contraction issues no table loads (a constexpr *array* indexed in a loop is emitted as a
-// global and re-fetched with serialised scalar loads).
-template <int P, int I>
-__device__ __forceinline__ constexpr double kc() {
-  constexpr double v = GllConst<P>::K[I];
-  return v;
-}
-template <int P, int I>
-__device__ __forceinline__ constexpr double gc() {
-  constexpr double v = GllConst<P>::G[I];
-  return v;
-}
-
-template <int P, int ROW, int... L>
-__device__ __forceinline__ void row_dot(const double* t, double& k, double& g, std::integer_sequence<int, L...>) {
-  ((k = fma(kc<P, ROW * (P + 1) + L>(), t[L], k), g = fma(gc<P, ROW * (P + 1) + L>(), t[L], g)), ...);
-}
-
-// One element's K_s / G_s contraction for output row ROW from a (2P+1)-window t
-// (t[P..2P] = this element's nodes, t[0..P] = the left neighbour's, used at row 0).
-template <int P, int ROW>
-__device__ __forceinline__ void contract_row(const double (&t)[2 * P + 1], bool hasL, double& k, double& g) {
-  using Seq = std::make_integer_sequence<int, P + 1>;
-  k = 0.0;
-  g = 0.0;
-  if (ROW == 0 && hasL) row_dot<P, P>(t, k, g, Seq{});
-  row_dot<P, ROW>(t + P, k, g, Seq{});
-}
-
-// Compile-time loop over output rows 0..P: f(std::integral_constant<int, ROW>).
-template <int... R, class F>
-__device__ __forceinline__ void for_rows(std::integer_sequence<int, R...>, F&& f) {
-  (f(std::integral_constant<int, R>{}), ...);
-}
 
 // Phase B item: y-direction contractions of element row `ae` on owned line r (lanes along lines).
 template <int P>
@@ -374,65 +301,6 @@ struct MSmem {
   double ws[C::n];
 };
 
-// Diagnostic phase stamp (SEM_DIAG bit 8): lane 0 of each wave records s_memtime.
-#define SEM_STAMP(k)                                                                      \
-  do {                                                                                    \
-    if (a.stamps) {                                                                       \
-      unsigned long long t_;                                                              \
-      __builtin_amdgcn_sched_barrier(0);                                                  \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
-      __builtin_amdgcn_sched_barrier(0);                                                  \
-      if ((threadIdx.x & 63) == 0) a.stamps[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
-    }                                                                                     \
-  } while (0)
-
-// Sum of GLL weights of the elements in [e_lo, e_hi) that hold 1-D node g (32-bit, P compile-time).
-template <int P>
-__device__ __forceinline__ double wsum(int g, int e_lo, int e_hi, const double* w) {
-  const int e = g / P, i = g - e * P;
-  const double wi = w[i], wP = w[P], w0 = w[0];  // unconditional reads: no per-lane branch
-  return i != 0 ? wi : (e - 1 >= e_lo && e - 1 < e_hi ? wP : 0.0) + (e >= e_lo && e < e_hi ? w0 : 0.0);
-}
-
-// Generic (VALU) contraction along one staged direction for nodes the MFMA blocks do not
-// cover (the domain's closing line / column): `base` points at the element's node 0 in the
-// staged tile, `stride` is the distance between consecutive nodes of the direction.
-template <int P>
-__device__ __forceinline__ void contract_generic(const double* Kt, const double* Gt, const double* base, int stride,
-                                                 int row, bool hasR, bool hasL, double& k, double& g) {
-  constexpr int n = P + 1;
-  k = 0.0;
-  g = 0.0;
-  if (row == 0 && hasL) {
-    for (int l = 0; l <= P; ++l) {
-      const double t = base[(l - P) * stride];
-      k = fma(Kt[P * n + l], t, k);
-      g = fma(Gt[P * n + l], t, g);
-    }
-  }
-  if (hasR) {
-    for (int l = 0; l <= P; ++l) {
-      const double t = base[l * stride];
-      k = fma(Kt[row * n + l], t, k);
-      g = fma(Gt[row * n + l], t, g);
-    }
-  }
-}
-
-// Buffer resource over `bytes` bytes at p (wave-uniform inputs only).  Loads at offsets outside
-// [0, bytes) -- including "negative" offsets, which wrap to huge unsigned values -- return 0
-// without touching memory, so halo staging needs no clamps.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
-}
-__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v),
-                                        r, off, 0, 0);
-}
-
 template <int P, int TX, int TY, int NW, bool PERSIST, bool SPLIT>
 __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void apply_tp_mfma(const ApplyArgs a) {
   using C = MCfg<P, TX, TY, NW, SPLIT>;
@@ -453,12 +321,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lk = lane >> 4;
   SEM_STAMP(0);
-  if (a.stamps && lane == 0) {  // slot 7: the XCD this wave runs on (stamps are per-XCD clocks)
-    unsigned xcc, hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)" : "=s"(xcc), "=s"(hw));
-    a.stamps[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 7] =
-        (static_cast<unsigned long long>(hw) << 8) | (xcc & 0xf);
-  }
+  SEM_STAMP_HWID();
 
   const int nbytes = a.n_local32 * 8;
   const auto rx = brsrc(a.x, nbytes), ru = brsrc(a.cu, a.cu ? nbytes : 0), rv = brsrc(a.cv, a.cv ? nbytes : 0);
@@ -1235,7 +1098,7 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   if (x == y) return set_error(SEM_EINVAL, "x and y must not alias");
   if (d->dir_mode < SEM_DIR_NONE || d->dir_mode > SEM_DIR_REPLACE) return set_error(SEM_EINVAL, "bad dir_mode");
   if (d->dir_mode == SEM_DIR_REPLACE && !d->dir_val) return set_error(SEM_EINVAL, "SEM_DIR_REPLACE needs dir_val");
-  if (d->algo < SEM_ALGO_AUTO || d->algo > SEM_ALGO_COLUMN) return set_error(SEM_EINVAL, "bad algo");
+  if (d->algo < SEM_ALGO_AUTO || d->algo > SEM_ALGO_BAND) return set_error(SEM_EINVAL, "bad algo");
   if (d->algo == SEM_ALGO_MFMA && h->P > 15) return set_error(SEM_EUNSUPPORTED, "MFMA path needs P <= 15");
   ApplyArgs a{};
   a.x = x;
@@ -1284,10 +1147,16 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   }();
   a.stamps = (diag & 8) ? stamps : nullptr;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  // AUTO: measured on MI355X (tools/kbench.py) -- the MFMA tile kernel wins on meshes that
-  // leave the chip latency-bound (< 2M DOFs), the single-phase column kernel on larger ones.
-  const bool small = h->n_local < (int64_t(1) << 21);
-  const bool use_col = d->algo == SEM_ALGO_COLUMN || (d->algo == SEM_ALGO_AUTO && !(small && h->P <= 15));
+  // Buffer-resource kernels (MFMA, band) address the local vector with 32-bit byte offsets.
+  // AUTO, measured on MI355X (tools/kbench.py): the band kernel up to ~3M DOFs (latency-bound
+  // meshes), the single-phase column kernel above (HBM-bound meshes).
+  const bool fits32 = h->n_local < (int64_t(1) << 28);
+  const bool band_auto = h->n_local < 3000000;
+  if (d->algo == SEM_ALGO_BAND || (d->algo == SEM_ALGO_AUTO && band_auto)) {
+    if (!fits32) return set_error(SEM_EUNSUPPORTED, "band path needs n_local < 2^28");
+    return launch_apply_band(a, h, s);
+  }
+  const bool use_col = d->algo == SEM_ALGO_COLUMN || d->algo == SEM_ALGO_AUTO;
   if (use_col) {
     switch (h->P) {
 #define SEM_CCASE(PP) \
@@ -1301,7 +1170,7 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
     }
   }
   const bool mfma = d->algo == SEM_ALGO_MFMA || d->algo == SEM_ALGO_AUTO;
-  if (mfma && h->n_local >= (int64_t(1) << 31)) return set_error(SEM_EUNSUPPORTED, "MFMA path needs n_local < 2^31");
+  if (mfma && !fits32) return set_error(SEM_EUNSUPPORTED, "MFMA path needs n_local < 2^28");
   if (mfma) {
     switch (h->P) {
 #define SEM_MCASE(PP) \
@@ -1328,10 +1197,11 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
 
 int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
   if (!h || !buf || len < 1) return set_error(SEM_EINVAL, "bad arguments");
-  const bool small = h->n_local < (int64_t(1) << 21);
   std::string name;
   const int P = h->P;
-  if (algo == SEM_ALGO_COLUMN || (algo == SEM_ALGO_AUTO && !(small && P <= 15))) {
+  if (algo == SEM_ALGO_BAND || (algo == SEM_ALGO_AUTO && h->n_local < 3000000)) {
+    name = band_kernel_name(P);
+  } else if (algo == SEM_ALGO_COLUMN || algo == SEM_ALGO_AUTO) {
     name = "sem::apply_tp_col<" + std::to_string(P) + ", 2, 64, 1>";
   } else if ((algo == SEM_ALGO_MFMA || algo == SEM_ALGO_AUTO) && P <= 15) {
     const int TL = std::max(1, 32 / P), TS = std::max(1, 16 / P);

@@ -70,7 +70,7 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
          (8, 17, 5), (9, 3, 4), (10, 2, 2), (11, 3, 1), (12, 5, 3), (13, 2, 3), (14, 1, 2), (15, 2, 2), (16, 3, 2)]
 
 
-ALGOS = [1, 2, 3]  # VALU two-phase, MFMA, VALU single-phase column kernel
+ALGOS = [1, 2, 3, 4]  # VALU two-phase, MFMA, VALU single-phase column kernel, assembled band
 
 
 @pytest.mark.parametrize("algo", ALGOS)

@@ -49,6 +49,11 @@ def main():
     ap.add_argument("--floor", action="store_true", help="also time torch.addcmul (same 32 B/DOF traffic)")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: per-wave phase stamps of one apply (needs SEM_DIAG=8 and SEM_DIAG_BUF)")
+    ap.add_argument("--nstamps", type=int, default=7, help="stamps per wave written by the kernel")
+    ap.add_argument("--roles", default="", help="wave roles by slot within a workgroup, e.g. X:0-3,Y:4-7,E:8")
+    ap.add_argument("--stride", type=int, default=8, help="stamp slots per wave (band kernel: 16)")
+    ap.add_argument("--tiles-x", type=int, default=32)
+    ap.add_argument("--tiles-y", type=int, default=8)
     ap.add_argument("--dss", type=int, default=0,
                     help="FETCH_SIZE calibration: time sem_dss on an ne x ne, P=8 element array (8-byte loads, "
                          "reads exactly ne^2*81*8 bytes)")
@@ -71,17 +76,30 @@ def main():
         torch.cuda.synchronize()
         m.apply(T, y, **kw)
         torch.cuda.synchronize()
-        st = buf.cpu().numpy().reshape(-1, 8).astype(np.int64)
-        st = st[st[:, 0] > 0]
+        st = buf.cpu().numpy().reshape(-1, a.stride).astype(np.int64)
+        slot = np.arange(len(st))
+        keep = st[:, 0] > 0
+        st, slot = st[keep], slot[keep]
         t0 = st[:, 0].min()
-        names = ["start", "loads issued", "staged->LDS", "barrier1", "mfma done", "barrier2", "end"]
+        ns = int(a.nstamps)
         print(f"{m.kernel_name(a.algo)}: {len(st)} waves; times in shader cycles relative to the first wave start")
-        for k in range(7):
-            col = st[:, k] - t0
-            print(f"  {names[k]:14s} min {col.min():8d} med {int(np.median(col)):8d} max {col.max():8d}")
-        for k in range(1, 7):
+        roles = {"all": np.ones(len(st), bool)}
+        if a.roles:  # e.g. "X:0-3,Y:4-7,E:8" wave slots within a workgroup of NW waves
+            nw = max(int(r.split(":")[1].split("-")[-1]) for r in a.roles.split(",")) + 1
+            for r in a.roles.split(","):
+                nm, rg = r.split(":")
+                lo, hi = (int(x) for x in (rg.split("-") + rg.split("-"))[:2]) if "-" in rg else (int(rg), int(rg))
+                roles[nm] = ((slot % nw) >= lo) & ((slot % nw) <= hi)
+        for nm, sel in roles.items():
+            sr = st[sel]
+            if len(sr) == 0:
+                continue
+            line = " ".join(f"s{k}:{int(np.median(sr[:, k] - sr[:, 0])):6d}" for k in range(1, ns))
+            print(f"  {nm:4s} ({len(sr):5d} waves) med since own start: {line}; start med {int(np.median(sr[:, 0] - t0))}")
+        for k in range(1, ns):
             d = st[:, k] - st[:, k - 1]
-            print(f"  phase {names[k-1]:>14s} -> {names[k]:14s}: med {int(np.median(d)):7d}  p90 {int(np.percentile(d, 90)):7d}")
+            print(f"  phase s{k-1}->s{k}: med {int(np.median(d)):7d}  p90 {int(np.percentile(d, 90)):7d}")
+        last = ns - 1
         # per-XCD view (each XCD has its own clock): dispatch ramp, wave span, active window
         xcc = st[:, 7] & 0xF
         hw = st[:, 7] >> 8  # HW_ID: cu_id [11:8], sh_id [12], se_id [15:13]
@@ -89,15 +107,33 @@ def main():
         win, ramp = [], []
         for c in sorted(set(cu.tolist())):
             sc = st[cu == c]
-            win.append(sc[:, 6].max() - sc[:, 0].min())
+            win.append(sc[:, last].max() - sc[:, 0].min())
             ramp.append(sc[:, 0].max() - sc[:, 0].min())
         print(f"  per CU ({len(win)} CUs): active window med {int(np.median(win))} max {int(np.max(win))}; "
               f"start ramp med {int(np.median(ramp))} max {int(np.max(ramp))}; waves/CU {len(st) / len(win):.1f}")
+        if a.stride >= 10:  # per-tile times on the chip-wide realtime clock (10 ns ticks), by tile class
+            nw = max(int(r.split(":")[1].split("-")[-1]) for r in a.roles.split(",")) + 1 if a.roles else 1
+            blk = slot // nw
+            r0 = st[:, 8].min()
+            beg, ends, cls = [], [], []
+            for bidx in np.unique(blk):
+                sb = st[blk == bidx]
+                beg.append((sb[:, 8].min() - r0) * 10)
+                ends.append((sb[:, 9].max() - r0) * 10)
+                tx, ty = divmod(int(sb[0, 6]), a.tiles_y)
+                cls.append(("X" if tx == a.tiles_x - 1 else "") + ("Y" if ty == a.tiles_y - 1 else "") or "I")
+            beg, ends, cls = np.array(beg), np.array(ends), np.array(cls)
+            print(f"  realtime (ns): workgroup start med {int(np.median(beg))} max {int(beg.max())}; "
+                  f"end med {int(np.median(ends))} p90 {int(np.percentile(ends, 90))} max {int(ends.max())}")
+            for c in sorted(set(cls.tolist())):
+                e, b0 = ends[cls == c], beg[cls == c]
+                print(f"  tiles {c:2s}: n {len(e):4d}  start med {int(np.median(b0)):5d}  end med {int(np.median(e)):5d}"
+                      f" p90 {int(np.percentile(e, 90)):5d} max {int(e.max()):5d}  span med {int(np.median(e - b0))}")
         for x in sorted(set(xcc.tolist())):
             sx = st[xcc == x]
             s0 = sx[:, 0].min()
-            print(f"  xcd {x}: waves {len(sx):5d}  last start {sx[:, 0].max() - s0:7d}  first end {sx[:, 6].min() - s0:7d}"
-                  f"  last end {sx[:, 6].max() - s0:7d}  med span {int(np.median(sx[:, 6] - sx[:, 0])):6d}")
+            print(f"  xcd {x}: waves {len(sx):5d}  last start {sx[:, 0].max() - s0:7d}  first end {sx[:, last].min() - s0:7d}"
+                  f"  last end {sx[:, last].max() - s0:7d}  med span {int(np.median(sx[:, last] - sx[:, 0])):6d}")
         return
     if a.dss:
         m = get_mesh(8, a.dss, a.dss, 1.0 / a.dss, 1.0 / a.dss)
