@@ -61,47 +61,70 @@ struct EOC {
   static constexpr double DG(int i, int m) { return 0.5 * (G(i, m) - G(i, P - m)); }
 };
 
-// Work items of an element's rows, split over NS threads: item 0 = row 0, item i in [1, NP] =
-// the mirror pair (i, P-i), item -1 = the centre row P/2 (even P).  Split 0 takes row 0 and the
-// even pairs, split 1 the odd pairs and the centre (NS = 2); NS = 1 takes everything.
+// Work items of an element's rows: item 0 = row 0 (the shared node; it also folds in the left
+// element's row P), items 1..NP = the mirror pairs (k, P-k), item NP+1 = the centre row P/2 (even
+// P).  They are dealt to NS splits (one thread each) longest-first by VALU cost.
 template <int P, int NS>
 struct EPlan {
-  static constexpr int NP = EOC<P>::NP;
+  static constexpr int NP = EOC<P>::NP, H = EOC<P>::H;
   static constexpr bool EVEN = EOC<P>::EVEN;
-  static constexpr bool in_split(int it, int s) {
-    return NS == 1 ? true : (it == 0 ? s == 0 : it < 0 ? s == 1 : (it % 2 == 0) == (s == 0));
-  }
-  static constexpr int code(int k) { return k == 0 ? 0 : (k <= NP ? k : -1); }  // k-th item overall
   static constexpr int NITEMS = 1 + NP + (EVEN ? 1 : 0);
-  static constexpr int size(int it) { return it > 0 ? 2 : 1; }
-  static constexpr int nrows(int s) {
+  static constexpr int code(int k) { return k == 0 ? 0 : (k <= NP ? k : -1); }
+  static constexpr int size(int k) { return code(k) > 0 ? 2 : 1; }
+  static constexpr int cost(int k) { return code(k) == 0 ? 4 * P + 2 : (code(k) > 0 ? 4 * H + 8 : 2 * H + 2); }
+  struct Deal {
+    int of[24];
+  };
+  static constexpr Deal deal() {
+    Deal d{};
+    int load[NS] = {};
+    bool done[24] = {};
+    for (int step = 0; step < NITEMS; ++step) {
+      int best = -1;
+      for (int k = 0; k < NITEMS; ++k)
+        if (!done[k] && (best < 0 || cost(k) > cost(best))) best = k;
+      int sp = 0;
+      for (int q = 1; q < NS; ++q)
+        if (load[q] < load[sp]) sp = q;
+      d.of[best] = sp;
+      load[sp] += cost(best);
+      done[best] = true;
+    }
+    return d;
+  }
+  static constexpr Deal DEAL = deal();
+  static constexpr bool in_split(int k, int sp) { return DEAL.of[k] == sp; }
+  static constexpr int nrows(int sp) {
     int r = 0;
     for (int k = 0; k < NITEMS; ++k)
-      if (in_split(code(k), s)) r += size(code(k));
+      if (in_split(k, sp)) r += size(k);
     return r;
   }
-  // first slot of item k within split s
-  static constexpr int slot(int s, int k) {
+  static constexpr int slot(int sp, int k) {  // first slot of item k within split sp
     int r = 0;
     for (int q = 0; q < k; ++q)
-      if (in_split(code(q), s)) r += size(code(q));
+      if (in_split(q, sp)) r += size(q);
     return r;
   }
-  static constexpr int row(int s, int sl) {  // element-local row of slot sl of split s
+  static constexpr int row(int sp, int sl) {  // element-local row of slot sl of split sp (-1: none)
     for (int k = 0; k < NITEMS; ++k) {
-      const int it = code(k);
-      if (!in_split(it, s)) continue;
-      const int f = slot(s, k);
+      if (!in_split(k, sp)) continue;
+      const int f = slot(sp, k), it = code(k);
       if (sl == f) return it == 0 ? 0 : (it < 0 ? P / 2 : it);
       if (it > 0 && sl == f + 1) return P - it;
     }
-    return 0;
+    return -1;
   }
-  static constexpr int NRMAX = nrows(0) > nrows(NS - 1) ? nrows(0) : nrows(NS - 1);
-  static constexpr bool needs_left(int s) { return in_split(0, s); }
-  static constexpr bool needs_eo(int s) {
+  static constexpr int nrmax() {
+    int m = 0;
+    for (int sp = 0; sp < NS; ++sp)
+      if (nrows(sp) > m) m = nrows(sp);
+    return m;
+  }
+  static constexpr bool needs_left(int sp) { return in_split(0, sp); }
+  static constexpr bool needs_eo(int sp) {
     for (int k = 1; k < NITEMS; ++k)
-      if (in_split(code(k), s)) return true;
+      if (in_split(k, sp)) return true;
     return false;
   }
 };
@@ -126,7 +149,7 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
   for_rows(std::make_integer_sequence<int, L::NITEMS>{}, [&](auto KI) {
     constexpr int kk = decltype(KI)::value;
     constexpr int it = L::code(kk);
-    if constexpr (L::in_split(it, S)) {
+    if constexpr (L::in_split(kk, S)) {
       constexpr int sl = L::slot(S, kk);
       if constexpr (it == 0) {  // shared-node row 0 (+ the left element's row P)
         constexpr double k00 = E::Ks(0, 0), g00 = E::G(0, 0);
@@ -176,24 +199,25 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
   });
 }
 
-template <int P, int TXE, int TYE, int RS, int YS>
+template <int P, int TXE, int TYE, int NS>
 struct BCfg {
   static constexpr int n = P + 1;
   static constexpr int BX = TXE * P, BY = TYE * P;      // lines / columns of the tile's element positions
-  static constexpr int XW = (BY + 63) / 64;             // waves per X group (a, s)
-  static constexpr int RP = EPlan<P, RS>::NRMAX;        // rows per X thread (at most)
-  static constexpr int NXW = TXE * RS * XW;             // X waves
-  static constexpr int YL = BX * TYE;                   // Y lanes per column split
+  static constexpr int XW = (BY + 63) / 64;             // waves per (element position, split) X group
+  static constexpr int LW = 64 * XW;                    // lanes per tile line (X role and epilogue)
+  static constexpr int NXW = TXE * NS * XW;             // X waves
+  static constexpr int YL = BX * TYE;                   // Y lanes per split: (line, element position)
   static constexpr int YW = (YL + 63) / 64;
-  static constexpr int JP = EPlan<P, YS>::NRMAX;        // columns per Y thread (at most)
-  static constexpr int NYW = YS * YW;                   // Y waves
+  static constexpr int NYW = NS * YW;                   // Y waves
   static constexpr int NW = NXW + NYW;
   static constexpr int THREADS = 64 * NW;
+  static constexpr int RP = EPlan<P, NS>::nrmax();      // rows (columns) per X (Y) thread
   static constexpr int RX = BX + P + 1, RY = BY + P + 1;  // staged lines [gx0-P, gx0+BX] x cols [gy0-P, gy0+BY]
   static constexpr int PT = RY | 1;                     // odd pitch
-  static constexpr int PY = BY | 1;
+  static constexpr int PY = LW + 1;                     // result tiles: BX lines x LW columns
   static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
-  static_assert(RS >= 1 && RS <= 2 && YS >= 1 && YS <= 2 && (P >= 2 || (RS == 1 && YS == 1)), "1 or 2 splits");
+  static constexpr int NE = (BX * LW + THREADS - 1) / THREADS;  // epilogue nodes per thread
+  static_assert(NS >= 1 && NS <= 4, "1 to 4 splits");
   static_assert(THREADS <= 1024, "workgroup too large");
 };
 
@@ -289,11 +313,14 @@ __device__ __forceinline__ double gll_w(int J) {
 }
 
 // FULL = false: no extra / accumulate terms, no Dirichlet mask or values (side bits only).
-template <int P, int TXE, int TYE, int RS, int YS, bool FULL>
-__global__ __launch_bounds__((BCfg<P, TXE, TYE, RS, YS>::THREADS)) void apply_band(const BandArgs a) {
-  using C = BCfg<P, TXE, TYE, RS, YS>;
-  constexpr int n = C::n, BX = C::BX, BY = C::BY, PT = C::PT, PY = C::PY;
+template <int P, int TXE, int TYE, int NS, bool FULL>
+__global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(const BandArgs a) {
+  using C = BCfg<P, TXE, TYE, NS>;
+  using PL = EPlan<P, NS>;
+  constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW;
   __shared__ double Ts[C::RX * PT];
+  __shared__ double XK[BX * PY];
+  __shared__ double XG[BX * PY];
   __shared__ double YK[BX * PY];
   __shared__ double YG[BX * PY];
   __shared__ double ws[n];
@@ -372,38 +399,32 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, RS, YS>::THREADS)) void apply_ba
     const int rr = idx / C::RY, cc = idx - rr * C::RY;
     st[s] = bload(rx, sbase + (rr * NY + cc) * 8);
   }
-  // X role: (element position xa, row split xs, column xc)
-  const int xg = w / C::XW;
-  const int xa = xg / RS, xs = xg - xa * RS;
-  const int xc = (w - xg * C::XW) * 64 + lane;
-  const bool xghost = m0 + xa == a.ex_end;                       // wave-uniform
-  const bool xact = w < C::NXW && xa < m1 - m0 && xc < cols_ok && (!xghost || xs == 0);
-  // Issued by every wave (uniform vmcnt bookkeeping, so the staging writes below wait for the
-  // staging loads only); the Y waves' offsets are out of bounds and touch no memory.
-  using XPlan = EPlan<P, RS>;
-  double pu[C::RP], pv[C::RP];
-  int prow[C::RP];  // element-local row of each slot (wave-uniform)
-  NodeOps ops[C::RP] = {};
-  const int pbase = w < C::NXW && !(a.diag & 32) ? nodeb + xa * P * NY + xc : -(1 << 28);
+  // epilogue nodes of this thread: q = tid + e*THREADS -> tile line r = q / LW, column c = q % LW
+  double pu[C::NE], pv[C::NE];
+  int eoff[C::NE];
+  NodeOps ops[C::NE] = {};
 #pragma unroll
-  for (int k = 0; k < C::RP; ++k) {
-    prow[k] = xs == 0 ? XPlan::row(0, k) : XPlan::row(RS - 1, k);
-    pu[k] = bload(ru, (pbase + prow[k] * NY) * 8);
-    pv[k] = bload(rv, (pbase + prow[k] * NY) * 8);
+  for (int e = 0; e < C::NE; ++e) {
+    const int q = tid + e * C::THREADS;
+    const int r = q / LW, c = q - r * LW;
+    const bool ok = q < BX * LW && r < rows_ok && c < cols_ok && !(a.diag & 32);  // diag 32: no u/v/y traffic
+    eoff[e] = ok ? nodeb + r * NY + c : -(1 << 26);  // out of bounds: touches no memory
+    pu[e] = bload(ru, eoff[e] * 8);
+    pv[e] = bload(rv, eoff[e] * 8);
   }
   if constexpr (FULL) {
 #pragma unroll
-    for (int k = 0; k < C::RP; ++k) ops[k] = load_node_ops(a, pbase + prow[k] * NY);
+    for (int e = 0; e < C::NE; ++e) ops[e] = load_node_ops(a, eoff[e]);
   }
 
-  // ---- LDS: staged window, weights
+  // ---- LDS: weights, staged window (columns outside the domain staged as 0: absent elements)
   if (tid < n) ws[tid] = gll_w<P>(tid);
 #pragma unroll
   for (int s = 0; s < C::NSTAGE; ++s) {
     const int idx = tid + s * C::THREADS;
     if ((s + 1) * C::THREADS <= C::RX * C::RY || idx < C::RX * C::RY) {
       const int rr = idx / C::RY, cc = idx - rr * C::RY;
-      const int gy = gy0 - P + cc;  // columns outside the domain are staged as 0 (absent elements)
+      const int gy = gy0 - P + cc;
       Ts[rr * PT + cc] = (gy >= 0 && gy < NY) ? st[s] : 0.0;
     }
   }
@@ -412,30 +433,40 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, RS, YS>::THREADS)) void apply_ba
   BSTAMP(2);
 
   constexpr double w0 = GllConst<P>::w[0], wP = GllConst<P>::w[P];
-  const bool hasLx = m0 + xa - 1 >= a.ex_begin;  // X role: left element of position xa (wave-uniform)
-
-  double XK[C::RP], XG[C::RP], XV[C::RP];
   if (w < C::NXW) {
-    // ---- X contractions: the rows of split xs of element position xa at column xc.  Lines
-    // outside the local range are staged as 0, so absent elements contribute nothing.
-    const double fk = (hasLx ? 1.0 : 0.0) + (xghost ? 0.0 : 1.0), fg = (xghost ? 0.0 : 1.0) - (hasLx ? 1.0 : 0.0);
-    for_rows(std::make_integer_sequence<int, RS>{}, [&](auto S) {
-      constexpr int s = decltype(S)::value;
-      if (xs != s) return;
-      double t[2 * P + 1];
-      constexpr int q0 = XPlan::needs_left(s) ? 0 : P;  // only row 0 reads the left element
+    // ---- X role: wave = (element position xa, split xs), lane = column xc: the x-direction rows
+    // of the split from a (2P+1)-node window along x -> LDS.  Lines outside the local range are
+    // staged as 0, so absent elements contribute nothing.
+    const int xg = w / C::XW;
+    const int xa = xg / NS, xs = xg - xa * NS;
+    const int xc = (w - xg * C::XW) * 64 + lane;
+    if (xa < m1 - m0) {
+      const bool xghost = m0 + xa == a.ex_end, hasLx = m0 + xa - 1 >= a.ex_begin;  // wave-uniform
+      const double fk = (hasLx ? 1.0 : 0.0) + (xghost ? 0.0 : 1.0);
+      const double fg = (xghost ? 0.0 : 1.0) - (hasLx ? 1.0 : 0.0);
+      for_rows(std::make_integer_sequence<int, NS>{}, [&](auto S) {
+        constexpr int s = decltype(S)::value;
+        if (xs != s) return;
+        double t[2 * P + 1];
+        constexpr int q0 = PL::needs_left(s) ? 0 : P;  // only row 0 reads the left element
 #pragma unroll
-      for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[(xa * P + qq) * PT + P + xc];
+        for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[(xa * P + qq) * PT + P + xc];
 #pragma unroll
-      for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
-      eo_rows<P, RS, s>(t, fk, fg, XK, XG);
+        for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
+        double k[C::RP], g[C::RP];
+        eo_rows<P, NS, s>(t, fk, fg, k, g);
 #pragma unroll
-      for (int k = 0; k < C::RP; ++k) XV[k] = t[P + XPlan::row(s, k)];
-    });
+        for (int sl = 0; sl < PL::nrows(s); ++sl) {
+          const int i = PL::row(s, sl);
+          if (xghost && i != 0) continue;  // a ghost position holds its row 0 only
+          XK[(xa * P + i) * PY + xc] = k[sl];
+          XG[(xa * P + i) * PY + xc] = g[sl];
+        }
+      });
+    }
   } else {
-    // ---- Y contractions: the columns of split h of element position b on line r -> LDS,
-    // scaled by Mx of the line.  Columns outside the domain are staged as 0.
-    using YPlan = EPlan<P, YS>;
+    // ---- Y role: wave = split h, lane = (line r, element position b): the y-direction columns of
+    // the split from a (2P+1)-node window along the line -> LDS, scaled by Mx of the line.
     const int wy = w - C::NXW;
     const int h = wy / C::YW;
     const int t2 = (wy - h * C::YW) * 64 + lane;
@@ -446,22 +477,22 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, RS, YS>::THREADS)) void apply_ba
       const int i = r % P, ex = m0 + r / P;
       const double mx = i != 0 ? ws[i] : (ex - 1 >= a.ex_begin ? wP : 0.0) + (ex < a.ex_end ? w0 : 0.0);
       const double sk = a.fKy * mx, sg = a.fY * mx;
-      for_rows(std::make_integer_sequence<int, YS>{}, [&](auto H) {
+      for_rows(std::make_integer_sequence<int, NS>{}, [&](auto H) {
         constexpr int hh = decltype(H)::value;
         if (h != hh) return;
         double t[2 * P + 1];
-        constexpr int q0 = YPlan::needs_left(hh) ? 0 : P;
+        constexpr int q0 = PL::needs_left(hh) ? 0 : P;
 #pragma unroll
         for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[(P + r) * PT + b * P + qq];
 #pragma unroll
         for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
-        double k[C::JP], g[C::JP];
-        eo_rows<P, YS, hh>(t, fk, fg, k, g);
+        double k[C::RP], g[C::RP];
+        eo_rows<P, NS, hh>(t, fk, fg, k, g);
 #pragma unroll
-        for (int q = 0; q < YPlan::nrows(hh); ++q) {
-          const int j = YPlan::row(hh, q);
-          YK[r * PY + b * P + j] = sk * k[q];
-          YG[r * PY + b * P + j] = sg * g[q];
+        for (int sl = 0; sl < PL::nrows(hh); ++sl) {
+          const int j = PL::row(hh, sl);
+          YK[r * PY + b * P + j] = sk * k[sl];
+          YG[r * PY + b * P + j] = sg * g[sl];
         }
       });
     }
@@ -470,27 +501,34 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, RS, YS>::THREADS)) void apply_ba
   __syncthreads();
   BSTAMP(4);
 
-  // ---- X epilogue: combine with the y-direction results, pointwise terms, store (coalesced)
-  if (xact) {
-    const int j = xc % P, ey = n0 + xc / P;
-    const double my = j != 0 ? ws[j] : (ey - 1 >= 0 ? wP : 0.0) + (ey < a.ney ? w0 : 0.0);
-    const int nr = xghost ? 1 : (xs == 0 ? XPlan::nrows(0) : XPlan::nrows(RS - 1));  // a ghost holds row 0 only
-    double zz[C::RP];
+  // ---- epilogue, every wave: node (r, c) = both directions + pointwise terms + Dirichlet rows;
+  // all values are formed before the first (coalesced) store
+  double zz[C::NE];
 #pragma unroll
-    for (int k = 0; k < C::RP; ++k) {
-      const int i = prow[k];  // element-local row (wave-uniform)
-      const int rl = xa * P + i;
-      const double mx = i != 0 ? ws[i] : (hasLx ? wP : 0.0) + (xghost ? 0.0 : w0);
-      const double u_ = has_u ? pu[k] : 1.0, v_ = has_v ? pv[k] : 1.0;
-      double z = fma(a.fKx * my, XK[k], YK[rl * PY + xc]);
-      z = fma(a.fM * mx * my, XV[k], z);
-      z = fma(a.fX * u_, my * XG[k], z);
-      z = fma(v_, YG[rl * PY + xc], z);
-      zz[k] = finish_node<FULL>(a, ops[k], gx0 + rl, gy0 + xc, XV[k], z);
+  for (int e = 0; e < C::NE; ++e) {
+    const int q = tid + e * C::THREADS;
+    const int r = q / LW, c = q - r * LW;
+    zz[e] = 0.0;
+    if (q < BX * LW && r < rows_ok && c < cols_ok) {
+      const int i = r % P, me = m0 + r / P;
+      const double mx = i != 0 ? ws[i] : (me - 1 >= a.ex_begin ? wP : 0.0) + (me < a.ex_end ? w0 : 0.0);
+      const int j = c % P, ne = n0 + c / P;
+      const double my = j != 0 ? ws[j] : (ne - 1 >= 0 ? wP : 0.0) + (ne < a.ney ? w0 : 0.0);
+      const int o = r * PY + c;
+      const double xv = Ts[(P + r) * PT + P + c];
+      const double u_ = has_u ? pu[e] : 1.0, v_ = has_v ? pv[e] : 1.0;
+      double z = fma(a.fKx * my, XK[o], YK[o]);
+      z = fma(a.fM * mx * my, xv, z);
+      z = fma(a.fX * u_, my * XG[o], z);
+      z = fma(v_, YG[o], z);
+      zz[e] = finish_node<FULL>(a, ops[e], gx0 + r, gy0 + c, xv, z);
     }
+  }
 #pragma unroll
-    for (int k = 0; k < C::RP; ++k)
-      if (k < nr && !(a.diag & 16)) bstore(ry, (pbase + prow[k] * NY) * 8, zz[k]);  // diag 16: no stores (timing)
+  for (int e = 0; e < C::NE; ++e) {
+    const int q = tid + e * C::THREADS;
+    const int r = q / LW, c = q - r * LW;
+    if (q < BX * LW && r < rows_ok && c < cols_ok && !(a.diag & 16)) bstore(ry, eoff[e] * 8, zz[e]);  // diag 16: no stores
   }
   BSTAMP(5);
   if (a.stamps) {
@@ -514,9 +552,9 @@ static int hip_check_b(hipError_t e, const char* what) {
   return set_error(SEM_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-template <int P, int TXE, int TYE, int RS, int YS>
+template <int P, int TXE, int TYE, int NS>
 static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
-  using C = BCfg<P, TXE, TYE, RS, YS>;
+  using C = BCfg<P, TXE, TYE, NS>;
   const int ncols = h->ex_end - h->ex_begin;
   const int tiles_x = (ncols + 1 + TXE - 1) / TXE;  // + the ghost position of the closing line
   const int tiles_y = (h->ney + 1 + TYE - 1) / TYE;
@@ -560,43 +598,40 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   b.nblk = static_cast<int>(nblk);
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   if (full)
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, RS, YS, true>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
                        s, b);
   else
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, RS, YS, false>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
                        s, b);
   return hip_check_b(hipGetLastError(), "apply (band) launch");
 }
 
-// Tile shape per order: ~64 columns (TYE = 64/P elements) so an X wave spans one tile row;
-// TXE element columns so a tile holds ~1024 nodes; row / column splits of 2 for even P.
+// Tile shape per order: ~64 columns (TYE = 64/P element positions) so a wave spans one tile line;
+// TXE element columns for ~512-node tiles; rows of an element split over NS threads.
 template <int P>
 struct BandShape {
   static constexpr int TYE = (64 / P) > 0 ? 64 / P : 1;
   static constexpr int TXE = (8 / P) > 4 ? 4 : ((8 / P) > 0 ? 8 / P : 1);
-  static constexpr int RS = P >= 2 ? 2 : 1;
-  static constexpr int YS = RS;
+  static constexpr int NS = P >= 2 ? 2 : 1;
 };
 
 template <int P>
 static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
   using S = BandShape<P>;
-  static const int force = [] {
-    const char* e = std::getenv("SEM_BAND_TILE");  // tuning override
-    return e ? std::atoi(e) : 0;
-  }();
+  const char* env = std::getenv("SEM_BAND_TILE");  // tuning override, read per call (in-process A/B)
+  const int force = env ? std::atoi(env) : 0;
   if constexpr (P == 8) {
-    if (force == 1) return launch_band<P, 2, S::TYE, S::RS, S::YS>(args, h, s);
-    if (force == 2) return launch_band<P, 1, S::TYE, 1, 1>(args, h, s);
+    if (force == 1) return launch_band<P, 1, S::TYE, 4>(args, h, s);
+    if (force == 2) return launch_band<P, 2, S::TYE, 4>(args, h, s);
   }
-  return launch_band<P, S::TXE, S::TYE, S::RS, S::YS>(args, h, s);
+  return launch_band<P, S::TXE, S::TYE, S::NS>(args, h, s);
 }
 
 std::string band_kernel_name(int P) {
   const int TYE = std::max(1, 64 / P), TXE = std::min(4, std::max(1, 8 / P));
-  const int RS = P >= 2 ? 2 : 1;
+  const int NS = P >= 2 ? 2 : 1;
   return "sem::apply_band<" + std::to_string(P) + ", " + std::to_string(TXE) + ", " + std::to_string(TYE) + ", " +
-         std::to_string(RS) + ", " + std::to_string(RS) + ">";
+         std::to_string(NS) + ">";
 }
 
 int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s) {

@@ -1148,10 +1148,11 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   a.stamps = (diag & 8) ? stamps : nullptr;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // Buffer-resource kernels (MFMA, band) address the local vector with 32-bit byte offsets.
-  // AUTO, measured on MI355X (tools/kbench.py): the band kernel up to ~3M DOFs (latency-bound
-  // meshes), the single-phase column kernel above (HBM-bound meshes).
+  // AUTO, measured on MI355X (tools/kbench.py): the band kernel on every mesh whose local vector
+  // fits its 32-bit buffer offsets (it beats the other kernels from 64^2 to 1024^2 elements);
+  // the single-phase column kernel above that.
   const bool fits32 = h->n_local < (int64_t(1) << 28);
-  const bool band_auto = h->n_local < 3000000;
+  const bool band_auto = fits32;
   if (d->algo == SEM_ALGO_BAND || (d->algo == SEM_ALGO_AUTO && band_auto)) {
     if (!fits32) return set_error(SEM_EUNSUPPORTED, "band path needs n_local < 2^28");
     return launch_apply_band(a, h, s);
@@ -1199,7 +1200,7 @@ int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
   if (!h || !buf || len < 1) return set_error(SEM_EINVAL, "bad arguments");
   std::string name;
   const int P = h->P;
-  if (algo == SEM_ALGO_BAND || (algo == SEM_ALGO_AUTO && h->n_local < 3000000)) {
+  if (algo == SEM_ALGO_BAND || (algo == SEM_ALGO_AUTO && h->n_local < (int64_t(1) << 28))) {
     name = band_kernel_name(P);
   } else if (algo == SEM_ALGO_COLUMN || algo == SEM_ALGO_AUTO) {
     name = "sem::apply_tp_col<" + std::to_string(P) + ", 2, 64, 1>";
