@@ -240,8 +240,8 @@ def main():
         Tb, ub, vb = (torch.rand(big.n_local, dtype=torch.float64, device=dev) * 2 - 1 for _ in range(3))
         yb = torch.empty_like(Tb)
         kwb = dict(kw, cu=ub, cv=vb)
-        sb, _ = time_steps(lambda: big.apply(Tb, yb, **kwb), 20, 3, dev, use_graph=False)
-        kb = sb / 20
+        sb, _ = time_steps(lambda: big.apply(Tb, yb, **kwb), 50, 3, dev, use_graph=True)
+        kb = sb / 50
         bb = 32.0 * big.n_local
         wl = f"cd_matvec_{args.hbm_ne}x{args.hbm_ne}_P{P}"
         out["roofline_hbm"] = {"workload": wl, "kernel": big.kernel_name(), "dofs": big.n_local,
