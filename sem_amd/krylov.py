@@ -97,3 +97,96 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
         r = b - matvec(x)
         matvecs += 1
         beta = torch.linalg.vector_norm(r).item()
+
+
+def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None, precond=None, callback=None):
+    """Left-preconditioned restarted GMRES, SciPy's `gmres` (scipy 1.15 iterative.py) restated on
+    device tensors: the Arnoldi process runs on M^-1 A, the inner loop stops on the
+    preconditioned residual estimate against an adaptive tolerance (gh-8400 control), and each
+    restart checks the true residual ||b - A x||_2 <= max(atol, rtol ||b||_2).
+
+    The Boussinesq coupler needs this variant (OpenMDAO's ScipyKrylov hands its block-Jacobi
+    preconditioner to SciPy as M): M^-1 is only ever applied to b, to residuals b - A x and to
+    products A v -- vectors in the range of A.  The NS block solve (a Schur complement with
+    spurious pressure modes of the equal-order P_N-P_N discretisation) needs its right-hand side
+    in that range; the Arnoldi vectors a right-preconditioned GMRES feeds M^-1 are not.
+    `maxiter` counts restarts, as SciPy's does.  info = 0 on convergence, else maxiter.
+    """
+    N = b.numel()
+    dt, dev = b.dtype, b.device
+    restart = min(N, restart or 20)
+    maxiter = maxiter or 10 * N
+    psolve = precond if precond is not None else (lambda t: t)
+    x = torch.zeros_like(b) if x0 is None else x0.clone()
+    bnorm = torch.linalg.vector_norm(b).item()
+    if bnorm == 0.0:
+        return GMRESResult(torch.zeros_like(b), 0, 0, 0.0, 0)
+    tol = max(atol, rtol * bnorm)
+    eps = np.finfo(np.float64).eps
+    ptol_max = 1.0
+    ptol = torch.linalg.vector_norm(psolve(b)).item() * min(ptol_max, tol / bnorm)
+    V = torch.empty((restart + 1, N), dtype=dt, device=dev)
+    total, matvecs = 0, 0
+    r = b - matvec(x) if x0 is not None else b.clone()
+    matvecs += x0 is not None
+    rnorm = torch.linalg.vector_norm(r).item()
+    if rnorm < tol:
+        return GMRESResult(x, 0, 0, rnorm, matvecs)
+    for _ in range(maxiter):
+        z = psolve(r)
+        zn = torch.linalg.vector_norm(z).item()
+        V[0] = z / zn
+        H = np.zeros((restart + 1, restart))
+        cs, sn = np.zeros(restart), np.zeros(restart)
+        g = np.zeros(restart + 1)
+        g[0] = zn
+        breakdown, presid, k_done = False, 0.0, 0
+        for k in range(restart):
+            w = psolve(matvec(V[k]))
+            matvecs += 1
+            h0 = torch.linalg.vector_norm(w).item()
+            Vk = V[:k + 1]
+            h = Vk @ w                       # CGS2 in place of SciPy's MGS
+            w = w - Vk.T @ h
+            h2 = Vk @ w
+            w = w - Vk.T @ h2
+            H[:k + 1, k] = (h + h2).cpu().numpy()
+            hn = torch.linalg.vector_norm(w).item()
+            if hn <= eps * h0:               # exact-solution indicator
+                H[k + 1, k], breakdown = 0.0, True
+            else:
+                H[k + 1, k] = hn
+                V[k + 1] = w / hn
+            for i in range(k):
+                t = cs[i] * H[i, k] + sn[i] * H[i + 1, k]
+                H[i + 1, k] = -sn[i] * H[i, k] + cs[i] * H[i + 1, k]
+                H[i, k] = t
+            den = math.hypot(H[k, k], H[k + 1, k])
+            cs[k], sn[k] = (1.0, 0.0) if den == 0.0 else (H[k, k] / den, H[k + 1, k] / den)
+            H[k, k], H[k + 1, k] = den, 0.0
+            g[k + 1] = -sn[k] * g[k]
+            g[k] = cs[k] * g[k]
+            presid = abs(g[k + 1])
+            total += 1
+            k_done = k + 1
+            if callback is not None:
+                callback(presid)
+            if presid <= ptol or breakdown:
+                break
+        Hk = np.triu(H[:k_done, :k_done]).copy()
+        gk = g[:k_done].copy()
+        if Hk[-1, -1] == 0.0:
+            gk[-1], Hk[-1, -1] = 0.0, 1.0
+        y = np.linalg.solve(Hk, gk)
+        x = x + V[:k_done].T @ torch.as_tensor(y, dtype=dt, device=dev)
+        r = b - matvec(x)
+        matvecs += 1
+        rnorm = torch.linalg.vector_norm(r).item()
+        if rnorm <= tol or breakdown:
+            break
+        if presid <= ptol:
+            ptol_max = max(eps, 0.25 * ptol_max)
+        else:
+            ptol_max = min(1.0, 1.5 * ptol_max)
+        ptol = presid * min(ptol_max, tol / rnorm)
+    return GMRESResult(x, 0 if rnorm <= tol else maxiter, total, rnorm, matvecs)

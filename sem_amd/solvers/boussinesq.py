@@ -1,0 +1,211 @@
+"""Boussinesq coupler counterpart: natural convection, NS + CD coupled.
+
+Restates OpenMDAO/Boussinesq_SequentialCoupler.py:10-108 (and the arithmetic of
+Boussinesq_ParallelCoupler.py:12-121, which differs only in where the two blocks run)
+without OpenMDAO, which is not available offline.  The two OpenMDAO components
+(OpenMDAO/ConvectionDiffusion_Component.py, OpenMDAO/NavierStokes_Component.py) are
+restated as the residual / Jacobian / block-solve maps below.  Everything they call is a
+solver counterpart (sem_amd.solvers), so every operator apply is a HIP kernel launch and
+the CD Newton updates run the device GMRES.  Any pair of objects with the reference
+solvers' private methods can be passed in (the golden fixture tests/golden/bous.npz was
+made by this coupler driving the reference's own solver classes).
+
+Coupled system (the PG group of the couplers, :66-73):
+    R_cd(T; u, v)     = cd._get_residuals(T, I_cd(u), I_cd(v))          (output T_cd)
+    R_ns(u, v, p; T)  = ns._get_residuals(u, v, p, I_ns(T))             (outputs u_ns, v_ns, p_ns)
+where I_cd / I_ns are the mesh transfers of change_inputs (CD component :23-36, NS component
+:23-33): the other solver's solution interpolated at this solver's nodes (the identity when
+both meshes agree, which the coupler then skips).
+
+Modes (:40-41,75-93):
+    'JNK'  Newton; linear system by restarted GMRES (restart 20, atol = mtol_gmres*sqrt(DOF),
+           rtol 0) preconditioned by one block-Jacobi sweep (each component's solve_linear:
+           cd._get_update / ns._get_update).  OpenMDAO's ScipyKrylov hands the preconditioner
+           to SciPy's GMRES as M, i.e. on the LEFT; krylov.gmres_left restates that algorithm
+           (see its docstring for why the side matters here).  The block-Jacobi sweep is the
+           block-diagonal solve: zero initial guesses, no off-diagonal terms (the coupler's
+           comment says it "requires change in linear_block_jac.py"; the changed file is not
+           in the reference, so this is the textbook block-Jacobi preconditioner).
+    'NJ'   Newton whose linear solve is the block-Jacobi sweep alone, with an Armijo-Goldstein
+           line search (maxiter AGi, contraction AGr, slope AGc).
+    'GS'   nonlinear block Gauss-Seidel: CD solve, then NS solve, until the residual norm is
+           below atol.
+Newton starts as OpenMDAO's NewtonSolver(solve_subsystems=True, max_sub_solves=0) does: one
+Gauss-Seidel pass of the subsystems' solve_nonlinear, then pure Newton steps.  Convergence is
+||R||_2 <= mtol_nonlin * sqrt(DOF), DOF = 3 N_ns + N_cd (:61-63).
+"""
+import math
+
+import numpy as np
+import torch
+
+from ..krylov import gmres_left
+
+
+class BoussinesqCoupler:
+    def __init__(self, L_x, L_y, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4, N_ex_cd=8, N_ey_cd=8, P_ns=4, N_ex_ns=8,
+                 N_ey_ns=8, mode='JNK', mtol_nonlin=1e-9, AGi=8, AGr=0.8, AGc=0.2, mtol_gmres=1e-10, restart=20,
+                 mtol_internal=1e-13, maxiter=None, iprint=0, cd=None, ns=None):
+        if mode not in ('JNK', 'NJ', 'GS'):
+            raise ValueError('Unknown method')
+        self.mode, self.iprint = mode, iprint
+        self.AGi, self.AGr, self.AGc, self.restart = AGi, AGr, AGc, restart
+        # backend solvers exactly as the couplers build them (:52-59)
+        if cd is None:
+            from .convection_diffusion import ConvectionDiffusionSolver
+            cd = ConvectionDiffusionSolver(L_x=L_x, L_y=L_y, Pe=Re * Pr, P=P_cd, N_ex=N_ex_cd, N_ey=N_ey_cd,
+                                           T_W=0.5, T_E=-0.5, mtol=mtol_internal)
+        if ns is None:
+            from .navier_stokes import NavierStokesSolver
+            ns = NavierStokesSolver(L_x=L_x, L_y=L_y, Re=Re, Gr=Ra / Pr, P=P_ns, N_ex=N_ex_ns, N_ey=N_ey_ns,
+                                    mtol=mtol_internal, mtol_newton=mtol_internal, iprint=[])
+        self.cd, self.ns = cd, ns
+        self.Ncd, self.Nns = cd.N, ns.N
+        self.DOF = 3 * self.Nns + self.Ncd
+        self.atol_gmres = mtol_gmres * math.sqrt(self.DOF)
+        self.atol_nonlin = mtol_nonlin * math.sqrt(self.DOF)
+        self.maxiter = maxiter if maxiter is not None else {'JNK': 100, 'NJ': 1000, 'GS': 1000}[mode]
+        self._same_mesh = (cd._P, cd._N_ex, cd._N_ey) == (ns._P, ns._N_ex, ns._N_ey)
+        self.iterations = 0
+
+    # ------------------------------------------------------------------ mesh transfers (change_inputs)
+    def _to_cd(self, f_ns):
+        """ConvectionDiffusion_Component.change_inputs (:23-36): NS field at the CD nodes."""
+        if self._same_mesh:
+            return np.array(f_ns, dtype=np.float64, copy=True)
+        cd = self.cd
+        shape = (2, cd._P * cd._N_ex + 1, cd._P * cd._N_ey + 1)
+        return np.asarray(self.ns._get_interpol(f_ns, np.reshape(cd.points, shape))).flatten()
+
+    def _to_ns(self, f_cd):
+        """NavierStokes_Component.change_inputs (:23-33): CD field at the NS nodes."""
+        if self._same_mesh:
+            return np.array(f_cd, dtype=np.float64, copy=True)
+        ns = self.ns
+        shape = (2, ns._P * ns._N_ex + 1, ns._P * ns._N_ey + 1)
+        return np.asarray(self.cd._get_interpol(f_cd, np.reshape(ns.points, shape))).flatten()
+
+    # ------------------------------------------------------------------ packing
+    def _split(self, x):
+        n, m = self.Ncd, self.Nns
+        return x[:n], x[n:n + m], x[n + m:n + 2 * m], x[n + 2 * m:]
+
+    @staticmethod
+    def _join(*parts):
+        return np.concatenate([np.asarray(a, dtype=np.float64) for a in parts])
+
+    # ------------------------------------------------------------------ component maps
+    def residuals(self, x):
+        """apply_nonlinear of both components (CD :38-39, NS :35-37)."""
+        T, u, v, p = self._split(x)
+        rT = self.cd._get_residuals(T, self._to_cd(u), self._to_cd(v))
+        ru, rv, rp = self.ns._get_residuals(u, v, p, self._to_ns(T))
+        return self._join(rT, ru, rv, rp)
+
+    def linearize(self, x):
+        """linearize of both components (CD :41-42, NS :39-40); called after residuals(x)."""
+        T, u, v, _ = self._split(x)
+        self.cd._calc_jacobians(T)
+        self.ns._calc_jacobians(u, v)
+
+    def jacobian_apply(self, dx):
+        """apply_linear, fwd mode (CD :44-49, NS :42-50): the coupled Jacobian on dx."""
+        dT, du, dv, dp = self._split(dx)
+        rT = self.cd._get_dresiduals(dT, self._to_cd(du), self._to_cd(dv))
+        ru, rv, rp = self.ns._get_dresiduals(du, dv, dp, self._to_ns(dT))
+        return self._join(rT, ru, rv, rp)
+
+    def block_jacobi(self, r):
+        """LinearBlockJac(maxiter=1): each component's solve_linear on its own residual block
+        (CD :51-57, NS :52-60), zero initial guesses."""
+        rT, ru, rv, rp = self._split(r)
+        dT = self.cd._get_update(rT, dT0=np.zeros(self.Ncd))
+        z = np.zeros(self.Nns)
+        du, dv, dp = self.ns._get_update(ru, rv, rp, du0=z, dv0=z, dp0=z)
+        return self._join(dT, du, dv, dp)
+
+    def gauss_seidel_pass(self, x):
+        """One pass of the subsystems' solve_nonlinear in group order (CD :59-61, NS :62-65)."""
+        T, u, v, p = self._split(x)
+        T = self.cd._get_solution(self._to_cd(u), self._to_cd(v), T0=T)
+        u, v, p = self.ns._get_solution(self._to_ns(T), u0=u, v0=v, p0=p)
+        return self._join(T, u, v, p)
+
+    # ------------------------------------------------------------------ solvers
+    def _log(self, msg):
+        if self.iprint:
+            print(msg)
+
+    def solve(self, x0=None):
+        """Run the coupled solve; returns (T, u, v, p) global vectors (NumPy)."""
+        x = np.zeros(self.DOF) if x0 is None else np.array(x0, dtype=np.float64)
+        x = self._solve_gs(x) if self.mode == 'GS' else self._solve_newton(x)
+        return tuple(np.array(a) for a in self._split(x))
+
+    def _solve_gs(self, x):
+        for k in range(self.maxiter):
+            x = self.gauss_seidel_pass(x)
+            norm = np.linalg.norm(self.residuals(x))
+            self._log(f'NLBGS {k + 1} ; {norm}')
+            self.iterations = k + 1
+            if norm <= self.atol_nonlin:
+                return x
+        raise RuntimeError(f'NLBGS failed to converge in {self.maxiter} iterations')
+
+    def _solve_newton(self, x):
+        x = self.gauss_seidel_pass(x)  # solve_subsystems=True, max_sub_solves=0: at iteration 0 only
+        r = self.residuals(x)
+        norm = np.linalg.norm(r)
+        self._log(f'Newton 0 ; {norm}')
+        k = 0
+        while norm > self.atol_nonlin:
+            if k >= self.maxiter:
+                raise RuntimeError(f'Newton failed to converge in {self.maxiter} iterations')
+            self.linearize(x)
+            if self.mode == 'JNK':
+                x = x + self._linear_jnk(-r)
+                r = self.residuals(x)
+                norm = np.linalg.norm(r)
+            else:
+                x, r, norm = self._armijo_goldstein(x, self.block_jacobi(-r), norm)
+            k += 1
+            self._log(f'Newton {k} ; {norm}')
+        self.iterations = k
+        return x
+
+    def _linear_jnk(self, b):
+        """GMRES on the coupled Jacobian, block-Jacobi preconditioned (ScipyKrylov :89-91)."""
+        mv = lambda t: torch.from_numpy(self.jacobian_apply(t.numpy()))  # noqa: E731
+        pc = lambda t: torch.from_numpy(self.block_jacobi(t.numpy()))  # noqa: E731
+        res = gmres_left(mv, torch.from_numpy(np.ascontiguousarray(b)), atol=self.atol_gmres, rtol=0.0,
+                         restart=self.restart, maxiter=5000, precond=pc)
+        if res.info != 0:
+            raise RuntimeError(f'GMRES failed to converge in {res.info} restarts')
+        return res.x.numpy()
+
+    def _armijo_goldstein(self, x, dx, norm0):
+        """ArmijoGoldsteinLS(maxiter=AGi, rho=AGr, c=AGc) on the residual norm along dx."""
+        alpha = 1.0
+        x_new = x + dx
+        r_new = self.residuals(x_new)
+        n_new = np.linalg.norm(r_new)
+        for _ in range(self.AGi):
+            if n_new <= norm0 * (1.0 - self.AGc * alpha):
+                break
+            alpha *= self.AGr
+            x_new = x + alpha * dx
+            r_new = self.residuals(x_new)
+            n_new = np.linalg.norm(r_new)
+        return x_new, r_new, n_new
+
+
+def run(points_plot, L_x, L_y, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4, N_ex_cd=8, N_ey_cd=8, P_ns=4, N_ex_ns=8, N_ey_ns=8,
+        mode='JNK', mtol_nonlin=1e-9, AGi=8, AGr=0.8, AGc=0.2, mtol_gmres=1e-10, restart=20, mtol_internal=1e-13):
+    """Drop-in for OpenMDAO/Boussinesq_SequentialCoupler.py:10-108 `run` (and the ParallelCoupler's):
+    same arguments, returns (T_plot, u_plot, v_plot) interpolated at points_plot."""
+    c = BoussinesqCoupler(L_x, L_y, Re, Ra, Pr, P_cd, N_ex_cd, N_ey_cd, P_ns, N_ex_ns, N_ey_ns, mode=mode,
+                          mtol_nonlin=mtol_nonlin, AGi=AGi, AGr=AGr, AGc=AGc, mtol_gmres=mtol_gmres, restart=restart,
+                          mtol_internal=mtol_internal)
+    T, u, v, _ = c.solve()
+    return (np.asarray(c.cd._get_interpol(T, points_plot)), np.asarray(c.ns._get_interpol(u, points_plot)),
+            np.asarray(c.ns._get_interpol(v, points_plot)))

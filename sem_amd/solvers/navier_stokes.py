@@ -127,6 +127,7 @@ class NavierStokesSolver:
         self._Jac_v_v = self._Sys + Re * SEM.tensordot(self._C_y, V, (2, 0))
         self._Jac_u_v = Re * SEM.tensordot(self._C_y, U, (2, 0))
         self._Jac_v_u = Re * SEM.tensordot(self._C_x, V, (2, 0))
+        self._velo_lu = None  # factorised on first use, reused until the next linearisation
 
     def _get_dresiduals(self, du, dv, dp, dT=None):
         """NavierStokes_Solver.py:138-160."""
@@ -151,10 +152,13 @@ class NavierStokesSolver:
         rc = self._continuity(DU, DV, DP)
         return self._out(ru, du), self._out(rv, du), self._out(rc, du)
 
-    def _get_update(self, dres_u, dres_v, dres_cont, du0=None, dv0=None, dp0=None):
-        """Velocity LU + pressure Schur LGMRES (NavierStokes_Solver.py:162-236)."""
-        host = lambda a: a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)  # noqa: E731
-        dres_u, dres_v, dres_cont = host(dres_u), host(dres_v), host(dres_cont)
+    def _velo_factor(self):
+        """SuperLU of the Dirichlet-row-replaced velocity Jacobian (NavierStokes_Solver.py:176-183).
+        The reference refactorises on every _get_update call; the factor depends only on the
+        Jacobians, so it is kept until _calc_jacobians runs again (the Boussinesq coupler's
+        block-Jacobi preconditioner calls _get_update once per Krylov iteration)."""
+        if getattr(self, "_velo_lu", None) is not None:
+            return self._velo_lu
         tStart = time.perf_counter()
         mask = np.hstack((self._mask_bound,) * 2)
         Jac_velo = sp_sparse.bmat([[self._Jac_u_u.tocsr(), self._Jac_u_v.tocsr()],
@@ -162,10 +166,17 @@ class NavierStokesSolver:
         Jac_velo[mask, :] = 0
         Jac_velo[mask, mask] = 1
         Jac_velo = Jac_velo.tocsc()
-        Jac_velo_lu = linalg.splu(Jac_velo)
+        self._velo_lu = linalg.splu(Jac_velo)
         if 'LU_suc' in self._iprint:
             print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec '
-                  f'with fill factor {Jac_velo_lu.nnz/Jac_velo.nnz:0.1f}')
+                  f'with fill factor {self._velo_lu.nnz/Jac_velo.nnz:0.1f}')
+        return self._velo_lu
+
+    def _get_update(self, dres_u, dres_v, dres_cont, du0=None, dv0=None, dp0=None):
+        """Velocity LU + pressure Schur LGMRES (NavierStokes_Solver.py:162-236)."""
+        host = lambda a: a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)  # noqa: E731
+        dres_u, dres_v, dres_cont = host(dres_u), host(dres_v), host(dres_cont)
+        Jac_velo_lu = self._velo_factor()
 
         def solve_jac_velo(a, b):
             return np.split(Jac_velo_lu.solve(np.hstack((a, b))), 2)

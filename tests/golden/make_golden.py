@@ -250,6 +250,38 @@ def gen_checksums(SEM):
     np.savez_compressed(os.path.join(OUT, "cfg2_checksums.npz"), **d)
 
 
+def gen_boussinesq(CDS, NSS):
+    """Coupled natural convection (OpenMDAO/Boussinesq_SequentialCoupler.py:10-108) with the
+    reference's own solver classes, driven by sem_amd.solvers.boussinesq.BoussinesqCoupler (the
+    OpenMDAO driver itself is not installed here).  Case "a": equal meshes 4x4 P=4, JNK;
+    case "b": CD on 4x4 P=4, NS on 3x3 P=6 (exercises the change_inputs mesh transfers), JNK;
+    case "c": same as "a" in NJ mode."""
+    sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..")))
+    from sem_amd.solvers.boussinesq import BoussinesqCoupler
+    d = {}
+    cases = {"a": (4, 4, 4, 4, 4, 4, "JNK"), "b": (4, 4, 4, 6, 3, 3, "JNK"), "c": (4, 4, 4, 4, 4, 4, "NJ")}
+    for key, (Pc, nxc, nyc, Pn, nxn, nyn, mode) in cases.items():
+        Re, Ra, Pr = 1e3, 1e3, 0.71
+        cd = CDS(L_x=1.0, L_y=1.0, Pe=Re * Pr, P=Pc, N_ex=nxc, N_ey=nyc, T_W=0.5, T_E=-0.5, mtol=1e-13)
+        ns = NSS(L_x=1.0, L_y=1.0, Re=Re, Gr=Ra / Pr, P=Pn, N_ex=nxn, N_ey=nyn, mtol=1e-13, mtol_newton=1e-13,
+                 iprint=[])
+        c = BoussinesqCoupler(1.0, 1.0, Re, Ra, Pr, Pc, nxc, nyc, Pn, nxn, nyn, mode=mode, cd=cd, ns=ns)
+        T, u, v, p = c.solve()
+        d[key + "_cfg"] = np.array([Pc, nxc, nyc, Pn, nxn, nyn])
+        d[key + "_mode"] = np.array(mode)
+        d[key + "_T"], d[key + "_u"], d[key + "_v"], d[key + "_p"] = T, u, v, p
+        d[key + "_iters"] = np.array(c.iterations)
+        # one coupled residual / Jacobian evaluation at a seeded state
+        r = np.random.default_rng(31)
+        x = r.uniform(-0.5, 0.5, c.DOF)
+        dx = r.uniform(-1, 1, c.DOF)
+        d[key + "_x"], d[key + "_dx"] = x, dx
+        d[key + "_R"] = c.residuals(x)
+        c.linearize(x)
+        d[key + "_JR"] = c.jacobian_apply(dx)
+    np.savez_compressed(os.path.join(OUT, "bous.npz"), **d)
+
+
 def main():
     install_adapters()
     from Solvers import GLL, SEM
@@ -261,6 +293,7 @@ def main():
     gen_cd(ConvectionDiffusionSolver)
     gen_ns(NavierStokesSolver)
     gen_checksums(SEM)
+    gen_boussinesq(ConvectionDiffusionSolver, NavierStokesSolver)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -41,3 +41,35 @@ def test_gmres_restarts_and_preconditioner():
     assert r.info == 0 and np.linalg.norm(M @ r.x.numpy() - b) <= 1e-10 * 1.0001
     r2 = gmres(mv, torch.from_numpy(b), atol=1e-300, restart=5, maxiter=7)
     assert r2.info == 7  # not converged: iterations performed, as SciPy reports
+
+
+def test_gmres_left_matches_scipy_left_preconditioned():
+    """krylov.gmres_left restates SciPy's gmres (left preconditioner M): same stopping rule,
+    converged to the same solution, M only ever applied to vectors in range(A)."""
+    from sem_amd.krylov import gmres_left
+    rng = np.random.default_rng(3)
+    n = 300
+    A = np.diag(np.linspace(1, 200, n)) + 0.1 * rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    dinv = 1.0 / np.diag(A)
+    mv = lambda v: torch.from_numpy(A @ v.numpy())  # noqa: E731
+    r = gmres_left(mv, torch.from_numpy(b), atol=1e-9, restart=20, maxiter=500,
+                   precond=lambda v: torch.from_numpy(dinv * v.numpy()))
+    assert r.info == 0 and np.linalg.norm(A @ r.x.numpy() - b) <= 1e-9
+    M = spla.LinearOperator((n, n), matvec=lambda v: dinv * v, dtype=float)
+    ref, info = spla.gmres(A, b, atol=1e-9, rtol=0, restart=20, maxiter=500, M=M)
+    assert info == 0
+    assert np.abs(r.x.numpy() - ref).max() < 1e-8
+    # not converged: info = maxiter (restarts), as SciPy reports
+    r2 = gmres_left(mv, torch.from_numpy(b), atol=1e-300, restart=4, maxiter=3)
+    assert r2.info == 3
+    assert gmres_left(mv, torch.zeros(n, dtype=torch.float64)).info == 0
+
+
+def test_gmres_left_cd_system():
+    from sem_amd.krylov import gmres_left
+    cd, A, b = _cd_system()
+    atol = 1e-9 * np.sqrt(cd.N)
+    mv = lambda v: torch.from_numpy(A.matvec(v.numpy()))  # noqa: E731
+    r = gmres_left(mv, torch.from_numpy(b), atol=atol, restart=20, maxiter=5000)
+    assert r.info == 0 and np.linalg.norm(A.matvec(r.x.numpy()) - b) <= atol

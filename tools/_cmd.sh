@@ -1,6 +1,6 @@
+#!/bin/bash
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_apply.py tests/test_gpu_partition.py -x -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider -k "4]" > gpurun_out/t_band.log 2>&1
-rc=$?; tail -3 gpurun_out/t_band.log; [ $rc -ne 0 ] && exit $rc
-for T in 0 1 2; do
-  echo "== tile $T"; SEM_BAND_TILE=$T timeout -k 10 120 python tools/kbench.py --algo 4 --meshes 8:64,12:128,8:256,8:1024 --reps 200 || exit $?
-done
+mkdir -p gpurun_out/r01d
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_boussinesq.py > gpurun_out/r01d/bous.log 2>&1 || { tail -30 gpurun_out/r01d/bous.log; exit 1; }
+tail -8 gpurun_out/r01d/bous.log
+timeout -k 10 300 python bench.py > gpurun_out/r01d/bench.json 2> gpurun_out/r01d/bench.err && cat gpurun_out/r01d/bench.json
