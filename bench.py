@@ -11,7 +11,7 @@ Pe = 40, T, u, v ~ U(-1, 1) from default_rng(2024)).  N = 263,169 DOFs per
 GPU; inputs resident in HBM before the timed region.  With --gpus N > 1 each
 rank holds one 64-element-column strip of a (64 N) x 64 mesh (weak scaling)
 and every step ends with the interface-line exchange (RCCL all-reduce of the
-shared-edge partial sums).
+shared-edge partial sums, or --exchange p2p: send/recv with the two neighbours).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N bench.py --gpus N ...
@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="capture steps in hipGraphs (N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--hbm-ne", type=int, default=1024, help="HBM-regime mesh size (0 = skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the measured path); gloo only to rehearse N > 1 on a 1-GPU box")
+    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "p2p"],
+                    help="interface assembly for N > 1: one RCCL all-reduce, or send/recv with the two neighbours")
     return ap.parse_args()
 
 
@@ -169,8 +173,12 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks may share one GPU
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
@@ -188,7 +196,7 @@ def main():
     y = torch.empty_like(T)
     sides = _lib.SIDE_W | _lib.SIDE_E
     kw = dict(c_stiff=1.0, c_gradx=Pe, cu=u, c_grady=Pe, cv=v, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides)
-    exch = part.exchanger(mesh, dist) if world > 1 else None
+    exch = part.exchanger(mesh, dist, kind=args.exchange) if world > 1 else None
 
     def step():
         mesh.apply(T, y, **kw)
@@ -223,8 +231,10 @@ def main():
         "data": "synthetic (T,u,v ~ U(-1,1), default_rng(2024+rank); Pe=40; Dirichlet W/E rows)",
         "config": {"workload": workload, "mesh_per_gpu": f"{ne}x{ne} elements", "P": P,
                    "global_mesh": f"{nex}x{ney}", "dofs_global": N_glob, "dofs_per_gpu": n_loc,
-                   "partition": f"element-column strips x{world}" + (", RCCL all-reduce of interface lines"
-                                                                       if world > 1 else ""),
+                   "partition": f"element-column strips x{world}" + (
+                       {"allreduce": ", RCCL all-reduce of interface lines",
+                        "p2p": ", RCCL send/recv of interface lines with neighbours"}[args.exchange]
+                       if world > 1 else ""),
                    "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": bool(args.graph and
                                                                                          world == 1)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -11,6 +11,15 @@ packed into a (G-1)*NY buffer, summed across ranks with one RCCL all-reduce
 over xGMI (torch.distributed backend "nccl" = RCCL on ROCm), and unpacked.  The
 payload is tiny (28.7 KB at 64^2 elements per GPU, G = 8) -- a latency-bound
 collective; nothing else crosses GPUs.
+
+NeighborExchange is the point-to-point alternative: in the x-major numbering an
+interface line is a contiguous slice of the local vector (the first / last NY
+entries), so each rank sends its two partial-sum lines straight to its left and
+right neighbours (one batch of RCCL send/recv pairs over the xGMI links to those
+two GPUs) and adds what it receives.  No pack kernel, 2 x NY x 8 bytes per link
+and direction, and no rank waits on a ring through all G ranks.  Both exchanges
+give bitwise-identical results (each shared node is the sum of exactly two partial
+sums, and a + b == b + a in IEEE arithmetic).
 """
 import torch
 
@@ -32,9 +41,14 @@ class StripPartition:
         """(left_slot, right_slot) of this rank's interface lines in the exchange buffer (-1 = none)."""
         return (rank - 1 if rank > 0 else -1), (rank if rank < self.world - 1 else -1)
 
-    def exchanger(self, mesh, dist, group=None):
-        """Callable y -> y with the interface partial sums assembled across ranks."""
-        return InterfaceExchange(self, mesh, dist, group)
+    def exchanger(self, mesh, dist, group=None, kind="allreduce"):
+        """Callable y -> y with the interface partial sums assembled across ranks.
+        kind: "allreduce" (one collective over all interface slots) or "p2p" (neighbours only)."""
+        if kind == "allreduce":
+            return InterfaceExchange(self, mesh, dist, group)
+        if kind == "p2p":
+            return NeighborExchange(self, mesh, dist, group)
+        raise ValueError("exchange kind must be 'allreduce' or 'p2p'")
 
 
 class InterfaceExchange:
@@ -48,4 +62,40 @@ class InterfaceExchange:
         self.mesh.interface_pack(y, self.part.bounds, self.buf)
         self.dist.all_reduce(self.buf, group=self.group)
         self.mesh.interface_unpack(self.buf, self.part.bounds, y)
+        return y
+
+
+class NeighborExchange:
+    """Interface assembly by point-to-point exchange with the two neighbouring strips."""
+
+    def __init__(self, part, mesh, dist, group=None):
+        self.part, self.mesh, self.dist, self.group = part, mesh, dist, group
+        self.rank = part.bounds.index(mesh.ex_begin if hasattr(mesh, "ex_begin") else mesh.eb)
+        self.NY = mesh.NY
+        left, right = part.slots(self.rank)
+        self.left = self.rank - 1 if left >= 0 else None
+        self.right = self.rank + 1 if right >= 0 else None
+        self.recv_l = torch.empty(self.NY, dtype=torch.float64, device=mesh.device) if self.left is not None else None
+        self.recv_r = torch.empty(self.NY, dtype=torch.float64, device=mesh.device) if self.right is not None else None
+
+    def _peer(self, r):
+        return r if self.group is None else self.dist.get_global_rank(self.group, r)
+
+    def __call__(self, y):
+        if self.part.world == 1:
+            return y
+        NY, d = self.NY, self.dist
+        ops = []
+        if self.left is not None:
+            ops.append(d.P2POp(d.isend, y[:NY], self._peer(self.left), self.group))
+            ops.append(d.P2POp(d.irecv, self.recv_l, self._peer(self.left), self.group))
+        if self.right is not None:
+            ops.append(d.P2POp(d.isend, y[-NY:], self._peer(self.right), self.group))
+            ops.append(d.P2POp(d.irecv, self.recv_r, self._peer(self.right), self.group))
+        for req in d.batch_isend_irecv(ops):
+            req.wait()
+        if self.left is not None:
+            y[:NY] += self.recv_l
+        if self.right is not None:
+            y[-NY:] += self.recv_r
         return y

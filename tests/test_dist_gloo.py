@@ -1,5 +1,6 @@
 """World-size-2 gloo test (CPU) of the element-strip decomposition and the interface
-exchange protocol of sem_amd.parallel.InterfaceExchange.
+exchange protocols of sem_amd.parallel (InterfaceExchange: one all-reduce;
+NeighborExchange: point-to-point with the two neighbouring strips).
 
 The device kernels cannot run here, so each rank's local apply is the oracle's
 matrix-free apply on its own strip of elements (the same partial sums the kernel
@@ -56,7 +57,7 @@ class StripDouble:
             y[-self.NY:] = buf[right * self.NY:(right + 1) * self.NY]
 
 
-def _worker(rank, world, port, P, nex, ney, q):
+def _worker(rank, world, port, P, nex, ney, q, kind="allreduce"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -76,7 +77,7 @@ def _worker(rank, world, port, P, nex, ney, q):
         mesh = StripDouble(P, nex, ney, dx, dy, eb, ee)
         sl = slice(mesh.dof_begin, mesh.dof_begin + mesh.n_local)
         y = mesh.apply(x[sl], mask, g[sl])
-        y = part.exchanger(mesh, dist)(y)
+        y = part.exchanger(mesh, dist, kind=kind)(y)
         want = O.apply_matrix_free(P, nex, ney, dx, dy, x, c_stiff=1.0)
         want[mask] = x[mask] - g[mask]
         err = np.abs(y.numpy() - want[sl]).max() / np.abs(want).max()
@@ -91,12 +92,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,P,nex,ney", [(2, 4, 6, 5), (2, 8, 9, 4), (3, 5, 7, 3)])
-def test_interface_exchange_gloo(world, P, nex, ney):
+@pytest.mark.parametrize("kind", ["allreduce", "p2p"])
+@pytest.mark.parametrize("world,P,nex,ney", [(2, 4, 6, 5), (2, 8, 9, 4), (3, 5, 7, 3), (4, 3, 8, 2)])
+def test_interface_exchange_gloo(world, P, nex, ney, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, P, nex, ney, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, nex, ney, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
@@ -113,3 +115,5 @@ def test_partition_bounds():
     assert [p.slots(r) for r in range(3)] == [(-1, 0), (0, 1), (1, -1)]
     with pytest.raises(ValueError):
         StripPartition(2, 3)
+    with pytest.raises(ValueError):
+        p.exchanger(None, None, kind="ring")
