@@ -232,8 +232,9 @@ def main():
         "config": {"workload": workload, "mesh_per_gpu": f"{ne}x{ne} elements", "P": P,
                    "global_mesh": f"{nex}x{ney}", "dofs_global": N_glob, "dofs_per_gpu": n_loc,
                    "partition": f"element-column strips x{world}" + (
-                       {"allreduce": ", RCCL all-reduce of interface lines",
-                        "p2p": ", RCCL send/recv of interface lines with neighbours"}[args.exchange]
+                       {"allreduce": ", all-reduce of interface lines",
+                        "p2p": ", send/recv of interface lines with neighbours"}[args.exchange]
+                       + (" (RCCL)" if args.dist_backend == "nccl" else " (gloo rehearsal)")
                        if world > 1 else ""),
                    "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": bool(args.graph and
                                                                                          world == 1)},

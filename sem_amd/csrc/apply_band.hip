@@ -233,7 +233,8 @@ struct BandArgs {
   double fKx, fKy, fM, fX, fY;  // cK*dy/dx, cK*dx/dy, cM*dx*dy/4, cX*dy/2, cY*dx/2
   int NY, lb0, lb1, ex_begin, ex_end, ney, nex, NXg, tiles_y, nbytes, dir_mode, diag;
   unsigned sides, flags;  // flags: 1 = cu given, 2 = cv given
-  int nblk, pad_;         // grid size (gridDim would be a second, dependent kernarg fetch)
+  int nblk;               // grid size (gridDim would be a second, dependent kernarg fetch)
+  int cpol;               // cache policy of the y stores / u,v loads (SEM_BAND_CPOL; see bstore_any)
   // FULL kernels only
   const double* ea;
   const double* eb;
@@ -301,6 +302,17 @@ __device__ __forceinline__ double finish_node(const BandArgs& a, const NodeOps& 
   return z;
 }
 
+// y store with the launch's cache policy (wave-uniform switch; the policy must be an immediate).
+__device__ __forceinline__ void bstore_any(int cpol, __amdgpu_buffer_rsrc_t r, int off, double v) {
+  switch (cpol & 255) {
+    case 1: bstore_c<2>(r, off, v); break;     // non-temporal
+    case 2: bstore_c<16>(r, off, v); break;    // sc1
+    case 3: bstore_c<17>(r, off, v); break;    // sc0 sc1 (system scope: write through L2)
+    case 4: bstore_c<19>(r, off, v); break;    // nt + sc0 sc1
+    default: bstore(r, off, v);
+  }
+}
+
 // GLL weight w_J of order P for a runtime J (compile-time constants, no memory access).
 template <int P>
 __device__ __forceinline__ double gll_w(int J) {
@@ -350,6 +362,7 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
   BPIN(a.flags);
   BPIN(a.stamps);
   BPIN(a.nblk);
+  BPIN(a.cpol);
 
   // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
   // tiles (y fastest) and neighbouring tiles share their halo lines through that XCD's L2.
@@ -409,8 +422,13 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
     const int r = q / LW, c = q - r * LW;
     const bool ok = q < BX * LW && r < rows_ok && c < cols_ok && !(a.diag & 32);  // diag 32: no u/v/y traffic
     eoff[e] = ok ? nodeb + r * NY + c : -(1 << 26);  // out of bounds: touches no memory
-    pu[e] = bload(ru, eoff[e] * 8);
-    pv[e] = bload(rv, eoff[e] * 8);
+    if (a.cpol & 256) {  // u, v are read once per launch: non-temporal
+      pu[e] = bload_c<2>(ru, eoff[e] * 8);
+      pv[e] = bload_c<2>(rv, eoff[e] * 8);
+    } else {
+      pu[e] = bload(ru, eoff[e] * 8);
+      pv[e] = bload(rv, eoff[e] * 8);
+    }
   }
   if constexpr (FULL) {
 #pragma unroll
@@ -528,7 +546,7 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
   for (int e = 0; e < C::NE; ++e) {
     const int q = tid + e * C::THREADS;
     const int r = q / LW, c = q - r * LW;
-    if (q < BX * LW && r < rows_ok && c < cols_ok && !(a.diag & 16)) bstore(ry, eoff[e] * 8, zz[e]);  // diag 16: no stores
+    if (q < BX * LW && r < rows_ok && c < cols_ok && !(a.diag & 16)) bstore_any(a.cpol, ry, eoff[e] * 8, zz[e]);
   }
   BSTAMP(5);
   if (a.stamps) {
@@ -551,6 +569,12 @@ static int hip_check_b(hipError_t e, const char* what) {
   if (e == hipSuccess) return SEM_OK;
   return set_error(SEM_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
+
+// Default cache policy (measured in-process, tools/ab_env.py, profiles/r01/band/cpol_ab.txt): on a mesh
+// whose working set stays in the MALL, system-scope y stores (sc0 sc1: written through L2 as they
+// are issued) save the end-of-kernel L2 writeback, 4.66 -> 4.38 us at cfg2; on HBM-sized meshes
+// that costs ~1 %, and non-temporal u, v loads (read once) are neutral to slightly better.
+static int band_cpol(long long n_local) { return 32LL * n_local < (128LL << 20) ? 3 : 256; }
 
 template <int P, int TXE, int TYE, int NS>
 static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
@@ -596,6 +620,10 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   b.has_e2 = g.has_e2;
   b.stamps = g.stamps;
   b.nblk = static_cast<int>(nblk);
+  {
+    const char* e = std::getenv("SEM_BAND_CPOL");  // cache-policy override, read per call (in-process A/B)
+    b.cpol = e ? std::atoi(e) : band_cpol(g.n_local32);
+  }
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   if (full)
     hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,

@@ -157,6 +157,16 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off, double
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v),
                                         r, off, 0, 0);
 }
+// Store / load with a compile-time cache policy (gfx950 CPol bits: 1 = sc0, 2 = nt, 16 = sc1).
+template <int CPOL>
+__device__ __forceinline__ void bstore_c(__amdgpu_buffer_rsrc_t r, int off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v),
+                                        r, off, 0, CPOL);
+}
+template <int CPOL>
+__device__ __forceinline__ double bload_c(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, CPOL));
+}
 
 
 }  // namespace sem
