@@ -129,14 +129,90 @@ struct EPlan {
   }
 };
 
+// Coefficient list of split S, in the order eo_rows consumes them (the DPP variant keeps them 16
+// per VGPR, lane l of every 16-lane row holding entry l, and broadcasts entry k with
+// v_fmac_f64_dpp row_newbcast:k -- one VALU operand instead of two s_mov_b32 per coefficient).
+// Per item: row 0 -> Ks(0,m), G(0,m) for m = 1..P; a pair -> SK, DK, SG, DG for m < H (+ Ks(it,c),
+// G(it,c) for even P); the centre row -> SK(c,m), DG(c,m) for m < H, then Ks(c,c), G(c,c).
+template <int P, int NS>
+struct CList {
+  using E = EOC<P>;
+  using L = EPlan<P, NS>;
+  static constexpr int H = E::H;
+  static constexpr int count(int kk) {
+    const int it = L::code(kk);
+    return it == 0 ? 2 * P : (it > 0 ? 4 * H + (E::EVEN ? 2 : 0) : 2 * H + 2);
+  }
+  static constexpr int base(int S, int kk) {
+    int b = 0;
+    for (int q = 0; q < kk; ++q)
+      if (L::in_split(q, S)) b += count(q);
+    return b;
+  }
+  static constexpr int size(int S) { return base(S, L::NITEMS); }
+  static constexpr int nmax() {
+    int m = 0;
+    for (int S = 0; S < NS; ++S) m = size(S) > m ? size(S) : m;
+    return m;
+  }
+  static constexpr int NCV = (nmax() + 15) / 16;  // VGPR pairs per lane
+  static constexpr int NPAD = 16 * (NCV > 0 ? NCV : 1);
+  static constexpr double value(int S, int j) {  // entry j of split S
+    for (int kk = 0; kk < L::NITEMS; ++kk) {
+      if (!L::in_split(kk, S)) continue;
+      const int b = base(S, kk);
+      if (j < b || j >= b + count(kk)) continue;
+      const int o = j - b, it = L::code(kk);
+      if (it == 0) return (o & 1) ? E::G(0, o / 2 + 1) : E::Ks(0, o / 2 + 1);
+      if (it > 0) {
+        if (o < 4 * H) {
+          const int m = o / 4, wh = o % 4;
+          return wh == 0 ? E::SK(it, m) : wh == 1 ? E::DK(it, m) : wh == 2 ? E::SG(it, m) : E::DG(it, m);
+        }
+        return o == 4 * H ? E::Ks(it, E::c) : E::G(it, E::c);
+      }
+      if (o < 2 * H) return (o & 1) ? E::DG(E::c, o / 2) : E::SK(E::c, o / 2);
+      return o == 2 * H ? E::Ks(E::c, E::c) : E::G(E::c, E::c);
+    }
+    return 0.0;
+  }
+  struct Tab {
+    double v[NS * NPAD];
+  };
+  static constexpr Tab make() {
+    Tab t{};
+    for (int S = 0; S < NS; ++S)
+      for (int j = 0; j < NPAD; ++j) t.v[S * NPAD + j] = value(S, j);
+    return t;
+  }
+};
+
+template <int P, int NS>
+__device__ const typename CList<P, NS>::Tab kBandCoef = CList<P, NS>::make();
+
+// acc + c * x: an immediate coefficient (c), or entry IDX of the split's DPP-broadcast list.  Only
+// valid with every lane of the wave active (a DPP read of a disabled lane does not return its value).
+template <bool DPP, int IDX, int NCV>
+__device__ __forceinline__ double cfma(const double (&cv)[NCV], double c, double x, double acc) {
+  if constexpr (DPP) {
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc)
+        : "v"(cv[IDX / 16]), "v"(x), "n"(IDX % 16));
+    return acc;
+  } else {
+    return fma(c, x, acc);
+  }
+}
+
 // Rows of split S of one element from a (2P+1)-node window t (t[P..2P] = the element, t[0..P] = the
 // left neighbour; absent elements are zero in the staged tile).  fk = hasL + hasR and
 // fg = hasR - hasL weight the shared node t[P] in row 0.  Results go to slots (EPlan order).
-template <int P, int NS, int S, int NR>
+template <int P, int NS, int S, bool DPP, int NR, int NCV>
 __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk, double fg, double (&k)[NR],
-                                        double (&g)[NR]) {
+                                        double (&g)[NR], const double (&cv)[NCV]) {
   using E = EOC<P>;
   using L = EPlan<P, NS>;
+  using CL = CList<P, NS>;
   constexpr int H = E::H;
   double e[H], o[H];
   if constexpr (L::needs_eo(S)) {
@@ -151,14 +227,15 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
     constexpr int it = L::code(kk);
     if constexpr (L::in_split(kk, S)) {
       constexpr int sl = L::slot(S, kk);
+      constexpr int cb = CL::base(S, kk);
       if constexpr (it == 0) {  // shared-node row 0 (+ the left element's row P)
         constexpr double k00 = E::Ks(0, 0), g00 = E::G(0, 0);
         double kv = (k00 * fk) * t[P], gv = (g00 * fg) * t[P];
         for_rows(std::make_integer_sequence<int, P>{}, [&](auto MI) {
           constexpr int m = decltype(MI)::value + 1;
           constexpr double km = E::Ks(0, m), gm = E::G(0, m);
-          kv = fma(km, t[P + m] + t[P - m], kv);
-          gv = fma(gm, t[P + m] - t[P - m], gv);
+          kv = cfma<DPP, cb + 2 * (m - 1)>(cv, km, t[P + m] + t[P - m], kv);
+          gv = cfma<DPP, cb + 2 * (m - 1) + 1>(cv, gm, t[P + m] - t[P - m], gv);
         });
         k[sl] = kv;
         g[sl] = gv;
@@ -167,15 +244,15 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
         for_rows(std::make_integer_sequence<int, H>{}, [&](auto MI) {
           constexpr int m = decltype(MI)::value;
           constexpr double sk = E::SK(it, m), dk = E::DK(it, m), sg = E::SG(it, m), dg = E::DG(it, m);
-          Ek = fma(sk, e[m], Ek);
-          Ok = fma(dk, o[m], Ok);
-          Eg = fma(sg, e[m], Eg);
-          Og = fma(dg, o[m], Og);
+          Ek = cfma<DPP, cb + 4 * m>(cv, sk, e[m], Ek);
+          Ok = cfma<DPP, cb + 4 * m + 1>(cv, dk, o[m], Ok);
+          Eg = cfma<DPP, cb + 4 * m + 2>(cv, sg, e[m], Eg);
+          Og = cfma<DPP, cb + 4 * m + 3>(cv, dg, o[m], Og);
         });
         if constexpr (E::EVEN) {
           constexpr double kc_ = E::Ks(it, E::c), gc_ = E::G(it, E::c);
-          Ek = fma(kc_, t[P + E::c], Ek);
-          Eg = fma(gc_, t[P + E::c], Eg);
+          Ek = cfma<DPP, cb + 4 * H>(cv, kc_, t[P + E::c], Ek);
+          Eg = cfma<DPP, cb + 4 * H + 1>(cv, gc_, t[P + E::c], Eg);
         }
         k[sl] = Ek + Ok;
         k[sl + 1] = Ek - Ok;
@@ -186,12 +263,12 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
         for_rows(std::make_integer_sequence<int, H>{}, [&](auto MI) {
           constexpr int m = decltype(MI)::value;
           constexpr double sk = E::SK(E::c, m), dg = E::DG(E::c, m);
-          kv = fma(sk, e[m], kv);
-          gv = fma(dg, o[m], gv);
+          kv = cfma<DPP, cb + 2 * m>(cv, sk, e[m], kv);
+          gv = cfma<DPP, cb + 2 * m + 1>(cv, dg, o[m], gv);
         });
         constexpr double kcc = E::Ks(E::c, E::c), gcc = E::G(E::c, E::c);
-        kv = fma(kcc, t[P + E::c], kv);
-        if constexpr (gcc != 0.0) gv = fma(gcc, t[P + E::c], gv);
+        kv = cfma<DPP, cb + 2 * H>(cv, kcc, t[P + E::c], kv);
+        if constexpr (gcc != 0.0) gv = cfma<DPP, cb + 2 * H + 1>(cv, gcc, t[P + E::c], gv);
         k[sl] = kv;
         g[sl] = gv;
       }
@@ -325,10 +402,12 @@ __device__ __forceinline__ double gll_w(int J) {
 }
 
 // FULL = false: no extra / accumulate terms, no Dirichlet mask or values (side bits only).
-template <int P, int TXE, int TYE, int NS, bool FULL>
+// DPP = true: row coefficients from the split's DPP-broadcast list (CList) instead of immediates.
+template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP>
 __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(const BandArgs a) {
   using C = BCfg<P, TXE, TYE, NS>;
   using PL = EPlan<P, NS>;
+  using CL = CList<P, NS>;
   constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW;
   __shared__ double Ts[C::RX * PT];
   __shared__ double XK[BX * PY];
@@ -412,6 +491,16 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
     const int rr = idx / C::RY, cc = idx - rr * C::RY;
     st[s] = bload(rx, sbase + (rr * NY + cc) * 8);
   }
+  // DPP variant: this wave's coefficient list (split of its role), entry 16 j + (lane & 15) in cv[j]
+  double cv[DPP ? CL::NCV : 1];
+  if constexpr (DPP) {
+    const int wsplit = w < C::NXW ? (w / C::XW) % NS : (w - C::NXW) / C::YW;
+    const double* tb = kBandCoef<P, NS>.v + wsplit * CL::NPAD + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < CL::NCV; ++j) cv[j] = tb[16 * j];
+  } else {
+    cv[0] = 0.0;
+  }
   // epilogue nodes of this thread: q = tid + e*THREADS -> tile line r = q / LW, column c = q % LW
   double pu[C::NE], pv[C::NE];
   int eoff[C::NE];
@@ -472,7 +561,7 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
 #pragma unroll
         for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
         double k[C::RP], g[C::RP];
-        eo_rows<P, NS, s>(t, fk, fg, k, g);
+        eo_rows<P, NS, s, DPP>(t, fk, fg, k, g, cv);
 #pragma unroll
         for (int sl = 0; sl < PL::nrows(s); ++sl) {
           const int i = PL::row(s, sl);
@@ -488,8 +577,11 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
     const int wy = w - C::NXW;
     const int h = wy / C::YW;
     const int t2 = (wy - h * C::YW) * 64 + lane;
-    const int r = t2 % BX, b = t2 / BX;
-    if (t2 < C::YL && r < rows_ok && b < n1 - n0) {
+    const bool yok = t2 < C::YL && t2 % BX < rows_ok && t2 / BX < n1 - n0;
+    // the DPP variant computes on every lane (a DPP read of a disabled lane is not its value) from
+    // clamped, in-bounds positions; only the LDS stores are predicated
+    const int r = DPP ? min(t2 % BX, BX - 1) : t2 % BX, b = DPP ? min(t2 / BX, C::YL / BX - 1) : t2 / BX;
+    if (DPP || yok) {
       const bool hasLy = n0 + b - 1 >= 0, hasRy = n0 + b < a.ney;
       const double fk = (hasLy ? 1.0 : 0.0) + (hasRy ? 1.0 : 0.0), fg = (hasRy ? 1.0 : 0.0) - (hasLy ? 1.0 : 0.0);
       const int i = r % P, ex = m0 + r / P;
@@ -505,12 +597,14 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
 #pragma unroll
         for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
         double k[C::RP], g[C::RP];
-        eo_rows<P, NS, hh>(t, fk, fg, k, g);
+        eo_rows<P, NS, hh, DPP>(t, fk, fg, k, g, cv);
+        if (yok) {
 #pragma unroll
-        for (int sl = 0; sl < PL::nrows(hh); ++sl) {
-          const int j = PL::row(hh, sl);
-          YK[r * PY + b * P + j] = sk * k[sl];
-          YG[r * PY + b * P + j] = sg * g[sl];
+          for (int sl = 0; sl < PL::nrows(hh); ++sl) {
+            const int j = PL::row(hh, sl);
+            YK[r * PY + b * P + j] = sk * k[sl];
+            YG[r * PY + b * P + j] = sg * g[sl];
+          }
         }
       });
     }
@@ -576,7 +670,7 @@ static int hip_check_b(hipError_t e, const char* what) {
 // that costs ~1 %, and non-temporal u, v loads (read once) are neutral to slightly better.
 static int band_cpol(long long n_local) { return 32LL * n_local < (128LL << 20) ? 3 : 256; }
 
-template <int P, int TXE, int TYE, int NS>
+template <int P, int TXE, int TYE, int NS, bool DPP = false>
 static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   using C = BCfg<P, TXE, TYE, NS>;
   const int ncols = h->ex_end - h->ex_begin;
@@ -626,11 +720,11 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   }
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   if (full)
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
-                       s, b);
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, DPP>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS),
+                       0, s, b);
   else
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS), 0,
-                       s, b);
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, DPP>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS),
+                       0, s, b);
   return hip_check_b(hipGetLastError(), "apply (band) launch");
 }
 
@@ -652,14 +746,23 @@ static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStrea
     if (force == 1) return launch_band<P, 1, S::TYE, 4>(args, h, s);
     if (force == 2) return launch_band<P, 2, S::TYE, 4>(args, h, s);
   }
+  if (force == 3) return launch_band<P, S::TXE, S::TYE, S::NS, true>(args, h, s);
+  if (force == 4) return launch_band<P, S::TXE, S::TYE, S::NS, false>(args, h, s);
+  // DPP-broadcast coefficients: 2-4 % faster from ~1M DOFs up (the VALU-bound regime), 2-3 % slower on
+  // the launch-latency-bound cfg2 mesh, whose extra coefficient loads sit on the critical path
+  // (profiles/r01/band/dpp_ab.txt)
+  if (args.n_local32 >= (1 << 20)) return launch_band<P, S::TXE, S::TYE, S::NS, true>(args, h, s);
   return launch_band<P, S::TXE, S::TYE, S::NS>(args, h, s);
 }
 
-std::string band_kernel_name(int P) {
+std::string band_kernel_name(int P, long long n_local) {
   const int TYE = std::max(1, 64 / P), TXE = std::min(4, std::max(1, 8 / P));
   const int NS = P >= 2 ? 2 : 1;
+  const char* e = std::getenv("SEM_BAND_TILE");
+  const int force = e ? std::atoi(e) : 0;
+  const bool dpp = force == 3 || (force == 0 && n_local >= (1 << 20));
   return "sem::apply_band<" + std::to_string(P) + ", " + std::to_string(TXE) + ", " + std::to_string(TYE) + ", " +
-         std::to_string(NS) + ">";
+         std::to_string(NS) + (dpp ? ", dpp" : "") + ">";
 }
 
 int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s) {

@@ -38,7 +38,7 @@
 namespace sem {
 
 int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s);  // apply_band.hip
-std::string band_kernel_name(int P);
+std::string band_kernel_name(int P, long long n_local);
 
 static int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) return SEM_OK;
@@ -1201,7 +1201,7 @@ int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
   std::string name;
   const int P = h->P;
   if (algo == SEM_ALGO_BAND || (algo == SEM_ALGO_AUTO && h->n_local < (int64_t(1) << 28))) {
-    name = band_kernel_name(P);
+    name = band_kernel_name(P, h->n_local);
   } else if (algo == SEM_ALGO_COLUMN || algo == SEM_ALGO_AUTO) {
     name = "sem::apply_tp_col<" + std::to_string(P) + ", 2, 64, 1>";
   } else if ((algo == SEM_ALGO_MFMA || algo == SEM_ALGO_AUTO) && P <= 15) {

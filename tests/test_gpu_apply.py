@@ -70,14 +70,24 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
          (8, 17, 5), (9, 3, 4), (10, 2, 2), (11, 3, 1), (12, 5, 3), (13, 2, 3), (14, 1, 2), (15, 2, 2), (16, 3, 2)]
 
 
-ALGOS = [1, 2, 3, 4]  # VALU two-phase, MFMA, VALU single-phase column kernel, assembled band
+ALGOS = [1, 2, 3, 4, "4dpp"]  # VALU two-phase, MFMA, column kernel, assembled band (+ DPP coefficient variant)
+BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2"}  # SEM_BAND_TILE values (read per call)
+
+
+def _algo(algo, monkeypatch):
+    """Select the kernel: an int is sem_apply_desc.algo; a band variant name also sets SEM_BAND_TILE."""
+    if isinstance(algo, str):
+        monkeypatch.setenv("SEM_BAND_TILE", BAND_VARIANTS[algo])
+        return 4
+    return algo
 
 
 @pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", CASES)
-def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo):
+def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo, monkeypatch):
     if algo == 2 and P > 15:
         pytest.skip("MFMA path covers P <= 15")
+    algo = _algo(algo, monkeypatch)
     from sem_amd.device import get_mesh
     Lx, Ly = 1.3, 0.7
     dx, dy = Lx / nex, Ly / ney
@@ -103,7 +113,8 @@ def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo):
 
 @pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", [(4, 4, 4), (8, 6, 5), (12, 3, 4), (8, 40, 33)])
-def test_dirichlet_rows(gpu, P, nex, ney, algo):
+def test_dirichlet_rows(gpu, P, nex, ney, algo, monkeypatch):
+    algo = _algo(algo, monkeypatch)
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.0 / ney)
@@ -136,8 +147,9 @@ def test_dirichlet_rows(gpu, P, nex, ney, algo):
 
 @pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", [(8, 130, 67), (12, 70, 45), (4, 300, 211)])
-def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo):
+def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo, monkeypatch):
     """Meshes big enough for the large-tile / persistent launch configurations."""
+    algo = _algo(algo, monkeypatch)
     from sem_amd.device import get_mesh
     dx, dy = 1.0 / nex, 2.0 / ney
     mesh = get_mesh(P, nex, ney, dx, dy)
@@ -149,6 +161,24 @@ def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo):
     X, U, V = (mesh.to_device(t) for t in (x, u, v))
     y = mesh.apply(X, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, algo=algo)
     assert rel(y, want) < TOL
+
+
+@pytest.mark.parametrize("P,nex,ney", [(P, 7, 5) for P in range(1, 17)] + [(8, 64, 64), (8, 3, 70)])
+def test_band_variants_bitwise_equal(gpu, P, nex, ney, monkeypatch):
+    """Band kernel variants (DPP-broadcast coefficients, other tile shapes) perform the same
+    operations in the same order as the default: results are bitwise identical."""
+    from sem_amd import _lib
+    from sem_amd.device import get_mesh
+    mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.5 / ney)
+    r = np.random.default_rng(P)
+    X, U, V = (mesh.to_device(r.uniform(-1, 1, mesh.n_local)) for _ in range(3))
+    kw = dict(c_mass=0.25, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, dir_mode=_lib.DIR_IDENTITY,
+              dir_sides=_lib.SIDE_W | _lib.SIDE_E, algo=4)
+    monkeypatch.delenv("SEM_BAND_TILE", raising=False)
+    base = mesh.apply(X, **kw)
+    for name in (["4dpp", "4t1", "4t2"] if P == 8 else ["4dpp"]):
+        monkeypatch.setenv("SEM_BAND_TILE", BAND_VARIANTS[name])
+        assert torch.equal(mesh.apply(X, **kw), base), name
 
 
 @pytest.mark.parametrize("key", ["P4_4x4", "P4_3x2", "P8_8x8", "P12_5x3"])

@@ -1,10 +1,8 @@
 #!/bin/bash
 set -o pipefail
-O=gpurun_out/r01g
+O=gpurun_out/r01k
 mkdir -p $O
-timeout -k 10 300 python -u tools/ab_env.py --var SEM_BAND_TILE --values 0,1,2 --meshes 8:64,8:256,8:1024 --rounds 5 > $O/tile.log 2>&1 || { tail -20 $O/tile.log; exit 1; }
-cat $O/tile.log
-for D in 0 16 48 112; do
-  SEM_DIAG=$D timeout -k 10 120 python -u tools/kbench.py --meshes 8:64 --reps 400 > $O/diag$D.log 2>&1 || { tail -5 $O/diag$D.log; exit 1; }
-  echo "SEM_DIAG=$D: $(grep 'P= 8' $O/diag$D.log)"
-done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_apply.py tests/test_gpu_partition.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+cat $O/bench.json
