@@ -745,6 +745,8 @@ static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStrea
   if constexpr (P == 8) {
     if (force == 1) return launch_band<P, 1, S::TYE, 4>(args, h, s);
     if (force == 2) return launch_band<P, 2, S::TYE, 4>(args, h, s);
+    if (force == 5) return launch_band<P, 2, S::TYE, 2, true>(args, h, s);
+    if (force == 6) return launch_band<P, 1, S::TYE, 1, true>(args, h, s);
   }
   if (force == 3) return launch_band<P, S::TXE, S::TYE, S::NS, true>(args, h, s);
   if (force == 4) return launch_band<P, S::TXE, S::TYE, S::NS, false>(args, h, s);

@@ -71,7 +71,7 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
 
 
 ALGOS = [1, 2, 3, 4, "4dpp"]  # VALU two-phase, MFMA, column kernel, assembled band (+ DPP coefficient variant)
-BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2"}  # SEM_BAND_TILE values (read per call)
+BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2", "4t5": "5", "4t6": "6", "4imm": "4"}  # SEM_BAND_TILE values (read per call)
 
 
 def _algo(algo, monkeypatch):
@@ -176,7 +176,7 @@ def test_band_variants_bitwise_equal(gpu, P, nex, ney, monkeypatch):
               dir_sides=_lib.SIDE_W | _lib.SIDE_E, algo=4)
     monkeypatch.delenv("SEM_BAND_TILE", raising=False)
     base = mesh.apply(X, **kw)
-    for name in (["4dpp", "4t1", "4t2"] if P == 8 else ["4dpp"]):
+    for name in (["4dpp", "4imm", "4t1", "4t2", "4t5", "4t6"] if P == 8 else ["4dpp", "4imm"]):
         monkeypatch.setenv("SEM_BAND_TILE", BAND_VARIANTS[name])
         assert torch.equal(mesh.apply(X, **kw), base), name
 
