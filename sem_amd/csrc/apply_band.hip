@@ -403,7 +403,10 @@ __device__ __forceinline__ double gll_w(int J) {
 
 // FULL = false: no extra / accumulate terms, no Dirichlet mask or values (side bits only).
 // DPP = true: row coefficients from the split's DPP-broadcast list (CList) instead of immediates.
-template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP>
+// GRAD = false: no gradient / convection terms (mass + stiffness only: the Laplacian K x, the
+// Helmholtz operators of Solvers/README.md, the NS pressure rows K[mask,:] p); the G rows are
+// then dead code and are not computed.
+template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD = true>
 __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(const BandArgs a) {
   using C = BCfg<P, TXE, TYE, NS>;
   using PL = EPlan<P, NS>;
@@ -567,7 +570,7 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
           const int i = PL::row(s, sl);
           if (xghost && i != 0) continue;  // a ghost position holds its row 0 only
           XK[(xa * P + i) * PY + xc] = k[sl];
-          XG[(xa * P + i) * PY + xc] = g[sl];
+          if constexpr (GRAD) XG[(xa * P + i) * PY + xc] = g[sl];
         }
       });
     }
@@ -603,7 +606,7 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
           for (int sl = 0; sl < PL::nrows(hh); ++sl) {
             const int j = PL::row(hh, sl);
             YK[r * PY + b * P + j] = sk * k[sl];
-            YG[r * PY + b * P + j] = sg * g[sl];
+            if constexpr (GRAD) YG[r * PY + b * P + j] = sg * g[sl];
           }
         }
       });
@@ -631,8 +634,10 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
       const double u_ = has_u ? pu[e] : 1.0, v_ = has_v ? pv[e] : 1.0;
       double z = fma(a.fKx * my, XK[o], YK[o]);
       z = fma(a.fM * mx * my, xv, z);
-      z = fma(a.fX * u_, my * XG[o], z);
-      z = fma(v_, YG[o], z);
+      if constexpr (GRAD) {
+        z = fma(a.fX * u_, my * XG[o], z);
+        z = fma(v_, YG[o], z);
+      }
       zz[e] = finish_node<FULL>(a, ops[e], gx0 + r, gy0 + c, xv, z);
     }
   }
@@ -719,12 +724,16 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
     b.cpol = e ? std::atoi(e) : band_cpol(g.n_local32);
   }
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
-  if (full)
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, DPP>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS),
-                       0, s, b);
+  const bool grad = g.cX != 0.0 || g.cY != 0.0;
+  const dim3 grid(static_cast<unsigned>(nblk)), block(C::THREADS);
+  if (full && grad)
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, DPP, true>), grid, block, 0, s, b);
+  else if (full)
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, DPP, false>), grid, block, 0, s, b);
+  else if (grad)
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, DPP, true>), grid, block, 0, s, b);
   else
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, DPP>), dim3(static_cast<unsigned>(nblk)), dim3(C::THREADS),
-                       0, s, b);
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, DPP, false>), grid, block, 0, s, b);
   return hip_check_b(hipGetLastError(), "apply (band) launch");
 }
 
