@@ -25,26 +25,37 @@ class GMRESResult:
         self.x, self.info, self.iters, self.res_norm, self.matvecs = x, info, iters, res_norm, matvecs
 
 
-def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, precond=None, callback=None):
+def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, precond=None, callback=None,
+          inner=None):
     """Right-preconditioned restarted GMRES.
 
     matvec(v) -> A v and precond(v) -> M^-1 v take and return 1-D tensors like b.
     Converges when ||b - A x||_2 <= max(atol, rtol * ||b||_2) (SciPy's criterion).
     info = 0 on convergence, else the number of iterations performed (SciPy's convention).
+    inner(V, w) -> V @ w (k inner products) replaces the local products; a partitioned solve passes
+    sem_amd.parallel.DistributedInner, so every rank sees the same Hessenberg entries and takes the
+    same path through the iteration.
     """
+    proj = inner if inner is not None else (lambda A, w: A @ w)
+
+    def vnorm(w):
+        if inner is None:
+            return torch.linalg.vector_norm(w).item()
+        return math.sqrt(max(proj(w.unsqueeze(0), w)[0].item(), 0.0))
+
     N = b.numel()
     dt, dev = b.dtype, b.device
     restart = min(N, restart or 100)
     maxiter = maxiter or 10 * N
     x = torch.zeros_like(b) if x0 is None else x0.clone()
-    bnorm = torch.linalg.vector_norm(b).item()
+    bnorm = vnorm(b)
     tol = max(atol, rtol * bnorm)
     V = torch.empty((restart + 1, N), dtype=dt, device=dev)
     Z = torch.empty((restart, N), dtype=dt, device=dev) if precond is not None else None
     total, matvecs = 0, 0
     r = b - matvec(x) if x0 is not None else b.clone()
     matvecs += x0 is not None
-    beta = torch.linalg.vector_norm(r).item()
+    beta = vnorm(r)
     while True:
         if beta <= tol:
             return GMRESResult(x, 0, total, beta, matvecs)
@@ -63,12 +74,12 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             w = matvec(zk)
             matvecs += 1
             Vk = V[:k + 1]
-            h = Vk @ w                       # CGS pass 1
+            h = proj(Vk, w)                  # CGS pass 1
             w = w - Vk.T @ h
-            h2 = Vk @ w                      # CGS pass 2 (re-orthogonalisation)
+            h2 = proj(Vk, w)                 # CGS pass 2 (re-orthogonalisation)
             w = w - Vk.T @ h2
             hcol = (h + h2).cpu().numpy()
-            hn = torch.linalg.vector_norm(w).item()
+            hn = vnorm(w)
             H[:k + 1, k] = hcol
             H[k + 1, k] = hn
             for i in range(k):               # apply previous Givens rotations
@@ -96,7 +107,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
         x = x + basis.T @ yt
         r = b - matvec(x)
         matvecs += 1
-        beta = torch.linalg.vector_norm(r).item()
+        beta = vnorm(r)
 
 
 def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None, precond=None, callback=None):

@@ -99,3 +99,25 @@ class NeighborExchange:
         if self.right is not None:
             y[-NY:] += self.recv_r
         return y
+
+
+class DistributedInner:
+    """Inner products of strip-partitioned vectors for sem_amd.krylov.gmres(inner=...).
+
+    A shared interface line is stored on both neighbouring ranks (with equal values after the
+    exchange); it is counted once, on the left-hand rank, and the per-rank partial products are
+    summed with one all-reduce (RCCL over xGMI under "nccl") per call: two per Arnoldi step for
+    CGS2, plus one per norm."""
+
+    def __init__(self, part, mesh, dist, group=None):
+        self.dist, self.group = dist, group
+        rank = part.bounds.index(mesh.ex_begin if hasattr(mesh, "ex_begin") else mesh.eb)
+        self.own = torch.ones(mesh.n_local, dtype=torch.float64, device=mesh.device)
+        if rank > 0:
+            self.own[:mesh.NY] = 0.0
+
+    def __call__(self, A, w):
+        h = A @ (w * self.own)
+        if self.dist is not None:
+            self.dist.all_reduce(h, group=self.group)
+        return h

@@ -1,0 +1,83 @@
+"""Strip-partitioned solve on the device: two ranks on one GPU (gloo for the collectives, the
+only backend that runs several ranks on one device), real band-kernel applies, real
+interface pack/unpack kernels, DistributedInner dot products -- against the single-domain
+device solve.  The RCCL path differs only in the backend string (bench.py --gpus N)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+P, NEX, NEY, PE = 6, 12, 7, 40.0
+
+
+def _inputs():
+    N = (NEX * P + 1) * (NEY * P + 1)
+    r = np.random.default_rng(11)
+    return r.uniform(-1, 1, N), r.uniform(-1, 1, N), r.uniform(-1, 1, N)
+
+
+def _solve(mesh, u, v, b, exch=None, inner=None):
+    from sem_amd import _lib
+    from sem_amd.krylov import gmres
+    U, V, B = (mesh.to_device(a) for a in (u, v, b))
+    kw = dict(c_stiff=1.0, c_gradx=PE, cu=U, c_grady=PE, cv=V, dir_mode=_lib.DIR_IDENTITY,
+              dir_sides=_lib.SIDE_W | _lib.SIDE_E)
+
+    def mv(x):
+        y = mesh.apply(x, **kw)
+        return exch(y) if exch is not None else y
+
+    return gmres(mv, B, atol=1e-11, restart=60, maxiter=20000, inner=inner)
+
+
+def _worker(rank, world, port, q, kind):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sem_amd.device import get_mesh
+        from sem_amd.parallel import DistributedInner, StripPartition
+        part = StripPartition(NEX, world)
+        eb, ee = part.local_range(rank)
+        mesh = get_mesh(P, NEX, NEY, 1.0 / NEX, 1.0 / NEY, eb, ee, 0)
+        u, v, b = _inputs()
+        sl = slice(mesh.dof_begin, mesh.dof_begin + mesh.n_local)
+        res = _solve(mesh, u[sl], v[sl], b[sl], exch=part.exchanger(mesh, dist, kind=kind),
+                     inner=DistributedInner(part, mesh, dist))
+        q.put((rank, res.info, res.iters, mesh.dof_begin, res.x.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_device_gmres(gpu, world):
+    from sem_amd.device import get_mesh
+    u, v, b = _inputs()
+    ref = _solve(get_mesh(P, NEX, NEY, 1.0 / NEX, 1.0 / NEY), u, v, b)
+    assert ref.info == 0
+    xr = ref.x.cpu().numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "allreduce")) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, info, iters, d0, x in out:
+        assert info == 0 and abs(iters - ref.iters) <= max(2, ref.iters // 50), (rank, iters, ref.iters)
+        assert np.abs(x - xr[d0:d0 + len(x)]).max() < 1e-8 * max(1.0, np.abs(xr).max())

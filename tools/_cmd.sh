@@ -1,8 +1,6 @@
 #!/bin/bash
 set -o pipefail
-O=gpurun_out/r01n
+O=gpurun_out/r01o
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -2 $O/tests.log
-timeout -k 10 300 python bench.py --cpu-seconds 2 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-cat $O/bench.json
+timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu tests/test_gpu_dist.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -5 $O/tests.log
