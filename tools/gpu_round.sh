@@ -13,7 +13,7 @@ run() {  # name limit cmd...
   tail -5 "gpurun_out/${TAG}_${name}.log"
   return $rc
 }
-run gputests 900 python -m pytest tests -m gpu -q -p no:cacheprovider -rf
+run gputests 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 120 --timeout-method thread
 rc=$?; [ $rc -gt 1 ] && exit $rc
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 600 python bench.py --steps "$STEPS" --warmup 200 || exit $?
