@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--ne", type=int, default=64, help="elements per direction per GPU")
     ap.add_argument("--P", type=int, default=8)
     ap.add_argument("--Pe", type=float, default=40.0)
-    ap.add_argument("--graph", type=int, default=1, help="capture steps in hipGraphs (N=1)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="capture steps in hipGraphs (N=1, and N>1 over RCCL: apply + pack + all-reduce + unpack)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--hbm-ne", type=int, default=1024, help="HBM-regime mesh size (0 = skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -78,7 +79,9 @@ def time_steps(step, steps, warmup, dev, use_graph, dist=None):
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
+            # thread-local capture mode: the process group's watchdog thread keeps querying its
+            # events while this thread captures; global mode would invalidate the capture
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if dist is not None else "global"):
                 for _ in range(batch):
                     step()
         torch.cuda.current_stream(dev).wait_stream(s)
@@ -204,7 +207,19 @@ def main():
         if exch is not None:
             exch(y)
 
-    secs, wall = time_steps(step, args.steps, args.warmup, dev, use_graph=(args.graph and world == 1), dist=dist)
+    # N > 1 over RCCL: the whole step (apply, pack, RCCL all-reduce or send/recv, unpack) is captured
+    # too -- RCCL collectives are stream-capturable -- so the per-step host cost (four launches and a
+    # collective call from Python) leaves the timed loop; gloo collectives are host-side and cannot be.
+    use_graph = bool(args.graph) and (world == 1 or args.dist_backend == "nccl")
+    try:
+        secs, wall = time_steps(step, args.steps, args.warmup, dev, use_graph=use_graph, dist=dist)
+    except RuntimeError as exc:  # capture refused: time the same steps eagerly
+        if not use_graph or world == 1:
+            raise
+        print(f"[bench] rank {rank}: hipGraph capture of the exchange failed ({exc}); timing eagerly",
+              file=sys.stderr, flush=True)
+        use_graph = False
+        secs, wall = time_steps(step, args.steps, 0, dev, use_graph=False, dist=dist)
     if dist is not None:
         t = torch.tensor([secs], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -240,8 +255,7 @@ def main():
                         "p2p": ", send/recv of interface lines with neighbours"}[args.exchange]
                        + (" (RCCL)" if args.dist_backend == "nccl" else " (gloo rehearsal)")
                        if world > 1 else ""),
-                   "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": bool(args.graph and
-                                                                                         world == 1)},
+                   "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": use_graph},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
                      "kernel": mesh.kernel_name(), "bytes_per_launch": bytes_launch,
