@@ -312,6 +312,7 @@ struct BandArgs {
   unsigned sides, flags;  // flags: 1 = cu given, 2 = cv given
   int nblk;               // grid size (gridDim would be a second, dependent kernarg fetch)
   int cpol;               // cache policy of the y stores / u,v loads (SEM_BAND_CPOL; see bstore_any)
+  int mchunk;             // apply_march: element positions marched by one workgroup
   // FULL kernels only
   const double* ea;
   const double* eb;
@@ -664,6 +665,279 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
 #undef BSTAMP
 }
 
+// ---- Marching form of the band kernel (HBM-sized meshes).
+// Same per-node arithmetic as apply_band<P, 1, TYE, NS> in the same order (results are bitwise
+// identical), but one workgroup owns a column band of TYE element rows and marches along x over a
+// chunk of `mchunk` element positions.  The staged (2P+1)-line window is a ring in LDS: a step
+// loads only the P lines the next element adds (the left element's lines stay), so x is read
+// once per band instead of (2P+1)/P times, and the next element's lines, u and v are loaded into
+// registers while the current element is contracted and stored -- the memory pipe stays busy
+// through the compute phases instead of every workgroup alternating load / compute / store.
+// Step m (element position m; ghost position ex_end holds only the closing line):
+//   A  ring holds lines [mP-P, mP+P]            -> X / Y contractions (ring reads) -> XK..YG
+//   B  new lines [(m+1)P+1, (m+1)P+P] -> ring slots of lines [mP-P, mP-1] (read only before B);
+//      epilogue of lines [mP, mP+P) (ring reads of those lines only) -> y
+template <int P, int TYE, int NS, bool FULL, bool DPP, bool GRAD>
+__global__ __launch_bounds__((BCfg<P, 1, TYE, NS>::THREADS)) void apply_march(const BandArgs a) {
+  using C = BCfg<P, 1, TYE, NS>;
+  using PL = EPlan<P, NS>;
+  using CL = CList<P, NS>;
+  constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW;
+  constexpr int R = C::RX;                                  // ring of 2P+1 lines
+  constexpr int NSTEP = (P * C::RY + C::THREADS - 1) / C::THREADS;  // new-line loads per thread per step
+  __shared__ double Ts[R * PT];
+  __shared__ double XK[BX * PY];
+  __shared__ double XG[BX * PY];
+  __shared__ double YK[BX * PY];
+  __shared__ double YG[BX * PY];
+  __shared__ double ws[n];
+
+  BPIN(a.x);
+  BPIN(a.y);
+  BPIN(a.cu);
+  BPIN(a.cv);
+  BPIN(a.fKx);
+  BPIN(a.fKy);
+  BPIN(a.fM);
+  BPIN(a.fX);
+  BPIN(a.fY);
+  BPIN(a.NY);
+  BPIN(a.lb0);
+  BPIN(a.lb1);
+  BPIN(a.ex_begin);
+  BPIN(a.ex_end);
+  BPIN(a.ney);
+  BPIN(a.nex);
+  BPIN(a.NXg);
+  BPIN(a.tiles_y);
+  BPIN(a.nbytes);
+  BPIN(a.dir_mode);
+  BPIN(a.sides);
+  BPIN(a.flags);
+  BPIN(a.nblk);
+  BPIN(a.cpol);
+  BPIN(a.mchunk);
+
+  // XCD-aware remap as in apply_band: an XCD gets a contiguous run of (chunk, band) pairs, band
+  // fastest, so bands marching side by side share their column halos in that XCD's L2
+  const int nb = a.nblk, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nb >> 3, rem = nb & 7;
+  const int Lq = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (bid >> 3);
+  const int cx = Lq / a.tiles_y, ty = Lq - cx * a.tiles_y;
+  const int mA = a.ex_begin + cx * a.mchunk, mB = min(mA + a.mchunk, a.ex_end + 1);
+  const int lb0 = a.lb0, NY = a.NY;
+  const int n0 = ty * TYE, n1 = min(n0 + TYE, a.ney + 1);
+  const int gy0 = n0 * P;
+  const int cols_ok = (min(n1, a.ney) - n0) * P + (n1 > a.ney ? 1 : 0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbytes = a.nbytes;
+  const bool has_u = a.flags & 1, has_v = a.flags & 2;
+  const auto rx = brsrc(a.x, nbytes), ru = brsrc(a.cu, has_u ? nbytes : 0), rv = brsrc(a.cv, has_v ? nbytes : 0);
+  const auto ry = brsrc(a.y, nbytes);
+
+  // column part of a staged index, and whether it is inside the domain (outside: staged as 0)
+  auto stage_col_ok = [&](int cc) { const int gy = gy0 - P + cc; return gy >= 0 && gy < NY; };
+
+  // ---- prologue: the full window of the first position, u / v (and operands) of its nodes
+  {
+    const int sbase = ((mA * P - P - lb0) * NY + gy0 - P) * 8;
+    double st[C::NSTAGE];
+#pragma unroll
+    for (int s = 0; s < C::NSTAGE; ++s) {
+      const int idx = min(tid + s * C::THREADS, C::RX * C::RY - 1);
+      const int rr = idx / C::RY, cc = idx - rr * C::RY;
+      st[s] = bload(rx, sbase + (rr * NY + cc) * 8);
+    }
+    if (tid < n) ws[tid] = gll_w<P>(tid);
+#pragma unroll
+    for (int s = 0; s < C::NSTAGE; ++s) {
+      const int idx = tid + s * C::THREADS;
+      if ((s + 1) * C::THREADS <= C::RX * C::RY || idx < C::RX * C::RY) {
+        const int rr = idx / C::RY, cc = idx - rr * C::RY;
+        Ts[rr * PT + cc] = stage_col_ok(cc) ? st[s] : 0.0;
+      }
+    }
+  }
+  double cv[DPP ? CL::NCV : 1];
+  if constexpr (DPP) {
+    const int wsplit = w < C::NXW ? (w / C::XW) % NS : (w - C::NXW) / C::YW;
+    const double* tb = kBandCoef<P, NS>.v + wsplit * CL::NPAD + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < CL::NCV; ++j) cv[j] = tb[16 * j];
+  } else {
+    cv[0] = 0.0;
+  }
+  // epilogue nodes of this thread (q = tid + e*THREADS -> line r, column c of the position)
+  int er[C::NE], ec_[C::NE];
+#pragma unroll
+  for (int e = 0; e < C::NE; ++e) {
+    const int q = tid + e * C::THREADS;
+    er[e] = q / LW;
+    ec_[e] = q - er[e] * LW;
+  }
+  auto node_off = [&](int m, int e) {  // local DOF of epilogue node e at position m (OOB if none)
+    const int rows_ok = m < a.ex_end ? P : 1;
+    const int q = tid + e * C::THREADS;
+    const bool ok = q < BX * LW && er[e] < rows_ok && ec_[e] < cols_ok;
+    return ok ? (m * P + er[e] - lb0) * NY + gy0 + ec_[e] : -(1 << 26);
+  };
+  double pu[C::NE], pv[C::NE];
+  NodeOps ops[C::NE] = {};
+  auto load_uv = [&](int m, double (&u_)[C::NE], double (&v_)[C::NE], NodeOps (&o_)[C::NE]) {
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e) {
+      const int off = node_off(m, e);
+      if (a.cpol & 256) {
+        u_[e] = bload_c<2>(ru, off * 8);
+        v_[e] = bload_c<2>(rv, off * 8);
+      } else {
+        u_[e] = bload(ru, off * 8);
+        v_[e] = bload(rv, off * 8);
+      }
+      if constexpr (FULL) o_[e] = load_node_ops(a, off);
+    }
+  };
+  load_uv(mA, pu, pv, ops);
+
+  constexpr double w0 = GllConst<P>::w[0], wP = GllConst<P>::w[P];
+  int sh = 0;  // ring slot of the window's first line (mP - P)
+#pragma unroll 1
+  for (int m = mA; m < mB; ++m) {
+    const bool more = m + 1 < mB;  // uniform
+    // ---- next position's new lines and node operands, in flight through this step
+    double nx[NSTEP];
+    double pun[C::NE], pvn[C::NE];
+    NodeOps opsn[C::NE] = {};
+    if (more) {
+      const int nbase = (((m + 1) * P + 1 - lb0) * NY + gy0 - P) * 8;
+#pragma unroll
+      for (int s = 0; s < NSTEP; ++s) {
+        const int idx = min(tid + s * C::THREADS, P * C::RY - 1);
+        const int rr = idx / C::RY, cc = idx - rr * C::RY;
+        nx[s] = bload(rx, nbase + (rr * NY + cc) * 8);
+      }
+      load_uv(m + 1, pun, pvn, opsn);
+    }
+    auto slot = [&](int rr) { const int s_ = sh + rr; return s_ >= R ? s_ - R : s_; };
+    __syncthreads();  // A
+
+    const int rows_ok = m < a.ex_end ? P : 1;
+    if (w < C::NXW) {
+      const int xg = w / C::XW;
+      const int xs = xg % NS;
+      const int xc = (w - xg * C::XW) * 64 + lane;
+      const bool xghost = m == a.ex_end, hasLx = m - 1 >= a.ex_begin;
+      const double fk = (hasLx ? 1.0 : 0.0) + (xghost ? 0.0 : 1.0);
+      const double fg = (xghost ? 0.0 : 1.0) - (hasLx ? 1.0 : 0.0);
+      for_rows(std::make_integer_sequence<int, NS>{}, [&](auto S) {
+        constexpr int s = decltype(S)::value;
+        if (xs != s) return;
+        double t[2 * P + 1];
+        constexpr int q0 = PL::needs_left(s) ? 0 : P;
+#pragma unroll
+        for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[slot(qq) * PT + P + xc];
+#pragma unroll
+        for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
+        double k[C::RP], g[C::RP];
+        eo_rows<P, NS, s, DPP>(t, fk, fg, k, g, cv);
+#pragma unroll
+        for (int sl = 0; sl < PL::nrows(s); ++sl) {
+          const int i = PL::row(s, sl);
+          if (xghost && i != 0) continue;
+          XK[i * PY + xc] = k[sl];
+          if constexpr (GRAD) XG[i * PY + xc] = g[sl];
+        }
+      });
+    } else {
+      const int wy = w - C::NXW;
+      const int h = wy / C::YW;
+      const int t2 = (wy - h * C::YW) * 64 + lane;
+      const bool yok = t2 < C::YL && t2 % BX < rows_ok && t2 / BX < n1 - n0;
+      const int r = DPP ? min(t2 % BX, BX - 1) : t2 % BX, b = DPP ? min(t2 / BX, C::YL / BX - 1) : t2 / BX;
+      if (DPP || yok) {
+        const bool hasLy = n0 + b - 1 >= 0, hasRy = n0 + b < a.ney;
+        const double fk = (hasLy ? 1.0 : 0.0) + (hasRy ? 1.0 : 0.0), fg = (hasRy ? 1.0 : 0.0) - (hasLy ? 1.0 : 0.0);
+        const int i = r;
+        const double mx = i != 0 ? ws[i] : (m - 1 >= a.ex_begin ? wP : 0.0) + (m < a.ex_end ? w0 : 0.0);
+        const double sk = a.fKy * mx, sg = a.fY * mx;
+        const int srow = slot(P + r) * PT + b * P;
+        for_rows(std::make_integer_sequence<int, NS>{}, [&](auto H) {
+          constexpr int hh = decltype(H)::value;
+          if (h != hh) return;
+          double t[2 * P + 1];
+          constexpr int q0 = PL::needs_left(hh) ? 0 : P;
+#pragma unroll
+          for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[srow + qq];
+#pragma unroll
+          for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
+          double k[C::RP], g[C::RP];
+          eo_rows<P, NS, hh, DPP>(t, fk, fg, k, g, cv);
+          if (yok) {
+#pragma unroll
+            for (int sl = 0; sl < PL::nrows(hh); ++sl) {
+              const int j = PL::row(hh, sl);
+              YK[r * PY + b * P + j] = sk * k[sl];
+              if constexpr (GRAD) YG[r * PY + b * P + j] = sg * g[sl];
+            }
+          }
+        });
+      }
+    }
+    __syncthreads();  // B
+
+    // ---- next position's new lines into the ring (slots of lines mP-P..mP-1, no longer read)
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < NSTEP; ++s) {
+        const int idx = tid + s * C::THREADS;
+        if ((s + 1) * C::THREADS <= P * C::RY || idx < P * C::RY) {
+          const int rr = idx / C::RY, cc = idx - rr * C::RY;
+          Ts[slot(rr) * PT + cc] = stage_col_ok(cc) ? nx[s] : 0.0;  // line mP+P+1+rr = slot (sh+rr) of step m
+        }
+      }
+    }
+
+    // ---- epilogue of position m
+    double zz[C::NE];
+    int eoff[C::NE];
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e) {
+      const int r = er[e], c = ec_[e];
+      eoff[e] = node_off(m, e);
+      zz[e] = 0.0;
+      if (eoff[e] >= 0) {
+        const int i = r;
+        const double mx = i != 0 ? ws[i] : (m - 1 >= a.ex_begin ? wP : 0.0) + (m < a.ex_end ? w0 : 0.0);
+        const int j = c % P, ne = n0 + c / P;
+        const double my = j != 0 ? ws[j] : (ne - 1 >= 0 ? wP : 0.0) + (ne < a.ney ? w0 : 0.0);
+        const int o = r * PY + c;
+        const double xv = Ts[slot(P + r) * PT + P + c];
+        const double u_ = has_u ? pu[e] : 1.0, v_ = has_v ? pv[e] : 1.0;
+        double z = fma(a.fKx * my, XK[o], YK[o]);
+        z = fma(a.fM * mx * my, xv, z);
+        if constexpr (GRAD) {
+          z = fma(a.fX * u_, my * XG[o], z);
+          z = fma(v_, YG[o], z);
+        }
+        zz[e] = finish_node<FULL>(a, ops[e], m * P + r, gy0 + c, xv, z);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e)
+      if (eoff[e] >= 0) bstore_any(a.cpol, ry, eoff[e] * 8, zz[e]);
+    if (more) {
+#pragma unroll
+      for (int e = 0; e < C::NE; ++e) {
+        pu[e] = pun[e];
+        pv[e] = pvn[e];
+        if constexpr (FULL) ops[e] = opsn[e];
+      }
+    }
+    sh = sh + P >= R ? sh + P - R : sh + P;
+  }
+}
+
 static int hip_check_b(hipError_t e, const char* what) {
   if (e == hipSuccess) return SEM_OK;
   return set_error(SEM_EHIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -737,6 +1011,77 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   return hip_check_b(hipGetLastError(), "apply (band) launch");
 }
 
+// Marching launch: one workgroup per (column band of TYE element rows, chunk of element positions).
+// The chunk length is chosen so that about SEM_MARCH_WG (default 1024: four per CU) workgroups cover
+// the mesh in one resident round.
+template <int P, int TYE, int NS, bool DPP>
+static int launch_march(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
+  using C = BCfg<P, 1, TYE, NS>;
+  const int ncols = h->ex_end - h->ex_begin;
+  const long long npos = ncols + 1;  // + the ghost position of the closing line
+  const long long tiles_y = (h->ney + 1 + TYE - 1) / TYE;
+  const char* e = std::getenv("SEM_MARCH_WG");
+  const long long target = std::max(64, e ? std::atoi(e) : 1024);
+  const long long chunks_want = std::max(1LL, std::min(npos, target / tiles_y));
+  const long long mchunk = (npos + chunks_want - 1) / chunks_want;
+  const long long nchunks = (npos + mchunk - 1) / mchunk;
+  const long long nblk = nchunks * tiles_y;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
+  BandArgs b{};
+  b.x = g.x;
+  b.y = g.y;
+  b.cu = g.cu;
+  b.cv = g.cv;
+  b.fKx = g.cK * g.sx;
+  b.fKy = g.cK * g.sy;
+  b.fM = g.cM * g.hxy;
+  b.fX = g.cX * g.hy;
+  b.fY = g.cY * g.hx;
+  b.NY = static_cast<int>(g.NY);
+  b.lb0 = static_cast<int>(g.line_begin);
+  b.lb1 = static_cast<int>(g.line_end);
+  b.ex_begin = g.ex_begin;
+  b.ex_end = g.ex_end;
+  b.ney = g.ney;
+  b.nex = g.nex;
+  b.NXg = static_cast<int>(g.NXg);
+  b.tiles_y = static_cast<int>(tiles_y);
+  b.nbytes = g.n_local32 * 8;
+  b.dir_mode = g.dir_mode;
+  b.diag = g.diag;
+  b.sides = g.sides;
+  b.flags = (g.cu ? 1u : 0u) | (g.cv ? 2u : 0u);
+  b.ea = g.ea;
+  b.eb = g.eb;
+  b.ec = g.ec;
+  b.ed = g.ed;
+  b.dval = g.dval;
+  b.mask = g.mask;
+  b.cE = g.cE;
+  b.cA = g.cA;
+  b.has_e1 = g.has_e1;
+  b.has_e2 = g.has_e2;
+  b.stamps = nullptr;
+  b.nblk = static_cast<int>(nblk);
+  b.mchunk = static_cast<int>(mchunk);
+  {
+    const char* ce = std::getenv("SEM_BAND_CPOL");
+    b.cpol = ce ? std::atoi(ce) : band_cpol(g.n_local32);
+  }
+  const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
+  const bool grad = g.cX != 0.0 || g.cY != 0.0;
+  const dim3 grid(static_cast<unsigned>(nblk)), block(C::THREADS);
+  if (full && grad)
+    hipLaunchKernelGGL((apply_march<P, TYE, NS, true, DPP, true>), grid, block, 0, s, b);
+  else if (full)
+    hipLaunchKernelGGL((apply_march<P, TYE, NS, true, DPP, false>), grid, block, 0, s, b);
+  else if (grad)
+    hipLaunchKernelGGL((apply_march<P, TYE, NS, false, DPP, true>), grid, block, 0, s, b);
+  else
+    hipLaunchKernelGGL((apply_march<P, TYE, NS, false, DPP, false>), grid, block, 0, s, b);
+  return hip_check_b(hipGetLastError(), "apply (march) launch");
+}
+
 // Tile shape per order: ~64 columns (TYE = 64/P element positions) so a wave spans one tile line;
 // TXE element columns for ~512-node tiles; rows of an element split over NS threads.
 template <int P>
@@ -757,6 +1102,12 @@ static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStrea
     if (force == 5) return launch_band<P, 2, S::TYE, 2, true>(args, h, s);
     if (force == 6) return launch_band<P, 1, S::TYE, 1, true>(args, h, s);
   }
+  if constexpr (P == 8 || P == 12) {
+    if (force == 7) return launch_march<P, S::TYE, S::NS, false>(args, h, s);
+    if (force == 8) return launch_march<P, S::TYE, S::NS, true>(args, h, s);
+  }
+  if constexpr (P == 8 || P == 12) {
+  }
   if (force == 3) return launch_band<P, S::TXE, S::TYE, S::NS, true>(args, h, s);
   if (force == 4) return launch_band<P, S::TXE, S::TYE, S::NS, false>(args, h, s);
   // DPP-broadcast coefficients: 2-4 % faster from ~1M DOFs up (the VALU-bound regime), 2-3 % slower on
@@ -771,7 +1122,10 @@ std::string band_kernel_name(int P, long long n_local) {
   const int NS = P >= 2 ? 2 : 1;
   const char* e = std::getenv("SEM_BAND_TILE");
   const int force = e ? std::atoi(e) : 0;
-  const bool dpp = force == 3 || (force == 0 && n_local >= (1 << 20));
+  const bool dpp = force == 3 || force == 8 || (force == 0 && n_local >= (1 << 20));
+  if (force == 7 || force == 8)
+    return "sem::apply_march<" + std::to_string(P) + ", " + std::to_string(TYE) + ", " + std::to_string(NS) +
+           (dpp ? ", dpp" : "") + ">";
   return "sem::apply_band<" + std::to_string(P) + ", " + std::to_string(TXE) + ", " + std::to_string(TYE) + ", " +
          std::to_string(NS) + (dpp ? ", dpp" : "") + ">";
 }
