@@ -54,6 +54,13 @@ def gen_consts(verbose=False):
     return CONSTS
 
 
+# Per-source flags.  apply_band.hip: the command processor preloads the first 14 kernel-argument
+# SGPRs (the scalar prologue arguments of apply_band_kp), so a tile's first global load does not
+# wait on a kernarg memory fetch.  The code object keeps a fallback prologue that loads them itself
+# when the firmware does not preload.
+EXTRA_FLAGS = {"apply_band.hip": ["-mllvm", "-amdgpu-kernarg-preload-count=14"]}
+
+
 def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
@@ -69,7 +76,7 @@ def build(force=False, verbose=False):
         if (not force and os.path.exists(obj)
                 and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, src)))):
             continue
-        cmd = [hipcc] + flags + ["-c", "-o", obj, os.path.join(CSRC, src)]
+        cmd = [hipcc] + flags + EXTRA_FLAGS.get(src, []) + ["-c", "-o", obj, os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((src, subprocess.Popen(cmd)))

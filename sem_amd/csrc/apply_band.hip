@@ -407,8 +407,15 @@ __device__ __forceinline__ double gll_w(int J) {
 // GRAD = false: no gradient / convection terms (mass + stiffness only: the Laplacian K x, the
 // Helmholtz operators of Solvers/README.md, the NS pressure rows K[mask,:] p); the G rows are
 // then dead code and are not computed.
-template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD = true>
-__global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(const BandArgs a) {
+// Kernel body.  The fields the prologue needs before its first global load (x, cu, cv pointers and
+// the tile-mapping integers) arrive as separate values: from the struct (apply_band) or as leading
+// scalar kernel arguments that the command processor preloads into SGPRs (apply_band_kp, KP =
+// true), so the first staging load does not wait for a kernarg memory fetch.
+template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD, bool KP>
+__device__ __forceinline__ void band_body(const double* __restrict__ px, const double* __restrict__ pcu,
+                                          const double* __restrict__ pcv, int pNY, int plb0, int pex_begin,
+                                          int pex_end, int pney, int pnblk, int ptiles_y, int pnbytes,
+                                          const BandArgs& a) {
   using C = BCfg<P, TXE, TYE, NS>;
   using PL = EPlan<P, NS>;
   using CL = CList<P, NS>;
@@ -420,56 +427,29 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
   __shared__ double YG[BX * PY];
   __shared__ double ws[n];
 
-  BPIN(a.x);
-  BPIN(a.y);
-  BPIN(a.cu);
-  BPIN(a.cv);
-  BPIN(a.fKx);
-  BPIN(a.fKy);
-  BPIN(a.fM);
-  BPIN(a.fX);
-  BPIN(a.fY);
-  BPIN(a.NY);
-  BPIN(a.lb0);
-  BPIN(a.lb1);
-  BPIN(a.ex_begin);
-  BPIN(a.ex_end);
-  BPIN(a.ney);
-  BPIN(a.nex);
-  BPIN(a.NXg);
-  BPIN(a.tiles_y);
-  BPIN(a.nbytes);
-  BPIN(a.dir_mode);
-  BPIN(a.diag);
-  BPIN(a.sides);
-  BPIN(a.flags);
-  BPIN(a.stamps);
-  BPIN(a.nblk);
-  BPIN(a.cpol);
-
   // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
   // tiles (y fastest) and neighbouring tiles share their halo lines through that XCD's L2.
-  const int nb = a.nblk, bid = blockIdx.x;
+  const int nb = pnblk, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nb >> 3, rem = nb & 7;
   const int L = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (bid >> 3);
-  const int tx = L / a.tiles_y, ty = L - tx * a.tiles_y;
+  const int tx = L / ptiles_y, ty = L - tx * ptiles_y;
 
-  const int lb0 = a.lb0, NY = a.NY;
+  const int lb0 = plb0, NY = pNY;
   // element positions [m0, m1) x [n0, n1); position ex_end (ney) is the ghost holding the closing line (column)
-  const int m0 = a.ex_begin + tx * TXE, m1 = min(m0 + TXE, a.ex_end + 1);
-  const int n0 = ty * TYE, n1 = min(n0 + TYE, a.ney + 1);
+  const int m0 = pex_begin + tx * TXE, m1 = min(m0 + TXE, pex_end + 1);
+  const int n0 = ty * TYE, n1 = min(n0 + TYE, pney + 1);
   const int gx0 = m0 * P, gy0 = n0 * P;
-  const int rows_ok = (min(m1, a.ex_end) - m0) * P + (m1 > a.ex_end ? 1 : 0);  // valid lines of the tile
-  const int cols_ok = (min(n1, a.ney) - n0) * P + (n1 > a.ney ? 1 : 0);       // valid columns
+  const int rows_ok = (min(m1, pex_end) - m0) * P + (m1 > pex_end ? 1 : 0);  // valid lines of the tile
+  const int cols_ok = (min(n1, pney) - n0) * P + (n1 > pney ? 1 : 0);       // valid columns
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // Diagnostics (SEM_DIAG bit 8): s_memtime phase stamps held in SGPRs, written at the very end
   // so that no diagnostic store sits in the vmcnt queue of the measured phases.
   unsigned long long stv[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0, rt1 = 0;
-  if (a.stamps) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
+  if (!KP && a.stamps) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
 #define BSTAMP(k)                                                                      \
   do {                                                                                 \
-    if (a.stamps) {                                                                    \
+    if ((!KP || (k) >= 2) && a.stamps) {  /* KP: no stamps before the loads issue */   \
       __builtin_amdgcn_sched_barrier(0);                                               \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stv[k])::"memory"); \
       __builtin_amdgcn_sched_barrier(0);                                               \
@@ -477,9 +457,9 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
   } while (0)
   BSTAMP(0);
 
-  const int nbytes = a.nbytes;
-  const bool has_u = a.flags & 1, has_v = a.flags & 2;
-  const auto rx = brsrc(a.x, nbytes), ru = brsrc(a.cu, has_u ? nbytes : 0), rv = brsrc(a.cv, has_v ? nbytes : 0);
+  const int nbytes = pnbytes;
+  const bool has_u = pcu != nullptr, has_v = pcv != nullptr;
+  const auto rx = brsrc(px, nbytes), ru = brsrc(pcu, has_u ? nbytes : 0), rv = brsrc(pcv, has_v ? nbytes : 0);
   const auto ry = brsrc(a.y, nbytes);
   const int nodeb = (gx0 - lb0) * NY + gy0;  // local DOF index of the tile's first node
 
@@ -487,7 +467,7 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
   // the staged x window, then u, v of this thread's epilogue nodes.  Buffer bounds make lines
   // outside the local range read 0; columns past the domain's y-ends wrap into neighbouring
   // lines.  Neither is ever consumed.
-  const int sbase = (a.diag & 64) ? -(1 << 30) : ((gx0 - P - lb0) * NY + gy0 - P) * 8;  // diag 64: no staging loads
+  const int sbase = (!KP && (a.diag & 64)) ? -(1 << 30) : ((gx0 - P - lb0) * NY + gy0 - P) * 8;  // diag 64: no staging loads
   double st[C::NSTAGE];
 #pragma unroll
   for (int s = 0; s < C::NSTAGE; ++s) {
@@ -527,6 +507,21 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
 #pragma unroll
     for (int e = 0; e < C::NE; ++e) ops[e] = load_node_ops(a, eoff[e]);
   }
+  if constexpr (KP) {  // the struct's fields: fetched now, while the staging loads are in flight
+    BPIN(a.y);
+    BPIN(a.fKx);
+    BPIN(a.fKy);
+    BPIN(a.fM);
+    BPIN(a.fX);
+    BPIN(a.fY);
+    BPIN(a.NXg);
+    BPIN(a.dir_mode);
+    BPIN(a.sides);
+    BPIN(a.cpol);
+    BPIN(a.lb1);
+    BPIN(a.nex);
+    BPIN(a.diag);
+  }
 
   // ---- LDS: weights, staged window (columns outside the domain staged as 0: absent elements)
   if (tid < n) ws[tid] = gll_w<P>(tid);
@@ -552,7 +547,7 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
     const int xa = xg / NS, xs = xg - xa * NS;
     const int xc = (w - xg * C::XW) * 64 + lane;
     if (xa < m1 - m0) {
-      const bool xghost = m0 + xa == a.ex_end, hasLx = m0 + xa - 1 >= a.ex_begin;  // wave-uniform
+      const bool xghost = m0 + xa == pex_end, hasLx = m0 + xa - 1 >= pex_begin;  // wave-uniform
       const double fk = (hasLx ? 1.0 : 0.0) + (xghost ? 0.0 : 1.0);
       const double fg = (xghost ? 0.0 : 1.0) - (hasLx ? 1.0 : 0.0);
       for_rows(std::make_integer_sequence<int, NS>{}, [&](auto S) {
@@ -586,10 +581,10 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
     // clamped, in-bounds positions; only the LDS stores are predicated
     const int r = DPP ? min(t2 % BX, BX - 1) : t2 % BX, b = DPP ? min(t2 / BX, C::YL / BX - 1) : t2 / BX;
     if (DPP || yok) {
-      const bool hasLy = n0 + b - 1 >= 0, hasRy = n0 + b < a.ney;
+      const bool hasLy = n0 + b - 1 >= 0, hasRy = n0 + b < pney;
       const double fk = (hasLy ? 1.0 : 0.0) + (hasRy ? 1.0 : 0.0), fg = (hasRy ? 1.0 : 0.0) - (hasLy ? 1.0 : 0.0);
       const int i = r % P, ex = m0 + r / P;
-      const double mx = i != 0 ? ws[i] : (ex - 1 >= a.ex_begin ? wP : 0.0) + (ex < a.ex_end ? w0 : 0.0);
+      const double mx = i != 0 ? ws[i] : (ex - 1 >= pex_begin ? wP : 0.0) + (ex < pex_end ? w0 : 0.0);
       const double sk = a.fKy * mx, sg = a.fY * mx;
       for_rows(std::make_integer_sequence<int, NS>{}, [&](auto H) {
         constexpr int hh = decltype(H)::value;
@@ -627,9 +622,9 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
     zz[e] = 0.0;
     if (q < BX * LW && r < rows_ok && c < cols_ok) {
       const int i = r % P, me = m0 + r / P;
-      const double mx = i != 0 ? ws[i] : (me - 1 >= a.ex_begin ? wP : 0.0) + (me < a.ex_end ? w0 : 0.0);
+      const double mx = i != 0 ? ws[i] : (me - 1 >= pex_begin ? wP : 0.0) + (me < pex_end ? w0 : 0.0);
       const int j = c % P, ne = n0 + c / P;
-      const double my = j != 0 ? ws[j] : (ne - 1 >= 0 ? wP : 0.0) + (ne < a.ney ? w0 : 0.0);
+      const double my = j != 0 ? ws[j] : (ne - 1 >= 0 ? wP : 0.0) + (ne < pney ? w0 : 0.0);
       const int o = r * PY + c;
       const double xv = Ts[(P + r) * PT + P + c];
       const double u_ = has_u ? pu[e] : 1.0, v_ = has_v ? pv[e] : 1.0;
@@ -663,6 +658,49 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
     }
   }
 #undef BSTAMP
+}
+
+template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD = true>
+__global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(const BandArgs a) {
+  BPIN(a.x);
+  BPIN(a.y);
+  BPIN(a.cu);
+  BPIN(a.cv);
+  BPIN(a.fKx);
+  BPIN(a.fKy);
+  BPIN(a.fM);
+  BPIN(a.fX);
+  BPIN(a.fY);
+  BPIN(a.NY);
+  BPIN(a.lb0);
+  BPIN(a.lb1);
+  BPIN(a.ex_begin);
+  BPIN(a.ex_end);
+  BPIN(a.ney);
+  BPIN(a.nex);
+  BPIN(a.NXg);
+  BPIN(a.tiles_y);
+  BPIN(a.nbytes);
+  BPIN(a.dir_mode);
+  BPIN(a.diag);
+  BPIN(a.sides);
+  BPIN(a.flags);
+  BPIN(a.stamps);
+  BPIN(a.nblk);
+  BPIN(a.cpol);
+  band_body<P, TXE, TYE, NS, FULL, DPP, GRAD, false>(a.x, (a.flags & 1) ? a.cu : nullptr, (a.flags & 2) ? a.cv : nullptr,
+                                                     a.NY, a.lb0, a.ex_begin, a.ex_end, a.ney, a.nblk, a.tiles_y,
+                                                     a.nbytes, a);
+}
+
+// Same kernel with the prologue's fields as leading scalar arguments (14 SGPRs, preloaded by the
+// command processor when the code object asks for it: -amdgpu-kernarg-preload-count in build.py).
+template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD = true>
+__global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band_kp(
+    const double* px, const double* pcu, const double* pcv, int pNY, int plb0, int pex_begin, int pex_end, int pney,
+    int pnblk, int ptiles_y, int pnbytes, const BandArgs a) {
+  band_body<P, TXE, TYE, NS, FULL, DPP, GRAD, true>(px, pcu, pcv, pNY, plb0, pex_begin, pex_end, pney, pnblk, ptiles_y,
+                                                    pnbytes, a);
 }
 
 // ---- Marching form of the band kernel (HBM-sized meshes).
@@ -1000,6 +1038,20 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   const bool grad = g.cX != 0.0 || g.cY != 0.0;
   const dim3 grid(static_cast<unsigned>(nblk)), block(C::THREADS);
+  const char* kpe = std::getenv("SEM_BAND_KP");  // SEM_BAND_KP=0: struct-only arguments (A/B), read per call
+  if (!(kpe && std::atoi(kpe) == 0)) {
+#define SEM_KP_ARGS b.x, b.cu, b.cv, b.NY, b.lb0, b.ex_begin, b.ex_end, b.ney, b.nblk, b.tiles_y, b.nbytes, b
+    if (full && grad)
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, DPP, true>), grid, block, 0, s, SEM_KP_ARGS);
+    else if (full)
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, DPP, false>), grid, block, 0, s, SEM_KP_ARGS);
+    else if (grad)
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, false, DPP, true>), grid, block, 0, s, SEM_KP_ARGS);
+    else
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, false, DPP, false>), grid, block, 0, s, SEM_KP_ARGS);
+#undef SEM_KP_ARGS
+    return hip_check_b(hipGetLastError(), "apply (band) launch");
+  }
   if (full && grad)
     hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, DPP, true>), grid, block, 0, s, b);
   else if (full)

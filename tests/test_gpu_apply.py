@@ -182,6 +182,37 @@ def test_band_variants_bitwise_equal(gpu, P, nex, ney, monkeypatch):
         assert torch.equal(mesh.apply(X, **kw), base), name
 
 
+@pytest.mark.parametrize("P,nex,ney,eb,ee", [(8, 64, 64, 0, 64), (8, 40, 13, 10, 30), (4, 9, 7, 2, 9), (12, 5, 3, 0, 5)])
+@pytest.mark.parametrize("full", [False, True])
+def test_band_kernarg_forms_bitwise_equal(gpu, P, nex, ney, eb, ee, full, monkeypatch):
+    """apply_band_kp (prologue fields as preloaded scalar kernel arguments) and apply_band (all
+    fields in the struct) run the same body: bitwise-identical results, FULL path included."""
+    from sem_amd import _lib
+    from sem_amd.device import get_mesh
+    mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.5 / ney, eb, ee)
+    r = np.random.default_rng(7 * nex + eb)
+    N = mesh.n_local
+    X, U, V, A, B, Y0, G = (mesh.to_device(r.uniform(-1, 1, N)) for _ in range(7))
+    kw = dict(c_mass=0.25, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, algo=4)
+    if full:
+        mask = mesh.to_device((r.uniform(0, 1, N) < 0.1).astype(np.uint8), dtype=torch.uint8)
+        kw.update(c_extra=3.0, ea=A, eb=B, c_acc=2.0, dir_mode=_lib.DIR_IDENTITY, dir_mask=mask, dir_val=G)
+    else:
+        kw.update(dir_mode=_lib.DIR_IDENTITY, dir_sides=_lib.SIDE_W | _lib.SIDE_E)
+    monkeypatch.delenv("SEM_BAND_TILE", raising=False)
+    outs = {}
+    for kp in ("0", "1"):
+        monkeypatch.setenv("SEM_BAND_KP", kp)
+        outs[kp] = mesh.apply(X, Y0.clone(), **kw)
+    assert torch.equal(outs["0"], outs["1"])
+    # no convection coefficients (cu = cv = None): the preloaded null pointers select the u, v = 1 path
+    kw0 = dict(c_stiff=1.0, c_gradx=2.0, c_grady=3.0, algo=4)
+    monkeypatch.setenv("SEM_BAND_KP", "0")
+    a0 = mesh.apply(X, **kw0)
+    monkeypatch.setenv("SEM_BAND_KP", "1")
+    assert torch.equal(mesh.apply(X, **kw0), a0)
+
+
 @pytest.mark.parametrize("P,nex,ney,eb,ee,wg", [(8, 40, 13, 0, 40, 64), (8, 40, 13, 10, 30, 64), (8, 40, 13, 0, 17, 8),
                                                (12, 9, 21, 3, 9, 32), (8, 33, 64, 0, 33, 1024), (8, 5, 3, 2, 3, 64)])
 @pytest.mark.parametrize("full", [False, True])
