@@ -1178,8 +1178,10 @@ std::string band_kernel_name(int P, long long n_local) {
   if (force == 7 || force == 8)
     return "sem::apply_march<" + std::to_string(P) + ", " + std::to_string(TYE) + ", " + std::to_string(NS) +
            (dpp ? ", dpp" : "") + ">";
-  return "sem::apply_band<" + std::to_string(P) + ", " + std::to_string(TXE) + ", " + std::to_string(TYE) + ", " +
-         std::to_string(NS) + (dpp ? ", dpp" : "") + ">";
+  const char* kpe = std::getenv("SEM_BAND_KP");
+  const bool kp = !(kpe && std::atoi(kpe) == 0);
+  return std::string(kp ? "sem::apply_band_kp<" : "sem::apply_band<") + std::to_string(P) + ", " + std::to_string(TXE) +
+         ", " + std::to_string(TYE) + ", " + std::to_string(NS) + (dpp ? ", dpp" : "") + ">";
 }
 
 int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s) {
