@@ -81,7 +81,8 @@ def time_steps(step, steps, warmup, dev, use_graph, dist=None):
         with torch.cuda.stream(s):
             # thread-local capture mode: the process group's watchdog thread keeps querying its
             # events while this thread captures; global mode would invalidate the capture
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if dist is not None else "global"):
+            pg = torch.distributed.is_available() and torch.distributed.is_initialized()
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if pg else "global"):
                 for _ in range(batch):
                     step()
         torch.cuda.current_stream(dev).wait_stream(s)
