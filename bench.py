@@ -273,6 +273,17 @@ def main():
                                  "kernel": mesh.kernel_name(), "bytes_per_launch": 16.0 * n_loc,
                                  "achieved": 16.0 * n_loc / kl / 1e9, "unit_bw": "GB/s",
                                  "frac": 16.0 * n_loc / kl / 1e9 / HBM_PEAK_GBS}
+        # north_star's MFMA form of the same apply (element-block contractions on
+        # v_mfma_f64_16x16x4_f64, SEM_ALGO_MFMA): its fraction of the fp64 MFMA peak, beside the
+        # default VALU band kernel that beats it
+        kwm = dict(kw, algo=_lib.ALGO_MFMA)
+        sm, _ = time_steps(lambda: mesh.apply(T, y, **kwm), 1000, 100, dev, use_graph=True)
+        km = sm / 1000
+        out["mfma_variant"] = {"kernel": mesh.kernel_name(_lib.ALGO_MFMA), "kernel_us": km * 1e6,
+                               "value": N_glob / km, "unit": "DOF-updates/s",
+                               "fp64_tflops": flops_launch / km / 1e12, "mfma_peak_tflops": FP64_PEAK_TFLOPS,
+                               "frac_mfma_peak": flops_launch / km / 1e12 / FP64_PEAK_TFLOPS,
+                               "flops_per_launch": flops_launch, "speedup_band_over_mfma": km / kern_s}
 
     if rank == 0 and world == 1 and args.hbm_ne > 0:
         # HBM regime: 1024^2 elements, P=8 (N = 67.1 M, 2.15 GB moved per apply > 256 MB MALL)
