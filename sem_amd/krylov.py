@@ -63,8 +63,11 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             return GMRESResult(x, total, total, beta, matvecs)
         V[0] = r / beta
         H = np.zeros((restart + 1, restart))
-        cs, sn = np.zeros(restart), np.zeros(restart)
-        g = np.zeros(restart + 1)
+        # Givens rotations and the rotated right-hand side as Python floats: the O(k) rotation
+        # sweep per iteration runs in the interpreter, where float arithmetic is several times
+        # cheaper than on NumPy scalars (it dominated the host time of long unrestarted solves)
+        cs, sn = [0.0] * restart, [0.0] * restart
+        g = [0.0] * (restart + 1)
         g[0] = beta
         k_done = 0
         for k in range(restart):
@@ -78,18 +81,19 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             w = w - Vk.T @ h
             h2 = proj(Vk, w)                 # CGS pass 2 (re-orthogonalisation)
             w = w - Vk.T @ h2
-            hcol = (h + h2).cpu().numpy()
+            col = (h + h2).cpu().tolist()
             hn = vnorm(w)
-            H[:k + 1, k] = hcol
-            H[k + 1, k] = hn
+            col.append(hn)
             for i in range(k):               # apply previous Givens rotations
-                t = cs[i] * H[i, k] + sn[i] * H[i + 1, k]
-                H[i + 1, k] = -sn[i] * H[i, k] + cs[i] * H[i + 1, k]
-                H[i, k] = t
-            den = math.hypot(H[k, k], H[k + 1, k])
-            cs[k], sn[k] = (1.0, 0.0) if den == 0.0 else (H[k, k] / den, H[k + 1, k] / den)
-            H[k, k] = cs[k] * H[k, k] + sn[k] * H[k + 1, k]
-            H[k + 1, k] = 0.0
+                c, s_ = cs[i], sn[i]
+                a, b_ = col[i], col[i + 1]
+                col[i] = c * a + s_ * b_
+                col[i + 1] = -s_ * a + c * b_
+            den = math.hypot(col[k], col[k + 1])
+            cs[k], sn[k] = (1.0, 0.0) if den == 0.0 else (col[k] / den, col[k + 1] / den)
+            col[k] = cs[k] * col[k] + sn[k] * col[k + 1]
+            col[k + 1] = 0.0
+            H[:k + 2, k] = col
             g[k + 1] = -sn[k] * g[k]
             g[k] = cs[k] * g[k]
             total += 1
@@ -101,7 +105,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
                 break
             V[k + 1] = w / hn
         # x += Z y  with  H[:k,:k] y = g[:k]
-        y = np.linalg.solve(np.triu(H[:k_done, :k_done]), g[:k_done]) if k_done else np.zeros(0)
+        y = np.linalg.solve(np.triu(H[:k_done, :k_done]), np.asarray(g[:k_done])) if k_done else np.zeros(0)
         yt = torch.as_tensor(y, dtype=dt, device=dev)
         basis = Z[:k_done] if Z is not None else V[:k_done]
         x = x + basis.T @ yt
