@@ -20,6 +20,35 @@ import numpy as np
 import torch
 
 
+class _DeviceSweeps:
+    """The two basis passes of an Arnoldi step as HIP kernels (include/sem_ops.h: sem_basis_dot2,
+    sem_basis_update): one HBM pass over the basis each, instead of torch's GEMV / skinny-GEMM
+    routes.  Used for device tensors without a distributed inner product."""
+
+    def __init__(self, V):
+        from . import _lib
+        self.lib = _lib.load()
+        self.check = _lib.check
+        self.V, self.ldv = V, V.stride(0)
+        rows = V.shape[0]
+        self.out = torch.empty((rows, 2), dtype=V.dtype, device=V.device)
+        self.work = torch.empty(max(1, self.lib.sem_basis_dot2_work_size(rows)), dtype=V.dtype, device=V.device)
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.V.device).cuda_stream
+
+    def dot2(self, k, a, b):
+        """[V_j . a, V_j . b] for the first k rows -> (k, 2) view."""
+        self.check(self.lib.sem_basis_dot2(self.V.data_ptr(), self.ldv, k, self.V.shape[1], a.data_ptr(),
+                                           b.data_ptr(), self.work.data_ptr(), self.out.data_ptr(), self._stream()))
+        return self.out[:k]
+
+    def update(self, k, c, w):
+        """w -= V[:k]^T c, in place."""
+        self.check(self.lib.sem_basis_update(self.V.data_ptr(), self.ldv, k, self.V.shape[1], c.data_ptr(),
+                                             w.data_ptr(), self._stream()))
+
+
 class GMRESResult:
     def __init__(self, x, info, iters, res_norm, matvecs):
         self.x, self.info, self.iters, self.res_norm, self.matvecs = x, info, iters, res_norm, matvecs
@@ -52,6 +81,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     tol = max(atol, rtol * bnorm)
     V = torch.empty((restart + 1, N), dtype=dt, device=dev)
     G = torch.zeros((restart + 1, restart + 1), dtype=dt, device=dev)  # Gram matrix V^T V of the basis
+    sweeps = _DeviceSweeps(V) if (inner is None and V.is_cuda) else None
     Z = torch.empty((restart, N), dtype=dt, device=dev) if precond is not None else None
     total, matvecs = 0, 0
     r = b - matvec(x) if x0 is not None else b.clone()
@@ -82,12 +112,20 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             # V^T (w - V h) = (I - G) h come from the basis' Gram matrix G = V^T V, whose new row
             # V^T v_k costs one GEMV per iteration.  (One GEMM over [w, v_k] would make it two
             # sweeps, but torch routes that skinny product to a GEMM 14x slower than two GEMVs.)
-            h = proj(Vk, w)                  # CGS pass 1
-            gk = proj(Vk, V[k])              # Gram row of the newest basis vector
+            if sweeps is not None:           # one HIP pass: CGS pass 1 and the Gram row together
+                S = sweeps.dot2(k + 1, w.contiguous(), V[k])
+                h, gk = S[:, 0].clone(), S[:, 1].clone()
+            else:
+                h = proj(Vk, w)              # CGS pass 1
+                gk = proj(Vk, V[k])          # Gram row of the newest basis vector
             G[k, :k + 1] = gk
             G[:k + 1, k] = gk
             hh = 2.0 * h - G[:k + 1, :k + 1] @ h   # h + (I - G) h: both passes' coefficients
-            w = w - Vk.T @ hh
+            if sweeps is not None:
+                w = w.clone()
+                sweeps.update(k + 1, hh.contiguous(), w)
+            else:
+                w = w - Vk.T @ hh
             col = hh.cpu().tolist()
             hn = vnorm(w)
             col.append(hn)
