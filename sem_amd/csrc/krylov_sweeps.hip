@@ -29,12 +29,26 @@ __global__ __launch_bounds__(kDotThreads) void basis_dot2_kernel(const double* _
   const int64_t len = (n + kDotChunks - 1) / kDotChunks;
   const int64_t lo = c * len, hi = min(n, lo + len);
   const double* row = V + j * ldv;
-  double sa = 0.0, sb = 0.0;
-  for (int64_t i = lo + t; i < hi; i += kDotThreads) {
-    const double v = row[i];
-    sa = fma(v, a[i], sa);
-    sb = fma(v, b[i], sb);
+  // four independent accumulator pairs: four rows-loads in flight per thread
+  double sa0 = 0.0, sb0 = 0.0, sa1 = 0.0, sb1 = 0.0, sa2 = 0.0, sb2 = 0.0, sa3 = 0.0, sb3 = 0.0;
+  int64_t i = lo + t;
+  for (; i + 3 * kDotThreads < hi; i += 4 * kDotThreads) {
+    const double v0 = row[i], v1 = row[i + kDotThreads], v2 = row[i + 2 * kDotThreads], v3 = row[i + 3 * kDotThreads];
+    sa0 = fma(v0, a[i], sa0);
+    sb0 = fma(v0, b[i], sb0);
+    sa1 = fma(v1, a[i + kDotThreads], sa1);
+    sb1 = fma(v1, b[i + kDotThreads], sb1);
+    sa2 = fma(v2, a[i + 2 * kDotThreads], sa2);
+    sb2 = fma(v2, b[i + 2 * kDotThreads], sb2);
+    sa3 = fma(v3, a[i + 3 * kDotThreads], sa3);
+    sb3 = fma(v3, b[i + 3 * kDotThreads], sb3);
   }
+  for (; i < hi; i += kDotThreads) {
+    const double v = row[i];
+    sa0 = fma(v, a[i], sa0);
+    sb0 = fma(v, b[i], sb0);
+  }
+  double sa = (sa0 + sa1) + (sa2 + sa3), sb = (sb0 + sb1) + (sb2 + sb3);
   // wave reduction (fixed order), then the four waves in order
   for (int off = 32; off > 0; off >>= 1) {
     sa += __shfl_down(sa, off, 64);
