@@ -65,40 +65,55 @@ def make_inputs(mesh, seed=2024):
     return [mesh.to_device(r.uniform(-1, 1, N)) for _ in range(3)]
 
 
+GRAPH_BATCH = 100   # steps per captured hipGraph
+
+
+def capture(step, count, dev):
+    """One hipGraph holding `count` back-to-back steps (captured on a side stream)."""
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        # thread-local capture mode: the process group's watchdog thread keeps querying its
+        # events while this thread captures; global mode would invalidate the capture
+        pg = torch.distributed.is_available() and torch.distributed.is_initialized()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if pg else "global"):
+            for _ in range(count):
+                step()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    return g
+
+
 def time_steps(step, steps, warmup, dev, use_graph, dist=None):
-    """Time exactly `steps` steps between barrier + synchronize on both sides."""
+    """Time exactly `steps` steps between barrier + synchronize on both sides.
+
+    With graphs, all steps are captured up front: one graph of min(steps, 100) steps replayed
+    steps // 100 times, plus one graph for the remainder, so a short run (the driver's
+    --steps 20) is ONE graph replay of 20 back-to-back applies, not 20 single-launch replays.
+    Every graph is replayed once untimed before the timed region."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
-    replay = None
-    if use_graph:
-        batch = 100
-        while steps % batch:
-            batch //= 2
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            # thread-local capture mode: the process group's watchdog thread keeps querying its
-            # events while this thread captures; global mode would invalidate the capture
-            pg = torch.distributed.is_available() and torch.distributed.is_initialized()
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local" if pg else "global"):
-                for _ in range(batch):
-                    step()
-        torch.cuda.current_stream(dev).wait_stream(s)
-        g.replay()
+    plan = []
+    if use_graph and steps > 0:
+        batch = min(steps, GRAPH_BATCH)
+        reps, rem = divmod(steps, batch)
+        plan.append((capture(step, batch, dev), reps))
+        if rem:
+            plan.append((capture(step, rem, dev), 1))
+        for g, _ in plan:
+            g.replay()
         torch.cuda.synchronize(dev)
-        replay = (g, steps // batch)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record()
-    if replay:
-        g, reps = replay
-        for _ in range(reps):
-            g.replay()
+    if plan:
+        for g, reps in plan:
+            for _ in range(reps):
+                g.replay()
     else:
         for _ in range(steps):
             step()
@@ -110,16 +125,26 @@ def time_steps(step, steps, warmup, dev, use_graph, dist=None):
     return e0.elapsed_time(e1) / 1e3, wall
 
 
-def isolated_kernel_us(step, dev, n=50):
-    """Median device time of single launches, each bracketed by HIP events on the launch stream."""
+def graph_kernel_us(fn, dev, launches=1000, trials=5):
+    """Per-launch device time of `fn` from `launches` back-to-back launches captured in ONE graph,
+    HIP events on the launch stream; median of `trials` replays.  Graph-launch overhead is
+    amortised over 1000 launches, so this is the kernel's average duration (plus the in-graph
+    dispatch gap), the number a rocprofv3 kernel trace of the same launches averages to."""
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize(dev)
+    g = capture(fn, launches, dev)
+    g.replay()
+    torch.cuda.synchronize(dev)
     ts = []
-    for _ in range(n):
+    for _ in range(trials):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        step()
+        g.replay()
         b.record()
         torch.cuda.synchronize(dev)
-        ts.append(a.elapsed_time(b) * 1e3)
+        ts.append(a.elapsed_time(b) * 1e3 / launches)
+    del g
     return float(np.median(ts))
 
 
@@ -143,20 +168,29 @@ def cpu_baseline(P, ne, Pe, seconds):
         os.sched_setaffinity(0, {min(aff)})
     except (AttributeError, OSError):
         aff = None
-    reps, t0 = 0, time.perf_counter()
-    while True:
+    try:  # one thread (SciPy's CSR SpMV is single-threaded; this pins any BLAS pool too)
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(1)
+    except ImportError:
+        limiter = None
+    # median of 50 reps (after 3 warm-up reps), inside the time budget
+    for _ in range(3):
+        y = Sys @ T
+    ts, t_start = [], time.perf_counter()
+    while len(ts) < 50 and time.perf_counter() - t_start < seconds:
+        t0 = time.perf_counter()
         y = Sys @ T
         y[mask] = T[mask]
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+        ts.append(time.perf_counter() - t0)
+    if limiter is not None:
+        limiter.unregister()
     if aff is not None:
         os.sched_setaffinity(0, aff)
-    return {"value": N * reps / el, "unit": "DOF-updates/s", "cores": 1, "kind": "port",
-            "sample": f"cfg2 64x64 P=8 (N={N}): {reps} x (SciPy CSR Sys@T + Dirichlet rows), {el:.1f} s, "
-                      f"1 of {os.cpu_count()} host threads (oracle/sem_oracle.py restatement of "
-                      f"ConvectionDiffusion_Solver.py:85-87,112-119)"}
+    med = float(np.median(ts))
+    return {"value": N / med, "unit": "DOF-updates/s", "cores": 1, "kind": "port",
+            "sample": f"cfg2 64x64 P=8 (N={N}): median of {len(ts)} reps of (SciPy CSR Sys@T + Dirichlet "
+                      f"rows) = {med * 1e3:.3f} ms, 1 thread pinned to 1 core of {os.cpu_count()} host threads "
+                      f"(oracle/sem_oracle.py restatement of ConvectionDiffusion_Solver.py:85-87,112-119)"}
 
 
 def load_pmc(workload):
@@ -233,12 +267,9 @@ def main():
     n_loc = mesh.n_local
     bytes_launch, flops_launch = 32.0 * n_loc, 8.0 * (P + 1) ** 3 * (ee - eb) * ney
     apply_only = (lambda: mesh.apply(T, y, **kw))
-    if world == 1:
-        kern_s = secs / args.steps          # timed region / launches (graph-replayed, includes launch gaps)
-    else:
-        k_secs, _ = time_steps(apply_only, 500, 50, dev, use_graph=True)
-        kern_s = k_secs / 500
-    iso_us = isolated_kernel_us(apply_only, dev)
+    # the kernel's average launch duration: 1000 back-to-back launches in one graph (HIP events on
+    # the launch stream); the timed region's per-step time is reported beside it as step_us
+    kern_s = graph_kernel_us(apply_only, dev) * 1e-6
     achieved = bytes_launch / kern_s / 1e9
     workload = f"cd_matvec_{ne}x{ne}_P{P}"
     out = {
@@ -260,15 +291,16 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
                      "kernel": mesh.kernel_name(), "bytes_per_launch": bytes_launch,
-                     "flops_per_launch": flops_launch, "kernel_us": kern_s * 1e6, "kernel_us_isolated": iso_us,
+                     "flops_per_launch": flops_launch, "kernel_us": kern_s * 1e6,
+                     "kernel_us_from": "1000-launch hipGraph, HIP events on the launch stream",
+                     "step_us": secs / args.steps * 1e6,
                      "fp64_tflops": flops_launch / kern_s / 1e12, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
     }
 
     if world == 1:
         # BASELINE.json's metric read literally: the Laplacian-only y = K T (16 B/DOF: read T, write y)
         kwl = dict(c_stiff=1.0)
-        sl, _ = time_steps(lambda: mesh.apply(T, y, **kwl), 1000, 100, dev, use_graph=True)
-        kl = sl / 1000
+        kl = graph_kernel_us(lambda: mesh.apply(T, y, **kwl), dev) * 1e-6
         out["laplacian_only"] = {"value": N_glob / kl, "unit": "DOF-updates/s", "ms_per_step": kl * 1e3,
                                  "kernel": mesh.kernel_name(), "bytes_per_launch": 16.0 * n_loc,
                                  "achieved": 16.0 * n_loc / kl / 1e9, "unit_bw": "GB/s",
@@ -277,8 +309,7 @@ def main():
         # v_mfma_f64_16x16x4_f64, SEM_ALGO_MFMA): its fraction of the fp64 MFMA peak, beside the
         # default VALU band kernel that beats it
         kwm = dict(kw, algo=_lib.ALGO_MFMA)
-        sm, _ = time_steps(lambda: mesh.apply(T, y, **kwm), 1000, 100, dev, use_graph=True)
-        km = sm / 1000
+        km = graph_kernel_us(lambda: mesh.apply(T, y, **kwm), dev) * 1e-6
         out["mfma_variant"] = {"kernel": mesh.kernel_name(_lib.ALGO_MFMA), "kernel_us": km * 1e6,
                                "value": N_glob / km, "unit": "DOF-updates/s",
                                "fp64_tflops": flops_launch / km / 1e12, "mfma_peak_tflops": FP64_PEAK_TFLOPS,
@@ -291,8 +322,7 @@ def main():
         Tb, ub, vb = (torch.rand(big.n_local, dtype=torch.float64, device=dev) * 2 - 1 for _ in range(3))
         yb = torch.empty_like(Tb)
         kwb = dict(kw, cu=ub, cv=vb)
-        sb, _ = time_steps(lambda: big.apply(Tb, yb, **kwb), 50, 3, dev, use_graph=True)
-        kb = sb / 50
+        kb = graph_kernel_us(lambda: big.apply(Tb, yb, **kwb), dev, launches=50, trials=3) * 1e-6
         bb = 32.0 * big.n_local
         wl = f"cd_matvec_{args.hbm_ne}x{args.hbm_ne}_P{P}"
         out["roofline_hbm"] = {"workload": wl, "kernel": big.kernel_name(), "dofs": big.n_local,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 1
+#define SEM_ABI_VERSION 2
 
 enum sem_status {
   SEM_OK = 0,
@@ -111,11 +111,31 @@ typedef struct sem_apply_desc {
   int algo;                  /* enum sem_algo */
 } sem_apply_desc;
 
+/* Kernel-selection knobs.  Every value selects a variant with bitwise-identical results (tile
+ * shape, cache policy, argument passing); none changes an answer.  Defaults come from the
+ * environment variable named beside each knob, read ONCE at the first use; 0 = library default. */
+enum sem_tune {
+  SEM_TUNE_BAND_TILE = 0, /* SEM_BAND_TILE: band kernel tile / variant (tools/kbench.py)          */
+  SEM_TUNE_BAND_CPOL = 1, /* SEM_BAND_CPOL: cache policy of the band kernel's y stores / u,v loads */
+  SEM_TUNE_BAND_KP = 2,   /* SEM_BAND_KP: -1 = struct-only kernel arguments, else preloaded      */
+  SEM_TUNE_MARCH_WG = 3,  /* SEM_MARCH_WG: workgroups of the marching variant                     */
+  SEM_TUNE_MFMA_TILE = 4, /* SEM_MFMA_TILE: MFMA kernel tile                                      */
+  SEM_TUNE_COL_TILE = 5,  /* SEM_COL_TILE: column kernel tile                                     */
+  SEM_TUNE_COUNT = 6
+};
+
 /* ---- library ------------------------------------------------------------ */
 int sem_abi_version(void);
 const char* sem_last_error(void);
 /* Largest polynomial order with a compiled device kernel. */
 int sem_max_order(void);
+/* Hash of the sources and headers the library was built from (sem_amd/build.py embeds it); the
+ * Python loader refuses a library whose hash differs from the in-tree sources.  A "+diag" suffix
+ * marks a diagnostic build. */
+const char* sem_build_id(void);
+/* Set / read a kernel-selection knob (enum sem_tune); SEM_EINVAL for an unknown knob. */
+int sem_set_tuning(int knob, int value);
+int sem_get_tuning(int knob, int* value);
 
 /* ---- GLL reference element (host), Solvers/GLL.py ------------------------ */
 /* GLL.standard_nodes (GLL.py:7-33): xi[P+1], w[P+1], V[(P+1)^2] row-major (V nullable). */

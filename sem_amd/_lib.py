@@ -12,7 +12,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 
+ABI_VERSION = 2
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
+TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE = range(6)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
 DIR_NONE, DIR_IDENTITY, DIR_REPLACE = 0, 1, 2
 ALGO_AUTO, ALGO_VALU, ALGO_MFMA, ALGO_COLUMN, ALGO_BAND = 0, 1, 2, 3, 4
@@ -41,6 +43,9 @@ _SIGS = {
     "sem_abi_version": (C.c_int, []),
     "sem_last_error": (C.c_char_p, []),
     "sem_max_order": (C.c_int, []),
+    "sem_build_id": (C.c_char_p, []),
+    "sem_set_tuning": (C.c_int, [C.c_int, C.c_int]),
+    "sem_get_tuning": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
     "sem_gll_nodes": (C.c_int, [C.c_int, _dp, _dp, _dp]),
     "sem_gll_differentiation": (C.c_int, [C.c_int, _dp]),
     "sem_gll_gradient": (C.c_int, [C.c_int, _dp]),
@@ -84,14 +89,32 @@ def load():
             if not os.path.exists(LIB_PATH):
                 raise RuntimeError(f"libsemops.so is missing and could not be built: {e}") from e
     lib = C.CDLL(LIB_PATH)
+    if not hasattr(lib, "sem_build_id") or lib.sem_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH} was built for another ABI version; rebuild: python -m sem_amd.build")
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.sem_abi_version() != 1:
-        raise RuntimeError("libsemops ABI version mismatch")
+    _check_build_id(lib)
     _lib = lib
     return lib
+
+
+def _check_build_id(lib):
+    """The library must be built from the sources in this tree (a stale .so would make the GPU
+    tests validate old kernels), and must not be a diagnostic build unless asked for."""
+    bid = lib.sem_build_id().decode()
+    base, diag = bid.split("+")[0], bid.endswith("+diag")
+    if diag and os.environ.get("SEM_ALLOW_DIAG", "0") != "1":
+        raise RuntimeError(f"{LIB_PATH} is a diagnostic build (SEM_DIAGNOSTICS=1); set SEM_ALLOW_DIAG=1 to use it")
+    try:
+        from .build import source_hash
+        want = source_hash()
+    except OSError:  # sources not shipped with this tree: nothing to compare against
+        return
+    if base != want:
+        raise RuntimeError(f"{LIB_PATH} (build id {bid}) was not built from the sources in this tree "
+                           f"(hash {want}); rebuild: python -m sem_amd.build")
 
 
 def check(status):

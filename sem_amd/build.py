@@ -34,6 +34,17 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_hash():
+    """Hash of every source and header of the library (and this build script), embedded in the
+    library as sem_build_id(); sem_amd._lib refuses a library built from other sources."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in sorted(SOURCES + HEADERS) + [os.path.join("..", "build.py")]:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read() + b"\0")
+    return h.hexdigest()[:16]
+
+
 CONSTS = os.path.join(CSRC, "gll_consts.h")
 
 
@@ -61,22 +72,34 @@ def gen_consts(verbose=False):
 EXTRA_FLAGS = {"apply_band.hip": ["-mllvm", "-amdgpu-kernarg-preload-count=14"]}
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, diag=False):
+    """diag=True: a diagnostic build (SEM_DIAGNOSTICS=1: SEM_DIAG ablation bits and per-wave phase
+    stamps, for tools/kbench.py); its build id carries "+diag" and sem_amd._lib loads it only with
+    SEM_ALLOW_DIAG=1.  The default build has no diagnostic path at all."""
+    mode = "diag" if diag else "release"
+    stamp = os.path.join(LIBDIR, ".build_mode")
+    prev_mode = open(stamp).read().strip() if os.path.exists(stamp) else None
+    force = force or prev_mode != mode
     if not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     gen_consts(verbose)
     hipcc = _hipcc()
-    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-I", os.path.join(ROOT, "include")]
+    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-I", os.path.join(ROOT, "include"),
+             f"-DSEM_DIAGNOSTICS={1 if diag else 0}"]
     objs, procs = [], []
     hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS + [os.path.join("..", "build.py")])
+    bid = source_hash()
     for src in SOURCES:  # one hipcc per translation unit, in parallel; unchanged objects are reused
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
-        if (not force and os.path.exists(obj)
+        # the build id goes into the small host TU only, so a source change rebuilds just that TU
+        # and the changed one; it is recompiled on every build
+        extra = [f'-DSEM_BUILD_ID="{bid}"'] if src == "gll_tables.cpp" else []
+        if (not force and not extra and os.path.exists(obj)
                 and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, src)))):
             continue
-        cmd = [hipcc] + flags + EXTRA_FLAGS.get(src, []) + ["-c", "-o", obj, os.path.join(CSRC, src)]
+        cmd = [hipcc] + flags + extra + EXTRA_FLAGS.get(src, []) + ["-c", "-o", obj, os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((src, subprocess.Popen(cmd)))
@@ -89,9 +112,11 @@ def build(force=False, verbose=False):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    with open(stamp, "w") as f:
+        f.write(mode)
     return LIB
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
+    build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv)
     print(LIB)

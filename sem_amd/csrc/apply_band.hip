@@ -446,10 +446,10 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   // Diagnostics (SEM_DIAG bit 8): s_memtime phase stamps held in SGPRs, written at the very end
   // so that no diagnostic store sits in the vmcnt queue of the measured phases.
   unsigned long long stv[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0, rt1 = 0;
-  if (!KP && a.stamps) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
+  if (kDiag && !KP && a.stamps) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
 #define BSTAMP(k)                                                                      \
   do {                                                                                 \
-    if ((!KP || (k) >= 2) && a.stamps) {  /* KP: no stamps before the loads issue */   \
+    if (kDiag && (!KP || (k) >= 2) && a.stamps) {  /* KP: no stamps before the loads issue */   \
       __builtin_amdgcn_sched_barrier(0);                                               \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stv[k])::"memory"); \
       __builtin_amdgcn_sched_barrier(0);                                               \
@@ -467,7 +467,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   // the staged x window, then u, v of this thread's epilogue nodes.  Buffer bounds make lines
   // outside the local range read 0; columns past the domain's y-ends wrap into neighbouring
   // lines.  Neither is ever consumed.
-  const int sbase = (!KP && (a.diag & 64)) ? -(1 << 30) : ((gx0 - P - lb0) * NY + gy0 - P) * 8;  // diag 64: no staging loads
+  const int sbase = (kDiag && !KP && (a.diag & 64)) ? -(1 << 30) : ((gx0 - P - lb0) * NY + gy0 - P) * 8;  // diag 64: no staging loads
   double st[C::NSTAGE];
 #pragma unroll
   for (int s = 0; s < C::NSTAGE; ++s) {
@@ -493,7 +493,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   for (int e = 0; e < C::NE; ++e) {
     const int q = tid + e * C::THREADS;
     const int r = q / LW, c = q - r * LW;
-    const bool ok = q < BX * LW && r < rows_ok && c < cols_ok && !(a.diag & 32);  // diag 32: no u/v/y traffic
+    const bool ok = q < BX * LW && r < rows_ok && c < cols_ok && !(kDiag && (a.diag & 32));  // diag 32: no u/v/y traffic
     eoff[e] = ok ? nodeb + r * NY + c : -(1 << 26);  // out of bounds: touches no memory
     if (a.cpol & 256) {  // u, v are read once per launch: non-temporal
       pu[e] = bload_c<2>(ru, eoff[e] * 8);
@@ -520,7 +520,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
     BPIN(a.cpol);
     BPIN(a.lb1);
     BPIN(a.nex);
-    BPIN(a.diag);
+    if constexpr (kDiag) BPIN(a.diag);
   }
 
   // ---- LDS: weights, staged window (columns outside the domain staged as 0: absent elements)
@@ -641,10 +641,10 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   for (int e = 0; e < C::NE; ++e) {
     const int q = tid + e * C::THREADS;
     const int r = q / LW, c = q - r * LW;
-    if (q < BX * LW && r < rows_ok && c < cols_ok && !(a.diag & 16)) bstore_any(a.cpol, ry, eoff[e] * 8, zz[e]);
+    if (q < BX * LW && r < rows_ok && c < cols_ok && !(kDiag && (a.diag & 16))) bstore_any(a.cpol, ry, eoff[e] * 8, zz[e]);
   }
   BSTAMP(5);
-  if (a.stamps) {
+  if (kDiag && a.stamps) {
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1)::"memory");
     unsigned xcc_, hw_;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)" : "=s"(xcc_), "=s"(hw_));
@@ -682,10 +682,10 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
   BPIN(a.tiles_y);
   BPIN(a.nbytes);
   BPIN(a.dir_mode);
-  BPIN(a.diag);
+  if constexpr (kDiag) BPIN(a.diag);
   BPIN(a.sides);
   BPIN(a.flags);
-  BPIN(a.stamps);
+  if constexpr (kDiag) BPIN(a.stamps);
   BPIN(a.nblk);
   BPIN(a.cpol);
   band_body<P, TXE, TYE, NS, FULL, DPP, GRAD, false>(a.x, (a.flags & 1) ? a.cu : nullptr, (a.flags & 2) ? a.cv : nullptr,
@@ -1031,15 +1031,11 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   b.has_e2 = g.has_e2;
   b.stamps = g.stamps;
   b.nblk = static_cast<int>(nblk);
-  {
-    const char* e = std::getenv("SEM_BAND_CPOL");  // cache-policy override, read per call (in-process A/B)
-    b.cpol = e ? std::atoi(e) : band_cpol(g.n_local32);
-  }
+  b.cpol = tune(SEM_TUNE_BAND_CPOL) ? tune(SEM_TUNE_BAND_CPOL) : band_cpol(g.n_local32);
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   const bool grad = g.cX != 0.0 || g.cY != 0.0;
   const dim3 grid(static_cast<unsigned>(nblk)), block(C::THREADS);
-  const char* kpe = std::getenv("SEM_BAND_KP");  // SEM_BAND_KP=0: struct-only arguments (A/B), read per call
-  if (!(kpe && std::atoi(kpe) == 0)) {
+  if (tune(SEM_TUNE_BAND_KP) >= 0) {  // -1 (SEM_BAND_KP=0): struct-only arguments (A/B)
 #define SEM_KP_ARGS b.x, b.cu, b.cv, b.NY, b.lb0, b.ex_begin, b.ex_end, b.ney, b.nblk, b.tiles_y, b.nbytes, b
     if (full && grad)
       hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, DPP, true>), grid, block, 0, s, SEM_KP_ARGS);
@@ -1072,8 +1068,7 @@ static int launch_march(const ApplyArgs& g, const sem_handle* h, hipStream_t s) 
   const int ncols = h->ex_end - h->ex_begin;
   const long long npos = ncols + 1;  // + the ghost position of the closing line
   const long long tiles_y = (h->ney + 1 + TYE - 1) / TYE;
-  const char* e = std::getenv("SEM_MARCH_WG");
-  const long long target = std::max(64, e ? std::atoi(e) : 1024);
+  const long long target = std::max(64, tune(SEM_TUNE_MARCH_WG) ? tune(SEM_TUNE_MARCH_WG) : 1024);
   const long long chunks_want = std::max(1LL, std::min(npos, target / tiles_y));
   const long long mchunk = (npos + chunks_want - 1) / chunks_want;
   const long long nchunks = (npos + mchunk - 1) / mchunk;
@@ -1116,10 +1111,7 @@ static int launch_march(const ApplyArgs& g, const sem_handle* h, hipStream_t s) 
   b.stamps = nullptr;
   b.nblk = static_cast<int>(nblk);
   b.mchunk = static_cast<int>(mchunk);
-  {
-    const char* ce = std::getenv("SEM_BAND_CPOL");
-    b.cpol = ce ? std::atoi(ce) : band_cpol(g.n_local32);
-  }
+  b.cpol = tune(SEM_TUNE_BAND_CPOL) ? tune(SEM_TUNE_BAND_CPOL) : band_cpol(g.n_local32);
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   const bool grad = g.cX != 0.0 || g.cY != 0.0;
   const dim3 grid(static_cast<unsigned>(nblk)), block(C::THREADS);
@@ -1146,8 +1138,7 @@ struct BandShape {
 template <int P>
 static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
   using S = BandShape<P>;
-  const char* env = std::getenv("SEM_BAND_TILE");  // tuning override, read per call (in-process A/B)
-  const int force = env ? std::atoi(env) : 0;
+  const int force = tune(SEM_TUNE_BAND_TILE);  // tuning knob (sem_set_tuning / SEM_BAND_TILE, read once)
   if constexpr (P == 8) {
     if (force == 1) return launch_band<P, 1, S::TYE, 4>(args, h, s);
     if (force == 2) return launch_band<P, 2, S::TYE, 4>(args, h, s);
@@ -1172,14 +1163,12 @@ static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStrea
 std::string band_kernel_name(int P, long long n_local) {
   const int TYE = std::max(1, 64 / P), TXE = std::min(4, std::max(1, 8 / P));
   const int NS = P >= 2 ? 2 : 1;
-  const char* e = std::getenv("SEM_BAND_TILE");
-  const int force = e ? std::atoi(e) : 0;
+  const int force = tune(SEM_TUNE_BAND_TILE);
   const bool dpp = force == 3 || force == 8 || (force == 0 && n_local >= (1 << 20));
   if (force == 7 || force == 8)
     return "sem::apply_march<" + std::to_string(P) + ", " + std::to_string(TYE) + ", " + std::to_string(NS) +
            (dpp ? ", dpp" : "") + ">";
-  const char* kpe = std::getenv("SEM_BAND_KP");
-  const bool kp = !(kpe && std::atoi(kpe) == 0);
+  const bool kp = tune(SEM_TUNE_BAND_KP) >= 0;
   return std::string(kp ? "sem::apply_band_kp<" : "sem::apply_band<") + std::to_string(P) + ", " + std::to_string(TXE) +
          ", " + std::to_string(TYE) + ", " + std::to_string(NS) + (dpp ? ", dpp" : "") + ">";
 }

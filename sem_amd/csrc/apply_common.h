@@ -90,7 +90,7 @@ __device__ __forceinline__ void for_rows(std::integer_sequence<int, R...>, F&& f
 // Diagnostic phase stamp (SEM_DIAG bit 8): lane 0 of each wave records s_memtime.
 #define SEM_STAMP(k)                                                                      \
   do {                                                                                    \
-    if (a.stamps) {                                                                       \
+    if (kDiag && a.stamps) {                                                              \
       unsigned long long t_;                                                              \
       __builtin_amdgcn_sched_barrier(0);                                                  \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
@@ -102,7 +102,7 @@ __device__ __forceinline__ void for_rows(std::integer_sequence<int, R...>, F&& f
 // Diagnostic slot 7: the XCD and hardware id this wave runs on (stamps are per-XCD clocks).
 #define SEM_STAMP_HWID()                                                                                     \
   do {                                                                                                       \
-    if (a.stamps && (threadIdx.x & 63) == 0) {                                                               \
+    if (kDiag && a.stamps && (threadIdx.x & 63) == 0) {                                                      \
       unsigned xcc_, hw_;                                                                                    \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)"           \
                    : "=s"(xcc_), "=s"(hw_));                                                                 \

@@ -9,6 +9,7 @@
 // (FP contraction is disabled for this translation unit by the build).
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -28,6 +29,43 @@ int set_error(int code, const std::string& msg) {
 }
 void clear_error() { g_last_error.clear(); }
 const char* last_error() { return g_last_error.c_str(); }
+
+static int env_int(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : 0;
+}
+
+Tuning& tuning() {
+  static Tuning t = [] {  // the environment is read once, at the first use
+    Tuning r{};
+    r.v[SEM_TUNE_BAND_TILE] = env_int("SEM_BAND_TILE");
+    r.v[SEM_TUNE_BAND_CPOL] = env_int("SEM_BAND_CPOL");
+    const char* kp = std::getenv("SEM_BAND_KP");  // SEM_BAND_KP=0: struct-only kernel arguments
+    r.v[SEM_TUNE_BAND_KP] = (kp && std::atoi(kp) == 0) ? -1 : 0;
+    r.v[SEM_TUNE_MARCH_WG] = env_int("SEM_MARCH_WG");
+    r.v[SEM_TUNE_MFMA_TILE] = env_int("SEM_MFMA_TILE");
+    r.v[SEM_TUNE_COL_TILE] = env_int("SEM_COL_TILE");
+    return r;
+  }();
+  return t;
+}
+
+#if SEM_DIAGNOSTICS
+int diag_bits() {
+  static const int d = env_int("SEM_DIAG");  // ablation bits: results are wrong when set (diagnostic builds only)
+  return d;
+}
+unsigned long long* diag_stamps() {
+  static unsigned long long* p = [] {
+    const char* e = std::getenv("SEM_DIAG_BUF");  // device address of a stamp buffer
+    return e ? reinterpret_cast<unsigned long long*>(std::strtoull(e, nullptr, 0)) : nullptr;
+  }();
+  return p;
+}
+#else
+int diag_bits() { return 0; }
+unsigned long long* diag_stamps() { return nullptr; }
+#endif
 
 int gll_nodes(int P, double* xi, double* w, double* V) {
   if (P < 1 || P > 64) return set_error(SEM_EINVAL, "polynomial order must be in [1, 64]");
@@ -139,3 +177,8 @@ int global_index(int P, int nex, int ney, const int64_t* m, const int64_t* n, co
 }
 
 }  // namespace sem
+
+#ifndef SEM_BUILD_ID
+#define SEM_BUILD_ID "unknown"
+#endif
+extern "C" const char* sem_build_id(void) { return sem::kDiag ? SEM_BUILD_ID "+diag" : SEM_BUILD_ID; }

@@ -23,6 +23,28 @@ int global_index(int P, int nex, int ney, const int64_t* m, const int64_t* n, co
 
 constexpr int kMaxOrder = 16;  // largest P with a compiled device kernel
 
+// Diagnostic builds only (python -m sem_amd.build --diag): ablation bits and per-wave phase
+// stamps for performance analysis.  The shipped library is built with SEM_DIAGNOSTICS=0: the
+// ablation paths are compiled out and no environment variable can reach them.
+#ifndef SEM_DIAGNOSTICS
+#define SEM_DIAGNOSTICS 0
+#endif
+constexpr bool kDiag = SEM_DIAGNOSTICS != 0;
+
+// Kernel-selection knobs (enum sem_tune).  They pick among variants that compute bitwise-identical
+// results (tile shapes, cache policies, argument passing), so they never change an answer.  They
+// are read from the environment once, at the first use, and changed afterwards only through
+// sem_set_tuning (in-process A/B tools).  0 = library default.
+struct Tuning {
+  int v[SEM_TUNE_COUNT];
+};
+Tuning& tuning();
+inline int tune(int knob) { return tuning().v[knob]; }
+
+// Diagnostic state (SEM_DIAGNOSTICS builds only): SEM_DIAG bits and the SEM_DIAG_BUF stamp buffer.
+int diag_bits();
+unsigned long long* diag_stamps();
+
 }  // namespace sem
 
 // Immutable per-(device, partition) state.  Device table layout (doubles):

@@ -411,7 +411,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
     // ---- phases A and B: each wave owns a homogeneous list of tasks (the first half of the
     // waves phase A, the rest phase B); it issues every operand read of its tasks first, then
     // all MFMAs with one independent K and one G accumulator chain per task, then the writes.
-    if (!(a.diag & 1)) {
+    if (!(kDiag && (a.diag & 1))) {
       constexpr int NWA = C::NWA, NWB = NW - C::NWA;
       if (wave < NWA) {
         constexpr int TW = (C::TA + NWA - 1) / NWA, TG = TW < C::MAXG ? TW : C::MAXG;
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
       const double fkl = sm.FK[(ey * C::FL + rl) * n + P], fgl = sm.FG[(ey * C::FL + rl) * n + P];
       const double fkr = sm.FK[((ey + 1) * C::FL + rl) * n + j], fgr = sm.FG[((ey + 1) * C::FL + rl) * n + j];
       const double wi = sm.ws[i], wj = sm.ws[j];
-      if (a.diag & 2) {
+      if (kDiag && (a.diag & 2)) {
         bstore(ry, off, xv * cu_[qn] + cv_[qn]);
         continue;
       }
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
         const int p = (gx - lb0) * NY + gy;
         const double uu = a.cu ? a.cu[p] : 1.0, vv = a.cv ? a.cv[p] : 1.0;
         const double xv = sm.Ts[(P + rl) * C::PT + P + c];
-        if (a.diag & 2) {
+        if (kDiag && (a.diag & 2)) {
           a.y[p] = xv * uu + vv;
           return;
         }
@@ -665,10 +665,7 @@ static int launch_apply_mfma_auto(const ApplyArgs& args, const sem_handle* h, hi
   constexpr int TL = (32 / P) > 0 ? 32 / P : 1;
   constexpr int TS = (16 / P) > 0 ? 16 / P : 1;
   const long long big_tiles = static_cast<long long>((h->ex_end - h->ex_begin + TL - 1) / TL) * ((h->ney + TL - 1) / TL);
-  static const int force = [] {
-    const char* e = std::getenv("SEM_MFMA_TILE");  // tuning override: 1 = small 2-wave, 2 = large, 3 = small 4-wave
-    return e ? std::atoi(e) : 0;
-  }();
+  const int force = tune(SEM_TUNE_MFMA_TILE);  // tuning knob (sem_set_tuning / SEM_MFMA_TILE, read once)
   if (force == 2 || (force == 0 && big_tiles >= 4 * 256)) return launch_apply_mfma<P, TL, TL, 4, true, false>(args, h, s);
   if (force == 1) return launch_apply_mfma<P, TS, TS, 2, false, false>(args, h, s);
   return launch_apply_mfma<P, TS, TS, 4, false, true>(args, h, s);
@@ -868,10 +865,7 @@ static int launch_apply_col(const ApplyArgs& args_in, const sem_handle* h, hipSt
 
 template <int P>
 static int launch_apply_col_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
-  static const int force = [] {
-    const char* e = std::getenv("SEM_COL_TILE");  // tuning override
-    return e ? std::atoi(e) : 0;
-  }();
+  const int force = tune(SEM_TUNE_COL_TILE);  // tuning knob (sem_set_tuning / SEM_COL_TILE, read once)
   constexpr int RS = (P % 4 == 0) ? 4 : (P % 2 == 0 ? 2 : 1);
   constexpr int BYs = 64 / RS > 16 ? 64 / RS : 16;
   if (force == 1) return launch_apply_col<P, 2, BYs, RS>(args, h, s);
@@ -984,9 +978,32 @@ static unsigned grid_for(int64_t total, int threads) {
 // =========================================================================== C ABI
 using namespace sem;
 
+// Every launcher runs on the handle's device: a handle used while another device is current
+// would launch there against this device's pointers, so it is an error (SEM_EINVAL).
+static int on_device(const sem_handle* h) {
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return sem::set_error(SEM_EHIP, "hipGetDevice failed");
+  if (cur != h->device)
+    return sem::set_error(SEM_EINVAL, "handle belongs to device " + std::to_string(h->device) + " but device " +
+                                          std::to_string(cur) + " is current");
+  return SEM_OK;
+}
+
 extern "C" {
 
 int sem_abi_version(void) { return SEM_ABI_VERSION; }
+
+int sem_set_tuning(int knob, int value) {
+  if (knob < 0 || knob >= SEM_TUNE_COUNT) return set_error(SEM_EINVAL, "unknown tuning knob");
+  tuning().v[knob] = value;
+  return SEM_OK;
+}
+
+int sem_get_tuning(int knob, int* value) {
+  if (knob < 0 || knob >= SEM_TUNE_COUNT || !value) return set_error(SEM_EINVAL, "unknown tuning knob");
+  *value = tuning().v[knob];
+  return SEM_OK;
+}
 const char* sem_last_error(void) { return last_error(); }
 int sem_max_order(void) { return kMaxOrder; }
 
@@ -1100,6 +1117,7 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   if (d->dir_mode == SEM_DIR_REPLACE && !d->dir_val) return set_error(SEM_EINVAL, "SEM_DIR_REPLACE needs dir_val");
   if (d->algo < SEM_ALGO_AUTO || d->algo > SEM_ALGO_BAND) return set_error(SEM_EINVAL, "bad algo");
   if (d->algo == SEM_ALGO_MFMA && h->P > 15) return set_error(SEM_EUNSUPPORTED, "MFMA path needs P <= 15");
+  if (int st = on_device(h)) return st;
   ApplyArgs a{};
   a.x = x;
   a.y = y;
@@ -1136,16 +1154,8 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   a.dir_mode = d->dir_mode;
   a.sides = d->dir_sides;
   a.n_local32 = static_cast<int>(std::min<int64_t>(h->n_local, 0x7fffffff));
-  static const int diag = [] {
-    const char* e = std::getenv("SEM_DIAG");  // ablation for profiling only: results are wrong when set
-    return e ? std::atoi(e) : 0;
-  }();
-  a.diag = diag;
-  static unsigned long long* stamps = [] {
-    const char* e = std::getenv("SEM_DIAG_BUF");  // device address of a stamp buffer (diagnostics)
-    return e ? reinterpret_cast<unsigned long long*>(std::strtoull(e, nullptr, 0)) : nullptr;
-  }();
-  a.stamps = (diag & 8) ? stamps : nullptr;
+  a.diag = kDiag ? diag_bits() : 0;
+  a.stamps = (kDiag && (a.diag & 8)) ? diag_stamps() : nullptr;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // Buffer-resource kernels (MFMA, band) address the local vector with 32-bit byte offsets.
   // AUTO, measured on MI355X (tools/kbench.py): the band kernel on every mesh whose local vector
@@ -1220,6 +1230,7 @@ int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
 
 int sem_gather_elements(sem_handle* h, const double* u, double* ue, void* stream) {
   if (!h || !u || !ue) return set_error(SEM_EINVAL, "null argument");
+  if (int st = on_device(h)) return st;
   const int n = h->P + 1;
   const int64_t total = static_cast<int64_t>(h->ex_end - h->ex_begin) * h->ney * n * n;
   hipLaunchKernelGGL(gather_kernel, dim3(grid_for(total, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), u,
@@ -1230,6 +1241,7 @@ int sem_gather_elements(sem_handle* h, const double* u, double* ue, void* stream
 int sem_dss(sem_handle* h, const double* ae, double* out, void* stream) {
   if (!h || !ae || !out) return set_error(SEM_EINVAL, "null argument");
   if (static_cast<const void*>(ae) == static_cast<const void*>(out)) return set_error(SEM_EINVAL, "in/out alias");
+  if (int st = on_device(h)) return st;
   hipLaunchKernelGGL(dss_kernel, dim3(grid_for(h->n_local, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      ae, out, h->P, h->ney, h->ex_begin, h->ex_end, h->line_begin, h->NY, h->n_local);
   return hip_check(hipGetLastError(), "dss launch");
@@ -1240,6 +1252,7 @@ int sem_eval_interpolation(sem_handle* h, const double* ue, int na, const int* m
   if (!h || !ue || !out || na < 0 || nb < 0) return set_error(SEM_EINVAL, "bad interpolation arguments");
   if (na == 0 || nb == 0) return SEM_OK;
   if (!m_idx || !Sx || !n_idx || !Sy) return set_error(SEM_EINVAL, "null interpolation table");
+  if (int st = on_device(h)) return st;
   hipLaunchKernelGGL(interp_kernel, dim3(grid_for(static_cast<int64_t>(na) * nb, 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), ue, h->P, h->ney, h->ex_begin, h->ex_end, m_idx, Sx, na,
                      n_idx, Sy, nb, out);
@@ -1265,6 +1278,7 @@ int sem_interface_pack(sem_handle* h, const double* y, const int* bounds, int G,
   int L, R, st;
   if ((st = iface_slots(h, bounds, G, &L, &R))) return st;
   if (G < 2) return SEM_OK;
+  if ((st = on_device(h))) return st;
   const int64_t total = static_cast<int64_t>(G - 1) * h->NY;
   hipLaunchKernelGGL(iface_pack_kernel, dim3(grid_for(total, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      y, buf, h->NY, G - 1, L, static_cast<int64_t>(0), R, h->n_local - h->NY);
@@ -1276,6 +1290,7 @@ int sem_interface_unpack(sem_handle* h, const double* buf, const int* bounds, in
   int L, R, st;
   if ((st = iface_slots(h, bounds, G, &L, &R))) return st;
   if (G < 2) return SEM_OK;
+  if ((st = on_device(h))) return st;
   hipLaunchKernelGGL(iface_unpack_kernel, dim3(grid_for(h->NY, 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), buf, y, h->NY, L, static_cast<int64_t>(0), R,
                      h->n_local - h->NY);

@@ -26,6 +26,8 @@ class _DeviceSweeps:
     routes.  Used for device tensors without a distributed inner product."""
 
     def __init__(self, V):
+        if V.dtype != torch.float64 or not V.is_cuda or V.stride(1) != 1:
+            raise ValueError("the HIP basis sweeps need a float64 device basis with unit column stride")
         from . import _lib
         self.lib = _lib.load()
         self.check = _lib.check
@@ -37,14 +39,24 @@ class _DeviceSweeps:
     def _stream(self):
         return torch.cuda.current_stream(self.V.device).cuda_stream
 
+    def _vec(self, t, name):
+        V = self.V
+        if t.dtype != torch.float64 or t.device != V.device or not t.is_contiguous() or t.numel() != V.shape[1]:
+            raise ValueError(f"{name} must be a contiguous float64 vector of {V.shape[1]} entries on {V.device}")
+
     def dot2(self, k, a, b):
         """[V_j . a, V_j . b] for the first k rows -> (k, 2) view."""
+        self._vec(a, "a")
+        self._vec(b, "b")
         self.check(self.lib.sem_basis_dot2(self.V.data_ptr(), self.ldv, k, self.V.shape[1], a.data_ptr(),
                                            b.data_ptr(), self.work.data_ptr(), self.out.data_ptr(), self._stream()))
         return self.out[:k]
 
     def update(self, k, c, w):
         """w -= V[:k]^T c, in place."""
+        self._vec(w, "w")
+        if c.dtype != torch.float64 or c.device != self.V.device or not c.is_contiguous() or c.numel() < k:
+            raise ValueError("c must be a contiguous float64 vector of >= k entries on the basis device")
         self.check(self.lib.sem_basis_update(self.V.data_ptr(), self.ldv, k, self.V.shape[1], c.data_ptr(),
                                              w.data_ptr(), self._stream()))
 
@@ -81,7 +93,8 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     tol = max(atol, rtol * bnorm)
     V = torch.empty((restart + 1, N), dtype=dt, device=dev)
     G = torch.zeros((restart + 1, restart + 1), dtype=dt, device=dev)  # Gram matrix V^T V of the basis
-    sweeps = _DeviceSweeps(V) if (inner is None and V.is_cuda) else None
+    # the HIP sweeps read and write doubles: other dtypes take torch's GEMV route
+    sweeps = _DeviceSweeps(V) if (inner is None and V.is_cuda and V.dtype == torch.float64) else None
     Z = torch.empty((restart, N), dtype=dt, device=dev) if precond is not None else None
     total, matvecs = 0, 0
     r = b - matvec(x) if x0 is not None else b.clone()

@@ -72,23 +72,24 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
 
 ALGOS = [1, 2, 3, 4, "4dpp", "4m", "4mdpp"]  # VALU two-phase, MFMA, column kernel, assembled band (+ DPP coefficient variant)
 BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2", "4t5": "5", "4t6": "6", "4imm": "4",
-                 "4m": "7", "4mdpp": "8"}  # 4m*: marching kernel (P = 8, 12; other P fall back to the band tile)  # SEM_BAND_TILE values (read per call)
+                 "4m": "7", "4mdpp": "8"}  # 4m*: marching kernel (P = 8, 12; other P fall back to the band tile)  # SEM_TUNE_BAND_TILE values
 
 
-def _algo(algo, monkeypatch):
-    """Select the kernel: an int is sem_apply_desc.algo; a band variant name also sets SEM_BAND_TILE."""
+def _algo(algo, tuning):
+    """Select the kernel: an int is sem_apply_desc.algo; a band variant name also sets the band-tile knob."""
+    from sem_amd import _lib
     if isinstance(algo, str):
-        monkeypatch.setenv("SEM_BAND_TILE", BAND_VARIANTS[algo])
+        tuning(_lib.TUNE_BAND_TILE, BAND_VARIANTS[algo])
         return 4
     return algo
 
 
 @pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", CASES)
-def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo, monkeypatch):
+def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo, tuning):
     if algo == 2 and P > 15:
         pytest.skip("MFMA path covers P <= 15")
-    algo = _algo(algo, monkeypatch)
+    algo = _algo(algo, tuning)
     from sem_amd.device import get_mesh
     Lx, Ly = 1.3, 0.7
     dx, dy = Lx / nex, Ly / ney
@@ -114,8 +115,8 @@ def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo, monkeypatch):
 
 @pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", [(4, 4, 4), (8, 6, 5), (12, 3, 4), (8, 40, 33)])
-def test_dirichlet_rows(gpu, P, nex, ney, algo, monkeypatch):
-    algo = _algo(algo, monkeypatch)
+def test_dirichlet_rows(gpu, P, nex, ney, algo, tuning):
+    algo = _algo(algo, tuning)
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.0 / ney)
@@ -148,9 +149,9 @@ def test_dirichlet_rows(gpu, P, nex, ney, algo, monkeypatch):
 
 @pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", [(8, 130, 67), (12, 70, 45), (4, 300, 211)])
-def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo, monkeypatch):
+def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo, tuning):
     """Meshes big enough for the large-tile / persistent launch configurations."""
-    algo = _algo(algo, monkeypatch)
+    algo = _algo(algo, tuning)
     from sem_amd.device import get_mesh
     dx, dy = 1.0 / nex, 2.0 / ney
     mesh = get_mesh(P, nex, ney, dx, dy)
@@ -165,7 +166,7 @@ def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo, monkeypatch):
 
 
 @pytest.mark.parametrize("P,nex,ney", [(P, 7, 5) for P in range(1, 17)] + [(8, 64, 64), (8, 3, 70)])
-def test_band_variants_bitwise_equal(gpu, P, nex, ney, monkeypatch):
+def test_band_variants_bitwise_equal(gpu, P, nex, ney, tuning):
     """Band kernel variants (DPP-broadcast coefficients, other tile shapes) perform the same
     operations in the same order as the default: results are bitwise identical."""
     from sem_amd import _lib
@@ -175,16 +176,16 @@ def test_band_variants_bitwise_equal(gpu, P, nex, ney, monkeypatch):
     X, U, V = (mesh.to_device(r.uniform(-1, 1, mesh.n_local)) for _ in range(3))
     kw = dict(c_mass=0.25, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, dir_mode=_lib.DIR_IDENTITY,
               dir_sides=_lib.SIDE_W | _lib.SIDE_E, algo=4)
-    monkeypatch.delenv("SEM_BAND_TILE", raising=False)
+    tuning(_lib.TUNE_BAND_TILE, 0)
     base = mesh.apply(X, **kw)
     for name in (["4dpp", "4imm", "4t1", "4t2", "4t5", "4t6", "4m", "4mdpp"] if P in (8, 12) else ["4dpp", "4imm"]):
-        monkeypatch.setenv("SEM_BAND_TILE", BAND_VARIANTS[name])
+        tuning(_lib.TUNE_BAND_TILE, BAND_VARIANTS[name])
         assert torch.equal(mesh.apply(X, **kw), base), name
 
 
 @pytest.mark.parametrize("P,nex,ney,eb,ee", [(8, 64, 64, 0, 64), (8, 40, 13, 10, 30), (4, 9, 7, 2, 9), (12, 5, 3, 0, 5)])
 @pytest.mark.parametrize("full", [False, True])
-def test_band_kernarg_forms_bitwise_equal(gpu, P, nex, ney, eb, ee, full, monkeypatch):
+def test_band_kernarg_forms_bitwise_equal(gpu, P, nex, ney, eb, ee, full, tuning):
     """apply_band_kp (prologue fields as preloaded scalar kernel arguments) and apply_band (all
     fields in the struct) run the same body: bitwise-identical results, FULL path included."""
     from sem_amd import _lib
@@ -199,24 +200,24 @@ def test_band_kernarg_forms_bitwise_equal(gpu, P, nex, ney, eb, ee, full, monkey
         kw.update(c_extra=3.0, ea=A, eb=B, c_acc=2.0, dir_mode=_lib.DIR_IDENTITY, dir_mask=mask, dir_val=G)
     else:
         kw.update(dir_mode=_lib.DIR_IDENTITY, dir_sides=_lib.SIDE_W | _lib.SIDE_E)
-    monkeypatch.delenv("SEM_BAND_TILE", raising=False)
+    tuning(_lib.TUNE_BAND_TILE, 0)
     outs = {}
-    for kp in ("0", "1"):
-        monkeypatch.setenv("SEM_BAND_KP", kp)
+    for kp in (-1, 0):   # -1: struct-only kernel arguments; 0: preloaded prologue arguments
+        tuning(_lib.TUNE_BAND_KP, kp)
         outs[kp] = mesh.apply(X, Y0.clone(), **kw)
-    assert torch.equal(outs["0"], outs["1"])
+    assert torch.equal(outs[-1], outs[0])
     # no convection coefficients (cu = cv = None): the preloaded null pointers select the u, v = 1 path
     kw0 = dict(c_stiff=1.0, c_gradx=2.0, c_grady=3.0, algo=4)
-    monkeypatch.setenv("SEM_BAND_KP", "0")
+    tuning(_lib.TUNE_BAND_KP, -1)
     a0 = mesh.apply(X, **kw0)
-    monkeypatch.setenv("SEM_BAND_KP", "1")
+    tuning(_lib.TUNE_BAND_KP, 0)
     assert torch.equal(mesh.apply(X, **kw0), a0)
 
 
 @pytest.mark.parametrize("P,nex,ney,eb,ee,wg", [(8, 40, 13, 0, 40, 64), (8, 40, 13, 10, 30, 64), (8, 40, 13, 0, 17, 8),
                                                (12, 9, 21, 3, 9, 32), (8, 33, 64, 0, 33, 1024), (8, 5, 3, 2, 3, 64)])
 @pytest.mark.parametrize("full", [False, True])
-def test_march_bitwise_equal_band(gpu, P, nex, ney, eb, ee, wg, full, monkeypatch):
+def test_march_bitwise_equal_band(gpu, P, nex, ney, eb, ee, wg, full, tuning):
     """The marching kernel (LDS ring of staged lines, chunks of element positions per workgroup)
     reproduces the band kernel bitwise: strips, chunk boundaries, ghost positions, and the
     FULL path (extra pairs, accumulate, explicit Dirichlet mask and values)."""
@@ -232,10 +233,10 @@ def test_march_bitwise_equal_band(gpu, P, nex, ney, eb, ee, wg, full, monkeypatc
         kw.update(c_extra=3.0, ea=A, eb=B, c_acc=2.0, dir_mode=_lib.DIR_IDENTITY, dir_mask=mask, dir_val=G)
     else:
         kw.update(dir_mode=_lib.DIR_IDENTITY, dir_sides=_lib.SIDE_W | _lib.SIDE_E | _lib.SIDE_N)
-    monkeypatch.setenv("SEM_MARCH_WG", str(wg))
+    tuning(_lib.TUNE_MARCH_WG, wg)
     outs = {}
     for name in ("4imm", "4m", "4mdpp"):
-        monkeypatch.setenv("SEM_BAND_TILE", BAND_VARIANTS[name])
+        tuning(_lib.TUNE_BAND_TILE, BAND_VARIANTS[name])
         outs[name] = mesh.apply(X, Y0.clone(), **kw)
     assert torch.equal(outs["4m"], outs["4imm"])
     assert torch.equal(outs["4mdpp"], outs["4imm"])

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(_lib.exported_symbols()) == declared
-    assert lib.sem_abi_version() == 1
+    assert lib.sem_abi_version() == _lib.ABI_VERSION == 2
     assert lib.sem_max_order() == 16
 
 
@@ -104,3 +104,38 @@ def test_abi_error_paths_without_gpu():
     assert lib.sem_apply(None, None, None, None, None) == _lib.SEM_EINVAL
     with pytest.raises(ValueError):
         _lib.check(_lib.SEM_EINVAL)
+
+
+def test_release_build_has_no_diagnostic_path():
+    """no environment variable can change results.  The shipped library is built with
+    SEM_DIAGNOSTICS=0 (the SEM_DIAG ablation bits and stamp buffer are compiled out) and its build
+    id matches the in-tree sources."""
+    from sem_amd.build import source_hash
+    lib = _lib.load()
+    bid = lib.sem_build_id().decode()
+    assert bid == source_hash() and not bid.endswith("+diag")
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"SEM_DIAG" not in blob
+
+
+def test_tuning_knobs_set_and_get():
+    lib = _lib.load()
+    v = C.c_int()
+    _lib.check(lib.sem_get_tuning(_lib.TUNE_BAND_TILE, C.byref(v)))
+    old = v.value
+    _lib.check(lib.sem_set_tuning(_lib.TUNE_BAND_TILE, 3))
+    _lib.check(lib.sem_get_tuning(_lib.TUNE_BAND_TILE, C.byref(v)))
+    assert v.value == 3
+    _lib.check(lib.sem_set_tuning(_lib.TUNE_BAND_TILE, old))
+    assert lib.sem_set_tuning(99, 1) == _lib.SEM_EINVAL
+    assert lib.sem_get_tuning(-1, C.byref(v)) == _lib.SEM_EINVAL
+
+
+def test_loader_refuses_library_from_other_sources(monkeypatch):
+    """A library whose build id differs from the in-tree source hash is refused (a stale .so
+    would make the GPU tests validate old kernels)."""
+    from sem_amd import build
+    lib = _lib.load()
+    monkeypatch.setattr(build, "source_hash", lambda: "0" * 16)
+    with pytest.raises(RuntimeError, match="not built from the sources"):
+        _lib._check_build_id(lib)

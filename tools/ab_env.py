@@ -1,4 +1,5 @@
-"""In-process A/B of a per-call tuning variable of libsemops (SEM_BAND_TILE, SEM_BAND_CPOL).
+"""In-process A/B of a libsemops kernel-selection knob (include/sem_ops.h enum sem_tune), set
+through sem_set_tuning between captures (the library reads the environment only once).
 
 python tools/ab_env.py --var SEM_BAND_CPOL --values 0,1,3 [--meshes 8:64,8:1024] [--rounds 5]
 Each round times every value once (graph-replayed back-to-back CD applies, HIP events), so
@@ -27,6 +28,10 @@ def main():
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     vals = args.values.split(",")
+    lib = _lib.load()
+    knob = {"SEM_BAND_TILE": _lib.TUNE_BAND_TILE, "SEM_BAND_CPOL": _lib.TUNE_BAND_CPOL, "SEM_BAND_KP": _lib.TUNE_BAND_KP,
+            "SEM_MARCH_WG": _lib.TUNE_MARCH_WG, "SEM_MFMA_TILE": _lib.TUNE_MFMA_TILE,
+            "SEM_COL_TILE": _lib.TUNE_COL_TILE}[args.var]
     for spec in args.meshes.split(","):
         P, ne = (int(a) for a in spec.split(":"))
         mesh = get_mesh(P, ne, ne, 1.0 / ne, 1.0 / ne)
@@ -41,7 +46,10 @@ def main():
         res = {v_: [] for v_ in vals}
         for _ in range(args.rounds):
             for v_ in vals:
-                os.environ[args.var] = v_
+                val = int(v_)
+                if knob == _lib.TUNE_BAND_KP:   # SEM_BAND_KP=0 means struct-only arguments (knob value -1)
+                    val = -1 if val == 0 else 0
+                _lib.check(lib.sem_set_tuning(knob, val))
                 res[v_].append(time_graph(lambda: mesh.apply(T, y, **kw), reps))
                 if ref is None:
                     ref = y.clone()
@@ -51,7 +59,7 @@ def main():
             med, mn = statistics.median(res[v_]), min(res[v_])
             print(f"P={P:2d} ne={ne:5d} N={N:9d} {args.var}={v_:>5s}: median {med:9.2f} us  min {mn:9.2f} us  "
                   f"{32.0 * N / med / 1e3:8.1f} GB/s", flush=True)
-        os.environ.pop(args.var, None)
+        _lib.check(lib.sem_set_tuning(knob, 0))
 
 
 if __name__ == "__main__":
