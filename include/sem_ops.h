@@ -211,6 +211,33 @@ int sem_basis_dot2(const double* V, int64_t ldv, int k, int64_t n, const double*
                    double* out, void* stream);
 int sem_basis_update(const double* V, int64_t ldv, int k, int64_t n, const double* c, double* w, void* stream);
 
+/* ---- Navier-Stokes velocity Jacobian (device direct solve) --------------- */
+/* Replaces the host-side materialisation of the 2N x 2N velocity Jacobian for SuperLU
+ * (NavierStokes_Solver.py:176-184: sp_sparse.bmat of the four Jacobian blocks, Dirichlet rows
+ * set to identity, splu).  The Jacobian
+ *     J_uu = A + diag(juu), J_uv = diag(juv), J_vu = diag(jvu), J_vv = A + diag(jvv),
+ *     A = c_mass M + c_stiff K + c_gradx diag(cu) G_x + c_grady diag(cv) G_y
+ * (Sys = K + Re(u@C_x + v@C_y), :106; Jacobians :131-136) is written as the pieces of its static
+ * condensation over node lines (see sem_amd/csrc/ns_velocity.hip for the layout): dense
+ * interior blocks A_II per element column, dense interface-line blocks D, and the diagonal
+ * line-to-line couplings aIB, aBI, E, F.  Rows in the Dirichlet set (dir_mask, or dir_sides when
+ * dir_mask is NULL) are identity rows.  Whole-mesh handles only.  Sizes (doubles) from
+ * sem_velocity_block_sizes: sizes[0..5] = A_II, D, aIB, aBI, E, F. */
+typedef struct sem_velocity_desc {
+  double c_mass, c_stiff, c_gradx, c_grady;
+  const double* cu;   /* nullable = ones */
+  const double* cv;
+  const double* juu;  /* nullable = zeros */
+  const double* juv;
+  const double* jvu;
+  const double* jvv;
+  const uint8_t* dir_mask;
+  unsigned dir_sides;
+} sem_velocity_desc;
+int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes);
+int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* A_II, double* D, double* aIB, double* aBI,
+                        double* E, double* F, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,12 @@ class SemApplyDesc(C.Structure):
                 ("algo", C.c_int)]
 
 
+class SemVelocityDesc(C.Structure):
+    _fields_ = [("c_mass", C.c_double), ("c_stiff", C.c_double), ("c_gradx", C.c_double), ("c_grady", C.c_double),
+                ("cu", C.c_void_p), ("cv", C.c_void_p), ("juu", C.c_void_p), ("juv", C.c_void_p), ("jvu", C.c_void_p),
+                ("jvv", C.c_void_p), ("dir_mask", C.c_void_p), ("dir_sides", C.c_uint)]
+
+
 # name -> (restype, argtypes); mirrors include/sem_ops.h one-for-one
 _SIGS = {
     "sem_abi_version": (C.c_int, []),
@@ -69,6 +75,8 @@ _SIGS = {
     "sem_basis_dot2": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p]),
     "sem_basis_update": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sem_velocity_block_sizes": (C.c_int, [C.c_void_p, _i64p]),
+    "sem_velocity_blocks": (C.c_int, [C.c_void_p, C.POINTER(SemVelocityDesc)] + [C.c_void_p] * 7),
 }
 
 _lib = None

@@ -1,0 +1,223 @@
+// Navier-Stokes velocity-Jacobian blocks for the device direct solve (sem_amd/solvers/velocity_solve.py).
+//
+// The reference factorises the Dirichlet-row-replaced 2N x 2N velocity Jacobian
+//     [[J_uu, J_uv], [J_vu, J_vv]],  J_uu = Sys + Re diag(G_x u), J_uv = Re diag(G_y u), ...
+// with host SuperLU (NavierStokes_Solver.py:176-184) and solves with it twice per Schur-complement
+// matvec (:189-203).  Here the structured mesh is split into node lines (x-major numbering,
+// SEM.py:110): the interface lines x = L*P (L = 0..N_ex) and the P-1 interior lines of each element
+// column.  Interior lines of column e couple only to each other and to the two interface lines
+// L = e, e+1, so the Jacobian condenses statically: one dense block A_II per element column
+// (batched LU on the device), then a block-tridiagonal Schur complement over the interface lines.
+//
+// This kernel writes the pieces, one thread per Jacobian row, from the operator's tensor-product
+// form (the same algebra as the apply kernels, SEM.py:170-245):
+//   A x [gx,gy] = My[gy] sum_k (cK dy/dx Kx[gx][k] + cX cu dy/2 Gx[gx][k]) x[k][gy]
+//               + Mx[gx] sum_l (cK dx/dy Ky[gy][l] + cY cv dx/2 Gy[gy][l]) x[gx][l]
+//               + cM dx dy/4 Mx[gx] My[gy] x[gx][gy]
+// with Kx, Gx, Ky, Gy the 1-D direct-stiffness sums of the GLL tables (GLL.py:62-81) and Mx, My the
+// assembled GLL weights.  Unknowns of one line are ordered (component c, y node gy): m = 2 NY.
+//   A_II [e][(l-1) m + c NY + gy][(l'-1) m + c' NY + gy']   interior lines l, l' = 1..P-1 (dense)
+//   D    [L][c NY + gy][c' NY + gy']                         interface line L with itself (dense)
+//   aIB  [e][l-1][s][c NY + gy]   coefficient of line e P + s P (s = 0, 1) in interior row (l, c, gy)
+//   aBI  [e][s][l-1][c NY + gy]   coefficient of interior node (l, c, gy) in row (line eP + sP, c, gy)
+//   E    [L][c NY + gy]           row on line L, column on line L+1 (same c, gy)
+//   F    [L][c NY + gy]           row on line L+1, column on line L
+// Dirichlet rows (the reference's mask_bound) are identity rows: 1 on the diagonal, 0 elsewhere,
+// in every piece.  The dense blocks are zero-filled by the caller (hipMemsetAsync); each row is
+// written by exactly one thread, so nothing races.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "sem_internal.h"
+
+namespace sem {
+
+struct VelocityArgs {
+  const double* tab;  // K_s | G_s | w (handle table)
+  const double *cu, *cv, *juu, *juv, *jvu, *jvv;
+  const uint8_t* mask;
+  double fKx, fKy, fM, fX, fY;  // cK dy/dx, cK dx/dy, cM dx dy/4, cX dy/2, cY dx/2
+  int P, nex, ney, NY, NX;
+  unsigned sides;
+  double *AII, *D, *aIB, *aBI, *E, *F;
+};
+
+__device__ __forceinline__ bool is_dirichlet(const VelocityArgs& a, int gx, int gy) {
+  if (a.mask) return a.mask[static_cast<int64_t>(gx) * a.NY + gy] != 0;
+  return ((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
+         ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1);
+}
+
+// One thread per Jacobian row: row = line gx (0..NX-1), component c, node gy.
+__global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs a) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int NY = a.NY, P = a.P, n = P + 1, m = 2 * NY;
+  if (t >= static_cast<int64_t>(a.NX) * m) return;
+  const int gx = static_cast<int>(t / m), r = static_cast<int>(t - static_cast<int64_t>(gx) * m);
+  const int c = r / NY, gy = r - c * NY;
+  const double* Ks = a.tab;
+  const double* Gs = a.tab + n * n;
+  const double* w = a.tab + 2 * n * n;
+  const int L = gx / P, l = gx - L * P;  // interface line L (l == 0) or interior line l of column L
+  const int64_t node = static_cast<int64_t>(gx) * NY + gy;
+  const bool dir = is_dirichlet(a, gx, gy);
+  const int nI = (P - 1) * m;
+  // row pointer into the dense block holding this row, and the column offset of line-local node 0
+  double* row;
+  int64_t col0;  // column index of (this line, c = 0, gy = 0) within the block
+  if (l == 0) {
+    row = a.D + (static_cast<int64_t>(L) * m + r) * m;
+    col0 = 0;
+  } else {
+    row = a.AII + (static_cast<int64_t>(L) * nI + (l - 1) * m + r) * nI;
+    col0 = static_cast<int64_t>(l - 1) * m;
+  }
+  const int64_t self = col0 + r;
+  if (dir) {  // identity row: no coupling to anything else
+    row[self] = 1.0;
+    if (l == 0) {
+      if (L < a.nex) {
+        a.E[static_cast<int64_t>(L) * m + r] = 0.0;
+        for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L) * 2 + 0) * (P - 1) + k - 1) * m + r] = 0.0;
+      }
+      if (L > 0) {
+        a.F[static_cast<int64_t>(L - 1) * m + r] = 0.0;
+        for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L - 1) * 2 + 1) * (P - 1) + k - 1) * m + r] = 0.0;
+      }
+    } else {
+      for (int s = 0; s < 2; ++s) a.aIB[((static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 + s) * m + r] = 0.0;
+    }
+    return;
+  }
+  // assembled weights of this node's line (x) and column (y)
+  const double mx = l != 0 ? w[l] : (L > 0 ? w[P] : 0.0) + (L < a.nex ? w[0] : 0.0);
+  const int ey = gy / P, j = gy - ey * P;
+  const double my = j != 0 ? w[j] : (ey > 0 ? w[P] : 0.0) + (ey < a.ney ? w[0] : 0.0);
+  const double cu = a.cu ? a.cu[node] : 1.0, cv = a.cv ? a.cv[node] : 1.0;
+  const double fx = a.fKx * my, gxc = a.fX * cu * my;  // x rows: fx Ks[.][.] + gxc Gs[.][.]
+  const double fy = a.fKy * mx, gyc = a.fY * cv * mx;  // y rows: fy Ks[.][.] + gyc Gs[.][.]
+  auto xk = [&](int i, int k) { return fx * Ks[i * n + k] + gxc * Gs[i * n + k]; };
+  auto yk = [&](int i, int k) { return fy * Ks[i * n + k] + gyc * Gs[i * n + k]; };
+
+  // diagonal: x part + y part + mass + the Jacobian's own diagonal term
+  double dg = a.fM * mx * my + (c == 0 ? (a.juu ? a.juu[node] : 0.0) : (a.jvv ? a.jvv[node] : 0.0));
+  if (l != 0) {
+    dg += xk(l, l);
+  } else {
+    if (L > 0) dg += xk(P, P);
+    if (L < a.nex) dg += xk(0, 0);
+  }
+  // y coupling along the line (same component): elements ey-1 (row P) and ey (row j)
+  const int64_t yb = col0 + static_cast<int64_t>(c) * NY;  // column of (this line, c, gy = 0)
+  if (j != 0) {
+    for (int k = 0; k <= P; ++k) {
+      const double v = yk(j, k);
+      if (k == j) dg += v; else row[yb + ey * P + k] += v;
+    }
+  } else {
+    if (ey > 0)
+      for (int k = 0; k <= P; ++k) {
+        const double v = yk(P, k);
+        if (k == P) dg += v; else row[yb + (ey - 1) * P + k] += v;
+      }
+    if (ey < a.ney)
+      for (int k = 0; k <= P; ++k) {
+        const double v = yk(0, k);
+        if (k == 0) dg += v; else row[yb + ey * P + k] += v;
+      }
+  }
+  row[self] += dg;
+  // the other component at the same node: J_uv = diag(juv) (u rows), J_vu = diag(jvu) (v rows)
+  const double* jc = c == 0 ? a.juv : a.jvu;
+  if (jc) row[col0 + (1 - c) * NY + gy] = jc[node];
+
+  // x coupling to the other lines of this node's element column(s)
+  if (l != 0) {
+    double* AIIrow = row;
+    for (int k = 1; k < P; ++k)
+      if (k != l) AIIrow[static_cast<int64_t>(k - 1) * m + r] = xk(l, k);
+    for (int s = 0; s < 2; ++s) a.aIB[((static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 + s) * m + r] = xk(l, s * P);
+  } else {
+    if (L < a.nex) {  // left line of column L
+      for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L) * 2 + 0) * (P - 1) + k - 1) * m + r] = xk(0, k);
+      a.E[static_cast<int64_t>(L) * m + r] = xk(0, P);
+    }
+    if (L > 0) {  // right line of column L-1
+      for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L - 1) * 2 + 1) * (P - 1) + k - 1) * m + r] = xk(P, k);
+      a.F[static_cast<int64_t>(L - 1) * m + r] = xk(P, 0);
+    }
+  }
+}
+
+static int hip_check_v(hipError_t e, const char* what) {
+  if (e == hipSuccess) return SEM_OK;
+  return set_error(SEM_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace sem
+
+extern "C" {
+
+int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes) {
+  if (!h || !sizes) return sem::set_error(SEM_EINVAL, "null argument");
+  if (h->ex_begin != 0 || h->ex_end != h->nex)
+    return sem::set_error(SEM_EUNSUPPORTED, "the velocity blocks need a whole-mesh handle");
+  const int64_t m = 2 * h->NY, nI = static_cast<int64_t>(h->P - 1) * m, ne = h->nex;
+  sizes[0] = ne * nI * nI;             // A_II
+  sizes[1] = (ne + 1) * m * m;         // D
+  sizes[2] = ne * (h->P - 1) * 2 * m;  // aIB
+  sizes[3] = ne * 2 * (h->P - 1) * m;  // aBI
+  sizes[4] = ne * m;                   // E
+  sizes[5] = ne * m;                   // F
+  return SEM_OK;
+}
+
+int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, double* D, double* aIB, double* aBI,
+                        double* E, double* F, void* stream) {
+  if (!h || !d || !D || !E || !F) return sem::set_error(SEM_EINVAL, "null argument");
+  if (h->P > 1 && (!AII || !aIB || !aBI)) return sem::set_error(SEM_EINVAL, "null interior block");
+  if (h->ex_begin != 0 || h->ex_end != h->nex)
+    return sem::set_error(SEM_EUNSUPPORTED, "the velocity blocks need a whole-mesh handle");
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != h->device)
+    return sem::set_error(SEM_EINVAL, "handle belongs to another device than the current one");
+  int64_t sz[6];
+  sem_velocity_block_sizes(h, sz);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int st;
+  if (h->P > 1 && (st = sem::hip_check_v(hipMemsetAsync(AII, 0, sz[0] * sizeof(double), s), "memset A_II")))
+    return st;
+  if ((st = sem::hip_check_v(hipMemsetAsync(D, 0, sz[1] * sizeof(double), s), "memset D"))) return st;
+  sem::VelocityArgs a{};
+  a.tab = h->d_tab;
+  a.cu = d->cu;
+  a.cv = d->cv;
+  a.juu = d->juu;
+  a.juv = d->juv;
+  a.jvu = d->jvu;
+  a.jvv = d->jvv;
+  a.mask = d->dir_mask;
+  a.sides = d->dir_sides;
+  a.fKx = d->c_stiff * (h->dy / h->dx);
+  a.fKy = d->c_stiff * (h->dx / h->dy);
+  a.fM = d->c_mass * ((h->dx / 2.0) * (h->dy / 2.0));
+  a.fX = d->c_gradx * (h->dy / 2.0);
+  a.fY = d->c_grady * (h->dx / 2.0);
+  a.P = h->P;
+  a.nex = h->nex;
+  a.ney = h->ney;
+  a.NY = static_cast<int>(h->NY);
+  a.NX = static_cast<int>(h->NX);
+  a.AII = AII;
+  a.D = D;
+  a.aIB = aIB;
+  a.aBI = aBI;
+  a.E = E;
+  a.F = F;
+  const int64_t rows = h->NX * 2 * h->NY;
+  hipLaunchKernelGGL(sem::velocity_blocks_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)), dim3(256), 0, s, a);
+  return sem::hip_check_v(hipGetLastError(), "velocity blocks launch");
+}
+
+}  // extern "C"

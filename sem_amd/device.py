@@ -134,6 +134,28 @@ class Mesh:
         _lib.check(self._lib.sem_interface_unpack(self._h, _ptr(buf), b, len(bounds) - 1, _ptr(y),
                                                   self.stream_ptr(stream)))
 
+    def velocity_blocks(self, blocks, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None, cv=None,
+                        juu=None, juv=None, jvu=None, jvv=None, dir_mask=None, dir_sides=0, stream=None):
+        """Static-condensation pieces of the NS velocity Jacobian (include/sem_ops.h,
+        sem_velocity_blocks) into `blocks` (VelocityJacobianSolver.empty_blocks layout)."""
+        for nm, t in (("cu", cu), ("cv", cv), ("juu", juu), ("juv", juv), ("jvu", jvu), ("jvv", jvv)):
+            self._vec(t, nm)
+        if dir_mask is not None and (dir_mask.dtype != torch.uint8 or dir_mask.numel() != self.n_local):
+            raise ValueError("dir_mask must be a uint8 tensor of n_local entries")
+        sizes = (C.c_int64 * 6)()
+        _lib.check(self._lib.sem_velocity_block_sizes(self._h, sizes))
+        names = ("AII", "D", "aIB", "aBI", "E", "F")
+        for nm, sz in zip(names, sizes):
+            t = blocks.get(nm)
+            if sz and (t is None or t.numel() != sz or t.dtype != torch.float64 or t.device != self.device
+                       or not t.is_contiguous()):
+                raise ValueError(f"block {nm} must be a contiguous float64 tensor of {sz} entries on {self.device}")
+        d = _lib.SemVelocityDesc(float(c_mass), float(c_stiff), float(c_gradx), float(c_grady), _ptr(cu), _ptr(cv),
+                                 _ptr(juu), _ptr(juv), _ptr(jvu), _ptr(jvv), _ptr(dir_mask), int(dir_sides))
+        _lib.check(self._lib.sem_velocity_blocks(self._h, C.byref(d), *(_ptr(blocks.get(nm)) for nm in names),
+                                                 self.stream_ptr(stream)))
+        return blocks
+
     # ------------------------------------------------------------------ host-side 1-D tables
     def weights_1d(self):
         """Assembled 1-D GLL weights over the locally held lines (x) and all columns (y)."""

@@ -10,29 +10,32 @@ the GPU as fused launches:
   * `_calc_jacobians` (:123-136): Re diag(G_x u) ... as closed-form operators.
   * `_get_dresiduals` (:138-160): the velocity Jacobian blocks applied matrix-free.
 
-`_get_update` keeps the reference's algorithm: the 2N x 2N velocity Jacobian is
-materialised (`.tocsr()`) and factorised with SuperLU on the host, and the
-pressure Schur complement is solved by LGMRES with the mass-diagonal
-preconditioner (NavierStokes_Solver.py:162-236).  Replacing the direct solver is
-a later step.
+`_get_update` keeps the reference's algorithm -- a direct velocity solve inside a pressure
+Schur-complement Krylov solve with the mass-diagonal preconditioner (NavierStokes_Solver.py:162-236)
+-- entirely on the device: the velocity Jacobian is factored by static condensation over node
+lines (sem_amd/solvers/velocity_solve.py, blocks written by the sem_velocity_blocks HIP kernel)
+instead of host SuperLU, and the Schur system runs the device GMRES.  No CSR matrix is formed.
 """
 import time
 
 import numpy as np
-import scipy.sparse as sp_sparse
-import scipy.sparse.linalg as linalg
 import torch
 
 from .. import SEM, _lib
 from ..device import get_mesh
+from ..krylov import gmres
 from .convection_diffusion import DirichletRows
+from .velocity_solve import VelocityJacobianSolver
 
 
 class NavierStokesSolver:
     def __init__(self, L_x: float, L_y: float, Re: float, Gr: float, P: int, N_ex: int, N_ey: int,
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
-                 mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter']):  # noqa: B006
+                 mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
+                 max_basis: int = 3000):
         self._iprint = iprint
+        self._max_basis = max_basis
+        self._velo = None
         self._Re, self._Gr = Re, Gr
         if self._Re == 0 and self._Gr != 0:
             raise ValueError('Cannot have Re == 0 and Gr != 0')
@@ -73,7 +76,9 @@ class NavierStokesSolver:
         self._dval_u = m.to_device(np.where(self._mask_bound, du, 0.0))
         self._dval_v = m.to_device(np.where(self._mask_bound, dv, 0.0))
         self._pidx = torch.as_tensor(np.nonzero(self._mask_dir_p)[0], device=m.device)
+        self._pin_on_boundary = bool(self._mask_bound[self._mask_dir_p].any())
         self._dval_p = m.to_device(np.where(self._mask_dir_p, dpp, 0.0))
+        self._Mdiag = m.to_device(self._M.diagonal())
 
     # ------------------------------------------------------------------ helpers
     def _dev(self, a):
@@ -97,7 +102,7 @@ class NavierStokesSolver:
         r = m.apply(v, r, c_grady=1.0, c_acc=1.0, dir_mode=_lib.DIR_REPLACE, dir_val=kp, **self._dir.kw())
         if pdir is None:
             r[self._pidx] = p[self._pidx]
-        elif not self._mask_bound[self._pidx.item()]:
+        elif not self._pin_on_boundary:
             r[self._pidx] = p[self._pidx] - pdir[self._pidx]
         return r
 
@@ -127,7 +132,7 @@ class NavierStokesSolver:
         self._Jac_v_v = self._Sys + Re * SEM.tensordot(self._C_y, V, (2, 0))
         self._Jac_u_v = Re * SEM.tensordot(self._C_y, U, (2, 0))
         self._Jac_v_u = Re * SEM.tensordot(self._C_x, V, (2, 0))
-        self._velo_lu = None  # factorised on first use, reused until the next linearisation
+        self._velo = None  # factorised on first use, reused until the next linearisation
 
     def _get_dresiduals(self, du, dv, dp, dT=None):
         """NavierStokes_Solver.py:138-160."""
@@ -152,94 +157,102 @@ class NavierStokesSolver:
         rc = self._continuity(DU, DV, DP)
         return self._out(ru, du), self._out(rv, du), self._out(rc, du)
 
-    def _velo_factor(self):
-        """SuperLU of the Dirichlet-row-replaced velocity Jacobian (NavierStokes_Solver.py:176-183).
-        The reference refactorises on every _get_update call; the factor depends only on the
-        Jacobians, so it is kept until _calc_jacobians runs again (the Boussinesq coupler's
-        block-Jacobi preconditioner calls _get_update once per Krylov iteration)."""
-        if getattr(self, "_velo_lu", None) is not None:
-            return self._velo_lu
+    def _velocity_solver(self):
+        """Device factorisation of the Dirichlet-row-replaced velocity Jacobian -- the reference's
+        `bmat` + `splu` (NavierStokes_Solver.py:176-184) -- by static condensation over node lines
+        (sem_amd/solvers/velocity_solve.py).  The reference refactorises on every _get_update call;
+        the factor depends only on the Jacobians, so it is kept until _calc_jacobians runs again (the
+        Boussinesq coupler's block-Jacobi preconditioner calls _get_update once per Krylov iteration)."""
+        if self._velo is not None:
+            return self._velo
         tStart = time.perf_counter()
-        mask = np.hstack((self._mask_bound,) * 2)
-        Jac_velo = sp_sparse.bmat([[self._Jac_u_u.tocsr(), self._Jac_u_v.tocsr()],
-                                   [self._Jac_v_u.tocsr(), self._Jac_v_v.tocsr()]], format='lil')
-        Jac_velo[mask, :] = 0
-        Jac_velo[mask, mask] = 1
-        Jac_velo = Jac_velo.tocsc()
-        self._velo_lu = linalg.splu(Jac_velo)
+        m = self._mesh
+        vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device)
+        blocks = vs.empty_blocks()
+        kw = self._sys_kw(self._Sys)
+        m.velocity_blocks(blocks, juu=self._Jac_u_u._coeffs()[4], juv=self._Jac_u_v._coeffs()[4],
+                          jvu=self._Jac_v_u._coeffs()[4], jvv=self._Jac_v_v._coeffs()[4],
+                          dir_mask=self._dir.mask, dir_sides=self._dir.sides, **kw)
+        vs.factor(blocks.pop("AII"), **blocks)
+        self._velo = vs
         if 'LU_suc' in self._iprint:
-            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec '
-                  f'with fill factor {self._velo_lu.nnz/Jac_velo.nnz:0.1f}')
-        return self._velo_lu
+            torch.cuda.synchronize(m.device)
+            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec (device static condensation)')
+        return vs
 
     def _get_update(self, dres_u, dres_v, dres_cont, du0=None, dv0=None, dp0=None):
-        """Velocity LU + pressure Schur LGMRES (NavierStokes_Solver.py:162-236)."""
-        host = lambda a: a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)  # noqa: E731
-        dres_u, dres_v, dres_cont = host(dres_u), host(dres_v), host(dres_cont)
-        Jac_velo_lu = self._velo_factor()
-
-        def solve_jac_velo(a, b):
-            return np.split(Jac_velo_lu.solve(np.hstack((a, b))), 2)
-
-        Z = np.zeros(self.N)
-        b_schur = dres_cont - self._get_dresiduals(*solve_jac_velo(dres_u, dres_v), Z)[2]
+        """Velocity solve + pressure Schur-complement Krylov solve (NavierStokes_Solver.py:162-236), on
+        the device: the velocity Jacobian is factored once per linearisation (_velocity_solver) and the
+        Schur system is solved by the device GMRES (sem_amd/krylov.py) with the reference's
+        mass-diagonal preconditioner (:208-212) and stopping rule ||r||_2 <= mtol sqrt(N) (:222-224)."""
+        vs = self._velocity_solver()
+        ru, rv, rc = self._dev(dres_u), self._dev(dres_v), self._dev(dres_cont)
+        Z = torch.zeros(self.N, dtype=torch.float64, device=self._mesh.device)
+        b_schur = rc - self._get_dresiduals(*vs.solve(ru, rv), Z)[2]
+        count = [0]
 
         def schur_mv(dp):
-            schur_mv.fCount += 1
-            f_x, f_y = solve_jac_velo(*self._get_dresiduals(Z, Z, np.ascontiguousarray(dp).ravel())[:2])
-            return self._get_dresiduals(-f_x, -f_y, np.ascontiguousarray(dp).ravel())[2]
+            count[0] += 1
+            f_x, f_y = vs.solve(*self._get_dresiduals(Z, Z, dp)[:2])
+            return self._get_dresiduals(-f_x, -f_y, dp)[2]
 
-        schur_mv.fCount = 0
-        schur_LO = linalg.LinearOperator((self.N,) * 2, schur_mv, dtype=float)
-        Mdiag = self._M.diagonal()
+        mp = self._pidx
 
-        def precon_mv(c):
-            z = c / Mdiag
-            z[self._mask_dir_p] = c[self._mask_dir_p]
+        def precon(c):
+            z = c / self._Mdiag
+            z[mp] = c[mp]
             return z
 
-        precon_LO = linalg.LinearOperator((self.N,) * 2, precon_mv, dtype=float)
+        it = [0]
 
-        def print_res(xk):
-            print_res.iterCount += 1
+        def cb(est):
+            it[0] += 1
             if 'LGMRES_iter' in self._iprint:
-                print(f'NavierStokes LGMRES: {print_res.iterCount}\t{np.linalg.norm(schur_LO.matvec(xk) - b_schur)}')
+                print(f'NavierStokes GMRES: {it[0]}\t{est}')
 
-        print_res.iterCount = 0
-        dp, info = linalg.lgmres(A=schur_LO, b=b_schur, M=precon_LO, x0=dp0, atol=self._mtol * np.sqrt(self.N),
-                                 rtol=0, inner_m=int(self.N * 0.3), callback=print_res)
-        if info != 0:
-            raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {info} iterations')
+        r = gmres(schur_mv, b_schur, x0=self._dev(dp0), atol=self._mtol * np.sqrt(self.N), rtol=0.0,
+                  restart=max(1, min(int(self.N * 0.3), self._max_basis)), precond=precon, callback=cb)
+        if r.info != 0:
+            raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {r.info} iterations')
+        dp = r.x
+        self.schur_matvecs = count[0]
         if 'LGMRES_suc' in self._iprint:
-            res = np.linalg.norm(schur_LO.matvec(dp) - b_schur, ord=np.inf)
-            print(f'NavierStokes LGMRES: Converged in {schur_mv.fCount} evaluations with max-norm {res}')
+            res = (schur_mv(dp) - b_schur).abs().max().item()
+            print(f'NavierStokes GMRES: Converged in {count[0]} evaluations with max-norm {res}')
         b_u, b_v = self._get_dresiduals(Z, Z, dp)[:2]
-        du, dv = solve_jac_velo(dres_u - b_u, dres_v - b_v)
-        return du, dv, dp
+        du, dv = vs.solve(ru - b_u, rv - b_v)
+        return self._out(du, dres_u), self._out(dv, dres_u), self._out(dp, dres_u)
 
     def _get_solution(self, T, u0=None, v0=None, p0=None):
-        """Newton iteration (NavierStokes_Solver.py:238-270)."""
-        u = u0 if u0 is not None else np.zeros(self.N)
-        v = v0 if v0 is not None else np.zeros(self.N)
-        p = p0 if p0 is not None else np.zeros(self.N)
+        """Newton iteration (NavierStokes_Solver.py:238-270), iterates kept on the device; NumPy in,
+        NumPy out (device tensors in, device tensors out)."""
+        like = T
+        Z = torch.zeros(self.N, dtype=torch.float64, device=self._mesh.device)
+        u = self._dev(u0) if u0 is not None else Z.clone()
+        v = self._dev(v0) if v0 is not None else Z.clone()
+        p = self._dev(p0) if p0 is not None else Z.clone()
+        T = self._dev(T)
         self._k = 0
+        self.newton_history = []
         while True:
             res_u, res_v, res_cont = self._get_residuals(u, v, p, T)
-            norm = np.linalg.norm((res_u, res_v, res_cont), ord=2)
+            norm = torch.sqrt(res_u.square().sum() + res_v.square().sum() + res_cont.square().sum()).item()
             if 'NEWTON_iter' in self._iprint:
                 print(f'NavierStokes NEWTON: {self._k}\t{norm}')
             if norm <= self._mtol_newton * np.sqrt(self.N * 3):
+                self.newton_history.append((norm, 0))
                 if 'NEWTON_suc' in self._iprint:
-                    print(f'NavierStokes NEWTON: Converged in {self._k} iterations'
-                          f' with max-norm {np.linalg.norm((res_u, res_v, res_cont), ord=np.inf)}')
+                    mx = max(res_u.abs().max().item(), res_v.abs().max().item(), res_cont.abs().max().item())
+                    print(f'NavierStokes NEWTON: Converged in {self._k} iterations with max-norm {mx}')
                 break
             self._calc_jacobians(u, v)
             du, dv, dp = self._get_update(-res_u, -res_v, -res_cont)
+            self.newton_history.append((norm, self.schur_matvecs))
             u = u + du
             v = v + dv
             p = p + dp
             self._k += 1
-        return u, v, p
+        return self._out(u, like), self._out(v, like), self._out(p, like)
 
     def _get_vector(self, f_func):
         return f_func(self.points[0], self.points[1])

@@ -282,8 +282,37 @@ def gen_boussinesq(CDS, NSS):
     np.savez_compressed(os.path.join(OUT, "bous.npz"), **d)
 
 
+def gen_cfg5(SEM):
+    """Full-size cfg5 (128x128, P=12, N=2,362,369) operator checksums from the reference's own
+    assembled matrices (SEM.global_{stiffness,mass,gradient}_matrices, SEM.py:170-223).  The
+    reference's 8-D convection tensor is infeasible at this size (~632 GB); the
+    convection contraction enters through the identity tensordot(C_x, u, (1,0)) = diag(u) G_x,
+    pinned against the reference's own COO triplets at small sizes (matrices.npz)."""
+    d = {}
+    P, ne = 12, 128
+    dx = dy = 1.0 / ne
+    K = SEM.global_stiffness_matrix(P, ne, ne, dx, dy)
+    M = SEM.global_mass_matrix(P, ne, ne, dx, dy)
+    Gx, Gy = SEM.global_gradient_matrices(P, ne, ne, dx, dy)
+    N = K.shape[0]
+    T, u, v = rng_fields(N)
+    KT = K @ T
+    SysT = KT + 40.0 * (u * (Gx @ T) + v * (Gy @ T))
+    d["N"] = np.array(N)
+    d["nnz_K"], d["nnz_Gx"], d["nnz_M"] = np.array(K.nnz), np.array(Gx.nnz), np.array(M.nnz)
+    d["norm_KT"], d["norm_SysT"] = np.array(np.linalg.norm(KT)), np.array(np.linalg.norm(SysT))
+    d["norm_MT"] = np.array(np.linalg.norm(M @ T))
+    d["sample_idx"] = np.arange(0, N, 997)
+    d["sample_KT"], d["sample_SysT"], d["sample_MT"] = KT[::997], SysT[::997], (M @ T)[::997]
+    np.savez_compressed(os.path.join(OUT, "cfg5_checksums.npz"), **d)
+
+
 def main():
     install_adapters()
+    if "--only" in sys.argv:   # regenerate one fixture: --only cfg5
+        from Solvers import SEM
+        {"cfg5": gen_cfg5}[sys.argv[sys.argv.index("--only") + 1]](SEM)
+        return
     from Solvers import GLL, SEM
     from Solvers.ConvectionDiffusion_Solver import ConvectionDiffusionSolver
     from Solvers.NavierStokes_Solver import NavierStokesSolver
@@ -293,6 +322,7 @@ def main():
     gen_cd(ConvectionDiffusionSolver)
     gen_ns(NavierStokesSolver)
     gen_checksums(SEM)
+    gen_cfg5(SEM)
     gen_boussinesq(ConvectionDiffusionSolver, NavierStokesSolver)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):

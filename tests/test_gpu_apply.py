@@ -275,6 +275,34 @@ def test_cfg2_checksums_full_size(gpu):
     assert rel((M @ T)[g["sample_idx"]], g["sample_MT"]) < TOL
 
 
+def test_cfg5_checksums_full_size(gpu):
+    """cfg5 (128x128, P=12, N=2,362,369) against norms / strided samples of the reference's own
+    assembled K, M, G_x, G_y (tests/golden/make_golden.py gen_cfg5), through the fused kernel."""
+    from sem_amd import _lib
+    from sem_amd.device import get_mesh
+    g = golden("cfg5_checksums.npz")
+    N = int(g["N"])
+    r = np.random.default_rng(2024)
+    T, u, v = r.uniform(-1, 1, N), r.uniform(-1, 1, N), r.uniform(-1, 1, N)
+    d = 1.0 / 128
+    mesh = get_mesh(12, 128, 128, d, d)
+    assert mesh.n_local == N
+    Td, Ud, Vd = (mesh.to_device(a) for a in (T, u, v))
+    KT = mesh.apply(Td, c_stiff=1.0).cpu().numpy()
+    ST = mesh.apply(Td, c_stiff=1.0, c_gradx=40.0, cu=Ud, c_grady=40.0, cv=Vd).cpu().numpy()
+    MT = mesh.apply(Td, c_mass=1.0).cpu().numpy()
+    for y, nk, sk in ((KT, "norm_KT", "sample_KT"), (ST, "norm_SysT", "sample_SysT"), (MT, "norm_MT", "sample_MT")):
+        assert abs(np.linalg.norm(y) - float(g[nk])) < 1e-12 * float(g[nk]), nk
+        assert rel(y[g["sample_idx"]], g[sk]) < TOL, sk
+    # the bench's Dirichlet W/E identity rows on the same operator
+    NY = 128 * 12 + 1
+    yd = mesh.apply(Td, c_stiff=1.0, c_gradx=40.0, cu=Ud, c_grady=40.0, cv=Vd, dir_mode=_lib.DIR_IDENTITY,
+                    dir_sides=_lib.SIDE_W | _lib.SIDE_E).cpu().numpy()
+    want = ST.copy()
+    want[:NY], want[-NY:] = T[:NY], T[-NY:]
+    assert np.array_equal(yd, want)
+
+
 @pytest.mark.parametrize("P,ne", [(12, 128), (8, 1024)])
 def test_full_size_properties(gpu, P, ne):
     """cfg5 (128^2, P=12) and the HBM-regime mesh (1024^2, P=8, N=67M): size-independent

@@ -1,0 +1,39 @@
+"""CPU tests of the velocity-Jacobian static condensation (sem_amd/solvers/velocity_solve.py):
+the pieces describe the oracle's Dirichlet-row-replaced Jacobian exactly (the line-coupling
+structure the condensation relies on), and the condensed solve reproduces SciPy's sparse solve of
+the same matrix (the reference uses SuperLU on it, NavierStokes_Solver.py:176-192)."""
+import numpy as np
+import pytest
+import scipy.sparse.linalg as spla
+import torch
+
+from velocity_blocks import assemble, extract, oracle_velocity_jacobian
+from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
+
+CASES = [(4, 3, 2, 100.0), (2, 2, 3, 400.0), (1, 4, 3, 10.0), (6, 2, 2, 1000.0), (3, 1, 1, 1.0)]
+
+
+@pytest.mark.parametrize("P,nex,ney,Re", CASES)
+def test_pieces_describe_the_jacobian_exactly(P, nex, ney, Re):
+    ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    J = ns.Jvelo.toarray()
+    assert np.array_equal(assemble(extract(J, P, nex, ney), P, nex, ney), J)
+
+
+@pytest.mark.parametrize("P,nex,ney,Re", CASES)
+@pytest.mark.parametrize("interior", ["lu", "inverse"])
+def test_condensed_solve_matches_sparse_lu(P, nex, ney, Re, interior):
+    ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
+    vs = VelocityJacobianSolver(P, nex, ney, "cpu", interior=interior)
+    vs.factor(pcs.get("AII"), pcs["D"], pcs.get("aIB"), pcs.get("aBI"), pcs["E"], pcs["F"])
+    r = np.random.default_rng(5)
+    bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
+    xu, xv = vs.solve(torch.as_tensor(bu), torch.as_tensor(bv))
+    want = spla.spsolve(ns.Jvelo.tocsc(), np.hstack((bu, bv)))
+    got = np.hstack((xu.numpy(), xv.numpy()))
+    assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
+    # and it is a solve of J: small residual relative to |J||x|
+    J = ns.Jvelo
+    res = J @ got - np.hstack((bu, bv))
+    assert np.abs(res).max() <= 1e-11 * (abs(J).max() * np.abs(got).max())

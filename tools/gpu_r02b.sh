@@ -1,0 +1,9 @@
+set -o pipefail
+O=gpurun_out/r02b; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_abi.py tests/test_gpu_ns_velocity.py tests/test_gpu_solvers.py tests/test_gpu_boussinesq.py > $O/tests.log 2>&1; rc=$?
+tail -40 $O/tests.log | grep -v "^$" | tail -30
+[ $rc -gt 1 ] && exit $rc
+timeout -k 10 300 python -u tools/ns_solve.py --ne 8 --P 8 --Re 400 --out $O/ns8_400.json > $O/ns8_400.log 2>&1 || { tail -20 $O/ns8_400.log; exit 1; }
+tail -3 $O/ns8_400.log
+timeout -k 10 600 python -u tools/ns_solve.py --ne 16 --P 8 --Re 1000 --out $O/ns16_1000.json > $O/ns16_1000.log 2>&1 || { tail -20 $O/ns16_1000.log; exit 1; }
+tail -3 $O/ns16_1000.log
