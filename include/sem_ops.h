@@ -93,6 +93,10 @@ typedef struct sem_info {
  * NULL cu/cv mean "all ones"; an extra pair (ea,eb) or (ec,ed) is skipped when
  * either of its pointers is NULL.  c_acc != 0 reads y before overwriting it.
  * x must not alias y.
+ * On a strip handle (ex_end < N_ex) the rows of the right interface line x = ex_end*P are partial
+ * sums of the local elements; the pointwise terms (c_extra, c_acc) and Dirichlet rows of that line
+ * are left to the right-hand owner, so that the interface exchange (sum of the two strips'
+ * values) gives the assembled row.
  */
 typedef struct sem_apply_desc {
   double c_mass, c_stiff, c_gradx, c_grady;
@@ -109,6 +113,14 @@ typedef struct sem_apply_desc {
   const double* dir_val;     /* nullable */
   unsigned dir_sides;        /* SEM_SIDE_* bits used when dir_mask == NULL */
   int algo;                  /* enum sem_algo */
+  /* Element-position range [pos_begin, pos_end) of the handle's strip whose output lines are
+   * written (position p < ncols = ex_end - ex_begin covers lines (ex_begin+p)*P ..+P-1, position
+   * ncols the closing line ex_end*P); every other entry of y is left untouched.  pos_end = 0:
+   * all positions.  Each written node is the full (local) operator row, so applying the
+   * interface positions and the interior positions in separate launches gives the same y as one
+   * launch: the multi-GPU step overlaps the interface exchange with the interior launch.
+   * Band kernel only (AUTO / BAND). */
+  int pos_begin, pos_end;
 } sem_apply_desc;
 
 /* Kernel-selection knobs.  Every value selects a variant with bitwise-identical results (tile

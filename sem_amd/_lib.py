@@ -35,7 +35,7 @@ class SemApplyDesc(C.Structure):
                 ("cu", C.c_void_p), ("cv", C.c_void_p), ("c_extra", C.c_double), ("ea", C.c_void_p),
                 ("eb", C.c_void_p), ("ec", C.c_void_p), ("ed", C.c_void_p), ("c_acc", C.c_double),
                 ("dir_mode", C.c_int), ("dir_mask", C.c_void_p), ("dir_val", C.c_void_p), ("dir_sides", C.c_uint),
-                ("algo", C.c_int)]
+                ("algo", C.c_int), ("pos_begin", C.c_int), ("pos_end", C.c_int)]
 
 
 class SemVelocityDesc(C.Structure):

@@ -313,6 +313,8 @@ struct BandArgs {
   int nblk;               // grid size (gridDim would be a second, dependent kernarg fetch)
   int cpol;               // cache policy of the y stores / u,v loads (SEM_BAND_CPOL; see bstore_any)
   int mchunk;             // apply_march: element positions marched by one workgroup
+  int pos0, pos1;         // element-position range of the launch (struct-argument kernel only; the
+                          // preloaded-argument kernel always covers [0, ncols + 1))
   // FULL kernels only
   const double* ea;
   const double* eb;
@@ -356,9 +358,12 @@ template <bool FULL>
 __device__ __forceinline__ double finish_node(const BandArgs& a, const NodeOps& o, int gx, int gy, double xv,
                                               double z) {
   if constexpr (FULL) {
-    if (a.has_e1) z = fma(a.cE * o.ea, o.eb, z);
-    if (a.has_e2) z = fma(a.cE * o.ec, o.ed, z);
-    if (a.cA != 0.0) z = fma(a.cA, o.ya, z);
+    // pointwise terms are node values, not partial sums: on a strip's right interface line they
+    // are left to the right-hand owner (the exchange sums the two strips' values)
+    const bool own = !(gx == a.lb1 && a.ex_end < a.nex);
+    if (a.has_e1 && own) z = fma(a.cE * o.ea, o.eb, z);
+    if (a.has_e2 && own) z = fma(a.cE * o.ec, o.ed, z);
+    if (a.cA != 0.0 && own) z = fma(a.cA, o.ya, z);
   }
   if (a.dir_mode != SEM_DIR_NONE) {
     const bool side = ((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
@@ -436,7 +441,10 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
 
   const int lb0 = plb0, NY = pNY;
   // element positions [m0, m1) x [n0, n1); position ex_end (ney) is the ghost holding the closing line (column)
-  const int m0 = pex_begin + tx * TXE, m1 = min(m0 + TXE, pex_end + 1);
+  // KP kernels cover every position; the struct kernel may be restricted to [pos0, pos1) (the
+  // multi-GPU overlap applies the interface positions first, then the interior)
+  const int m0 = pex_begin + (KP ? 0 : a.pos0) + tx * TXE;
+  const int m1 = min(m0 + TXE, KP ? pex_end + 1 : pex_begin + a.pos1);
   const int n0 = ty * TYE, n1 = min(n0 + TYE, pney + 1);
   const int gx0 = m0 * P, gy0 = n0 * P;
   const int rows_ok = (min(m1, pex_end) - m0) * P + (m1 > pex_end ? 1 : 0);  // valid lines of the tile
@@ -991,11 +999,16 @@ template <int P, int TXE, int TYE, int NS, bool DPP = false>
 static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   using C = BCfg<P, TXE, TYE, NS>;
   const int ncols = h->ex_end - h->ex_begin;
-  const int tiles_x = (ncols + 1 + TXE - 1) / TXE;  // + the ghost position of the closing line
+  // element positions [pos0, pos1) of 0..ncols (ncols = the ghost position of the closing line)
+  const bool ranged = g.pos1 > 0;
+  const int pos0 = ranged ? g.pos0 : 0, pos1 = ranged ? g.pos1 : ncols + 1;
+  const int tiles_x = (pos1 - pos0 + TXE - 1) / TXE;
   const int tiles_y = (h->ney + 1 + TYE - 1) / TYE;
   const long long nblk = static_cast<long long>(tiles_x) * tiles_y;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
   BandArgs b{};
+  b.pos0 = pos0;
+  b.pos1 = pos1;
   b.x = g.x;
   b.y = g.y;
   b.cu = g.cu;
@@ -1035,7 +1048,7 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   const bool grad = g.cX != 0.0 || g.cY != 0.0;
   const dim3 grid(static_cast<unsigned>(nblk)), block(C::THREADS);
-  if (tune(SEM_TUNE_BAND_KP) >= 0) {  // -1 (SEM_BAND_KP=0): struct-only arguments (A/B)
+  if (tune(SEM_TUNE_BAND_KP) >= 0 && !ranged) {  // -1 (SEM_BAND_KP=0): struct-only arguments (A/B)
 #define SEM_KP_ARGS b.x, b.cu, b.cv, b.NY, b.lb0, b.ex_begin, b.ex_end, b.ney, b.nblk, b.tiles_y, b.nbytes, b
     if (full && grad)
       hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, DPP, true>), grid, block, 0, s, SEM_KP_ARGS);
@@ -1145,11 +1158,9 @@ static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStrea
     if (force == 5) return launch_band<P, 2, S::TYE, 2, true>(args, h, s);
     if (force == 6) return launch_band<P, 1, S::TYE, 1, true>(args, h, s);
   }
-  if constexpr (P == 8 || P == 12) {
-    if (force == 7) return launch_march<P, S::TYE, S::NS, false>(args, h, s);
-    if (force == 8) return launch_march<P, S::TYE, S::NS, true>(args, h, s);
-  }
-  if constexpr (P == 8 || P == 12) {
+  if constexpr (P == 8 || P == 12) {  // the marching variant covers whole strips only
+    if (force == 7 && args.pos1 == 0) return launch_march<P, S::TYE, S::NS, false>(args, h, s);
+    if (force == 8 && args.pos1 == 0) return launch_march<P, S::TYE, S::NS, true>(args, h, s);
   }
   if (force == 3) return launch_band<P, S::TXE, S::TYE, S::NS, true>(args, h, s);
   if (force == 4) return launch_band<P, S::TXE, S::TYE, S::NS, false>(args, h, s);

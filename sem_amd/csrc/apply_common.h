@@ -31,6 +31,7 @@ struct ApplyArgs {
   unsigned sides;
   int has_e1, has_e2;
   int n_local32;  // local vector length (MFMA path: < 2^31)
+  int pos0, pos1; // element-position range (band kernel; pos1 == 0: all positions)
   int diag;       // ablation bits for performance diagnosis (SEM_DIAG env); 0 in production
   unsigned long long* stamps;  // SEM_DIAG bit 8: per-wave s_memtime phase stamps (diagnostic builds only)
 };

@@ -113,9 +113,12 @@ __device__ __forceinline__ void phase_a(const ApplyArgs& a, const double* Ts, co
     if (a.cM != 0.0) z = fma(a.cM * a.hxy * weight_sum(gx, P, a.ex_begin, a.ex_end, ws) * my, xv, z);
     if (a.cX != 0.0) z = fma(a.cX * pu[i], a.hy * my * g, z);
     if (a.cY != 0.0) z = fma(a.cY * pv[i], Yg[rl * C::PY + c], z);
-    if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
-    if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
-    if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
+    // pointwise terms are node values, not partial sums: on a strip's right interface line they
+    // are left to the right-hand owner (the exchange sums the two strips' values)
+    const bool own = !(gx == a.line_end && a.ex_end < a.nex);
+    if (a.has_e1 && own) z = fma(a.cE * a.ea[p], a.eb[p], z);
+    if (a.has_e2 && own) z = fma(a.cE * a.ec[p], a.ed[p], z);
+    if (a.cA != 0.0 && own) z = fma(a.cA, a.y[p], z);
     if (a.dir_mode != SEM_DIR_NONE) {
       const bool isd = a.mask ? (a.mask[p] != 0)
                               : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
@@ -599,9 +602,10 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
         z = fma(fM * mx * my, xv, z);
         z = fma(fX * uu, my * XG, z);
         z = fma(fY * vv, mx * YG, z);
-        if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
-        if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
-        if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
+        const bool own = !(gx == lb1 && a.ex_end < a.nex);  // pointwise terms: right-hand owner only
+        if (a.has_e1 && own) z = fma(a.cE * a.ea[p], a.eb[p], z);
+        if (a.has_e2 && own) z = fma(a.cE * a.ec[p], a.ed[p], z);
+        if (a.cA != 0.0 && own) z = fma(a.cA, a.y[p], z);
         if (a.dir_mode != SEM_DIR_NONE) {
           const bool isd = a.mask ? (a.mask[p] != 0)
                                   : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
@@ -802,9 +806,10 @@ __global__ __launch_bounds__((CCfg<P, TX, BY, RS>::THREADS)) void apply_tp_col(c
       if (a.cM != 0.0) z = fma(a.cM * a.hxy * mx * my, xv, z);
       if (a.cX != 0.0) z = fma(a.cX * uval, a.hy * my * gxv, z);
       if (a.cY != 0.0) z = fma(a.cY * vval, a.hx * mx * gyv, z);
-      if (a.has_e1) z = fma(a.cE * a.ea[p], a.eb[p], z);
-      if (a.has_e2) z = fma(a.cE * a.ec[p], a.ed[p], z);
-      if (a.cA != 0.0) z = fma(a.cA, a.y[p], z);
+      const bool own = !(gx == lb1 && a.ex_end < a.nex);  // pointwise terms: right-hand owner only
+      if (a.has_e1 && own) z = fma(a.cE * a.ea[p], a.eb[p], z);
+      if (a.has_e2 && own) z = fma(a.cE * a.ec[p], a.ed[p], z);
+      if (a.cA != 0.0 && own) z = fma(a.cA, a.y[p], z);
       if (a.dir_mode != SEM_DIR_NONE) {
         const bool isd = a.mask ? (a.mask[p] != 0)
                                 : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NXg - 1) ||
@@ -1117,8 +1122,15 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   if (d->dir_mode == SEM_DIR_REPLACE && !d->dir_val) return set_error(SEM_EINVAL, "SEM_DIR_REPLACE needs dir_val");
   if (d->algo < SEM_ALGO_AUTO || d->algo > SEM_ALGO_BAND) return set_error(SEM_EINVAL, "bad algo");
   if (d->algo == SEM_ALGO_MFMA && h->P > 15) return set_error(SEM_EUNSUPPORTED, "MFMA path needs P <= 15");
+  const bool ranged = d->pos_end > 0;
+  if (ranged && (d->pos_begin < 0 || d->pos_begin >= d->pos_end || d->pos_end > h->ex_end - h->ex_begin + 1))
+    return set_error(SEM_EINVAL, "element-position range outside [0, ex_end - ex_begin + 1)");
+  if (ranged && d->algo != SEM_ALGO_AUTO && d->algo != SEM_ALGO_BAND)
+    return set_error(SEM_EUNSUPPORTED, "element-position ranges are implemented by the band kernel only");
   if (int st = on_device(h)) return st;
   ApplyArgs a{};
+  a.pos0 = ranged ? d->pos_begin : 0;
+  a.pos1 = ranged ? d->pos_end : 0;
   a.x = x;
   a.y = y;
   a.cu = d->cu;
@@ -1163,6 +1175,7 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   // the single-phase column kernel above that.
   const bool fits32 = h->n_local < (int64_t(1) << 28);
   const bool band_auto = fits32;
+  if (ranged && !fits32) return set_error(SEM_EUNSUPPORTED, "element-position ranges need n_local < 2^28");
   if (d->algo == SEM_ALGO_BAND || (d->algo == SEM_ALGO_AUTO && band_auto)) {
     if (!fits32) return set_error(SEM_EUNSUPPORTED, "band path needs n_local < 2^28");
     return launch_apply_band(a, h, s);

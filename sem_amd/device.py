@@ -79,8 +79,9 @@ class Mesh:
     # ------------------------------------------------------------------ kernels
     def apply(self, x, y=None, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None, cv=None, c_extra=0.0,
               ea=None, eb=None, ec=None, ed=None, c_acc=0.0, dir_mode=_lib.DIR_NONE, dir_mask=None, dir_val=None,
-              dir_sides=0, algo=_lib.ALGO_AUTO, stream=None):
-        """Fused operator apply (include/sem_ops.h, sem_apply)."""
+              dir_sides=0, algo=_lib.ALGO_AUTO, pos=None, stream=None):
+        """Fused operator apply (include/sem_ops.h, sem_apply).  pos = (begin, end): write only the
+        output lines of those element positions of the strip (0..ncols, ncols = closing line)."""
         x = self._vec(x, "x")
         if y is None:
             y = torch.empty_like(x)
@@ -92,7 +93,8 @@ class Mesh:
                 raise ValueError("dir_mask must be a uint8 tensor of n_local entries on the mesh device")
         d = _lib.SemApplyDesc(float(c_mass), float(c_stiff), float(c_gradx), float(c_grady), _ptr(cu), _ptr(cv),
                               float(c_extra), _ptr(ea), _ptr(eb), _ptr(ec), _ptr(ed), float(c_acc), int(dir_mode),
-                              _ptr(dir_mask), _ptr(dir_val), int(dir_sides), int(algo))
+                              _ptr(dir_mask), _ptr(dir_val), int(dir_sides), int(algo),
+                              *((0, 0) if pos is None else (int(pos[0]), int(pos[1]))))
         _lib.check(self._lib.sem_apply(self._h, C.byref(d), _ptr(x), _ptr(y), self.stream_ptr(stream)))
         return y
 

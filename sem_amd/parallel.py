@@ -56,13 +56,21 @@ class InterfaceExchange:
         self.part, self.mesh, self.dist, self.group = part, mesh, dist, group
         self.buf = torch.empty((part.world - 1) * mesh.NY, dtype=torch.float64, device=mesh.device)
 
+    def start(self, y):
+        """Pack the interface partial sums and start the all-reduce (returns its work handle; the
+        collective runs on the process group's own stream, concurrently with later launches)."""
+        self.mesh.interface_pack(y, self.part.bounds, self.buf)
+        return self.dist.all_reduce(self.buf, group=self.group, async_op=True)
+
+    def finish(self, y, work):
+        work.wait()
+        self.mesh.interface_unpack(self.buf, self.part.bounds, y)
+        return y
+
     def __call__(self, y):
         if self.part.world == 1:
             return y
-        self.mesh.interface_pack(y, self.part.bounds, self.buf)
-        self.dist.all_reduce(self.buf, group=self.group)
-        self.mesh.interface_unpack(self.buf, self.part.bounds, y)
-        return y
+        return self.finish(y, self.start(y))
 
 
 class NeighborExchange:
@@ -81,9 +89,7 @@ class NeighborExchange:
     def _peer(self, r):
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
 
-    def __call__(self, y):
-        if self.part.world == 1:
-            return y
+    def start(self, y):
         NY, d = self.NY, self.dist
         ops = []
         if self.left is not None:
@@ -92,13 +98,56 @@ class NeighborExchange:
         if self.right is not None:
             ops.append(d.P2POp(d.isend, y[-NY:], self._peer(self.right), self.group))
             ops.append(d.P2POp(d.irecv, self.recv_r, self._peer(self.right), self.group))
-        for req in d.batch_isend_irecv(ops):
+        return d.batch_isend_irecv(ops) if ops else []
+
+    def finish(self, y, reqs):
+        for req in reqs:
             req.wait()
+        NY = self.NY
         if self.left is not None:
             y[:NY] += self.recv_l
         if self.right is not None:
             y[-NY:] += self.recv_r
         return y
+
+    def __call__(self, y):
+        if self.part.world == 1:
+            return y
+        return self.finish(y, self.start(y))
+
+
+class StripApply:
+    """One partitioned operator apply with the interface assembly.
+
+    overlap=True: the output lines of the strip's two interface positions (first element column,
+    closing line) are computed first (two position-ranged launches, sem_apply_desc.pos_*), their
+    exchange is started -- an async RCCL all-reduce (or send/recv) on the process group's stream --
+    and the interior positions are computed while it runs; then the step waits and unpacks.  The
+    interior launch touches neither interface line, so nothing races with the collective.
+    overlap=False: one launch over the strip, then the exchange."""
+
+    def __init__(self, part, mesh, dist, group=None, kind="allreduce", overlap=True):
+        self.part, self.mesh, self.dist = part, mesh, dist
+        self.exch = part.exchanger(mesh, dist, group=group, kind=kind) if part.world > 1 else None
+        self.overlap = overlap and self.exch is not None
+        self.ncols = mesh.ex_end - mesh.ex_begin
+
+    def __call__(self, x, y=None, **kw):
+        m = self.mesh
+        if y is None:
+            y = torch.empty_like(x)
+        if self.exch is None:
+            return m.apply(x, y, **kw)
+        if not self.overlap:
+            m.apply(x, y, **kw)
+            return self.exch(y)
+        n = self.ncols
+        m.apply(x, y, pos=(0, 1), **kw)
+        m.apply(x, y, pos=(n, n + 1), **kw)
+        work = self.exch.start(y)
+        if n > 1:
+            m.apply(x, y, pos=(1, n), **kw)
+        return self.exch.finish(y, work)
 
 
 class DistributedInner:
@@ -121,3 +170,45 @@ class DistributedInner:
         if self.dist is not None:
             self.dist.all_reduce(h, group=self.group)
         return h
+
+
+class Partition:
+    """Element-strip partition of one solver across the ranks of `dist` (torch.distributed, RCCL
+    under "nccl"): this rank holds element columns part.local_range(rank).  Passed to
+    ConvectionDiffusionSolver(partition=...).  mesh_factory(P, nex, ney, dx, dy, eb, ee) builds the
+    strip's mesh (default: a libsemops handle on the current device)."""
+
+    def __init__(self, dist, group=None, exchange="allreduce", overlap=True, mesh_factory=None):
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.exchange, self.overlap = exchange, overlap
+        self.mesh_factory = mesh_factory
+
+    def setup(self, P, nex, ney, dx, dy):
+        self.part = StripPartition(nex, self.world)
+        eb, ee = self.part.local_range(self.rank)
+        if self.mesh_factory is not None:
+            mesh = self.mesh_factory(P, nex, ney, dx, dy, eb, ee)
+        else:
+            from .device import get_mesh
+            mesh = get_mesh(P, nex, ney, dx, dy, eb, ee)
+        self.mesh = mesh
+        self.step = StripApply(self.part, mesh, self.dist, self.group, self.exchange, self.overlap)
+        self.inner = DistributedInner(self.part, mesh, self.dist, self.group)
+        return mesh
+
+    def local(self, v):
+        """This rank's slice of a global vector (x-major numbering)."""
+        m = self.mesh
+        return v[m.dof_begin:m.dof_begin + m.n_local]
+
+    def gather(self, y):
+        """Global vector (every rank) from the local strips; shared lines agree after an exchange."""
+        m = self.mesh
+        full = torch.zeros(m.N, dtype=y.dtype, device=y.device)
+        own = y if self.rank == 0 else y[m.NY:]      # a shared line is taken from its left rank
+        off = m.dof_begin if self.rank == 0 else m.dof_begin + m.NY
+        full[off:off + own.numel()] = own
+        self.dist.all_reduce(full, group=self.group)
+        return full

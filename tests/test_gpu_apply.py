@@ -352,3 +352,41 @@ def test_bad_arguments_raise(gpu):
         mesh.apply(x, x, c_stiff=1.0)
     with pytest.raises(ValueError):
         mesh.apply(x.float(), c_stiff=1.0)
+
+
+@pytest.mark.parametrize("P,nex,ney,eb,ee", [(8, 64, 64, 0, 64), (8, 40, 13, 10, 30), (4, 9, 7, 2, 9), (12, 5, 3, 0, 5),
+                                             (6, 7, 5, 3, 4), (8, 1024, 8, 0, 1024)])
+@pytest.mark.parametrize("full", [False, True])
+def test_position_ranges_compose_bitwise(gpu, P, nex, ney, eb, ee, full):
+    """sem_apply_desc.pos_*: the interface positions and the interior positions in separate launches
+    (the multi-GPU overlap schedule) reproduce one whole-strip launch bitwise, and untouched lines
+    keep their previous values."""
+    from sem_amd import _lib
+    from sem_amd.device import get_mesh
+    mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.5 / ney, eb, ee)
+    r = np.random.default_rng(nex + 3 * eb)
+    N = mesh.n_local
+    X, U, V, A, B, Y0, G = (mesh.to_device(r.uniform(-1, 1, N)) for _ in range(7))
+    kw = dict(c_mass=0.25, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V)
+    if full:
+        kw.update(c_extra=3.0, ea=A, eb=B, c_acc=2.0, dir_mode=_lib.DIR_IDENTITY, dir_val=G,
+                  dir_sides=_lib.SIDE_W | _lib.SIDE_E | _lib.SIDE_S)
+    else:
+        kw.update(dir_mode=_lib.DIR_IDENTITY, dir_sides=_lib.SIDE_W | _lib.SIDE_E)
+    whole = mesh.apply(X, Y0.clone(), **kw)
+    n = ee - eb
+    y = Y0.clone()
+    mesh.apply(X, y, pos=(0, 1), **kw)
+    mesh.apply(X, y, pos=(n, n + 1), **kw)
+    if n > 1:
+        mesh.apply(X, y, pos=(1, n), **kw)
+    assert torch.equal(y, whole)
+    # a single position writes only its lines
+    y2 = Y0.clone()
+    mesh.apply(X, y2, pos=(n, n + 1), **kw)
+    NY = mesh.NY
+    assert torch.equal(y2[-NY:], whole[-NY:]) and torch.equal(y2[:-NY], Y0[:-NY])
+    with pytest.raises(ValueError):
+        mesh.apply(X, y2, pos=(0, n + 2), **kw)
+    with pytest.raises(RuntimeError):
+        mesh.apply(X, y2, pos=(0, 1), algo=_lib.ALGO_MFMA, **kw)

@@ -81,3 +81,56 @@ def test_partitioned_device_gmres(gpu, world):
     for rank, info, iters, d0, x in out:
         assert info == 0 and abs(iters - ref.iters) <= max(2, ref.iters // 50), (rank, iters, ref.iters)
         assert np.abs(x - xr[d0:d0 + len(x)]).max() < 1e-8 * max(1.0, np.abs(xr).max())
+
+
+def _worker_solver(rank, world, port, q, kind, overlap):
+    """ConvectionDiffusionSolver(partition=...) on real strip meshes: residual / Jacobian applies
+    and the Newton step with the partitioned device GMRES."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sem_amd.parallel import Partition
+        from sem_amd.solvers import ConvectionDiffusionSolver
+        part = Partition(dist, exchange=kind, overlap=overlap)
+        cd = ConvectionDiffusionSolver(1.0, 1.0, PE, P, NEX, NEY, T_W=0.5, T_E=-0.5, mtol=1e-10, partition=part)
+        r = np.random.default_rng(23)
+        T, u, v, dT, du, dv = (r.uniform(-1, 1, cd.N) for _ in range(6))
+        res = cd._get_residuals(T, u, v)
+        cd._calc_jacobians(T)
+        dres = cd._get_dresiduals(dT, du, dv)
+        pts = cd.points
+        sol = cd._get_solution(pts[1] - 0.5, 0.5 - pts[0])
+        q.put((rank, res, dres, sol, cd.matvecs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind,overlap", [(2, "allreduce", True), (3, "allreduce", True), (3, "p2p", True),
+                                                (2, "allreduce", False)])
+def test_partitioned_cd_solver(gpu, world, kind, overlap):
+    from sem_amd.solvers import ConvectionDiffusionSolver
+    cd = ConvectionDiffusionSolver(1.0, 1.0, PE, P, NEX, NEY, T_W=0.5, T_E=-0.5, mtol=1e-10)
+    r = np.random.default_rng(23)
+    T, u, v, dT, du, dv = (r.uniform(-1, 1, cd.N) for _ in range(6))
+    res = cd._get_residuals(T, u, v)
+    cd._calc_jacobians(T)
+    dres = cd._get_dresiduals(dT, du, dv)
+    pts = cd.points
+    sol = cd._get_solution(pts[1] - 0.5, 0.5 - pts[0])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_solver, args=(rr, world, port, q, kind, overlap)) for rr in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, pres, pdres, psol, mv in out:
+        assert np.abs(pres - res).max() <= 1e-13 * np.abs(res).max(), rank
+        assert np.abs(pdres - dres).max() <= 1e-13 * np.abs(dres).max(), rank
+        assert np.abs(psol - sol).max() < 1e-8, rank
+        assert abs(mv - cd.matvecs) <= 2, (rank, mv, cd.matvecs)

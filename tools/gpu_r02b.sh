@@ -1,7 +1,7 @@
 set -o pipefail
 O=gpurun_out/r02b; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_abi.py tests/test_gpu_ns_velocity.py tests/test_gpu_solvers.py tests/test_gpu_boussinesq.py > $O/tests.log 2>&1; rc=$?
-tail -40 $O/tests.log | grep -v "^$" | tail -30
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_abi.py tests/test_gpu_ns_velocity.py tests/test_gpu_solvers.py tests/test_gpu_boussinesq.py tests/test_gpu_dist.py "tests/test_gpu_apply.py::test_cfg5_checksums_full_size" tests/test_gpu_apply.py -k "position or cfg5 or ns or abi or solver or bous or dist or sweeps or tuning or launchers or cd or helmholtz" > $O/tests.log 2>&1; rc=$?
+grep -E "PASSED|FAILED|ERROR|passed|failed" $O/tests.log | tail -60
 [ $rc -gt 1 ] && exit $rc
 timeout -k 10 300 python -u tools/ns_solve.py --ne 8 --P 8 --Re 400 --out $O/ns8_400.json > $O/ns8_400.log 2>&1 || { tail -20 $O/ns8_400.log; exit 1; }
 tail -3 $O/ns8_400.log
