@@ -83,8 +83,11 @@ class NeighborExchange:
         left, right = part.slots(self.rank)
         self.left = self.rank - 1 if left >= 0 else None
         self.right = self.rank + 1 if right >= 0 else None
-        self.recv_l = torch.empty(self.NY, dtype=torch.float64, device=mesh.device) if self.left is not None else None
-        self.recv_r = torch.empty(self.NY, dtype=torch.float64, device=mesh.device) if self.right is not None else None
+        # gloo (the one-GPU rehearsal backend) sends and receives host tensors only: stage through host
+        self.host = dist.get_backend(group) == "gloo" and mesh.device.type == "cuda"
+        bdev = "cpu" if self.host else mesh.device
+        self.recv_l = torch.empty(self.NY, dtype=torch.float64, device=bdev) if self.left is not None else None
+        self.recv_r = torch.empty(self.NY, dtype=torch.float64, device=bdev) if self.right is not None else None
 
     def _peer(self, r):
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
@@ -93,10 +96,12 @@ class NeighborExchange:
         NY, d = self.NY, self.dist
         ops = []
         if self.left is not None:
-            ops.append(d.P2POp(d.isend, y[:NY], self._peer(self.left), self.group))
+            sl = y[:NY].cpu() if self.host else y[:NY]
+            ops.append(d.P2POp(d.isend, sl, self._peer(self.left), self.group))
             ops.append(d.P2POp(d.irecv, self.recv_l, self._peer(self.left), self.group))
         if self.right is not None:
-            ops.append(d.P2POp(d.isend, y[-NY:], self._peer(self.right), self.group))
+            sr = y[-NY:].cpu() if self.host else y[-NY:]
+            ops.append(d.P2POp(d.isend, sr, self._peer(self.right), self.group))
             ops.append(d.P2POp(d.irecv, self.recv_r, self._peer(self.right), self.group))
         return d.batch_isend_irecv(ops) if ops else []
 
@@ -105,9 +110,9 @@ class NeighborExchange:
             req.wait()
         NY = self.NY
         if self.left is not None:
-            y[:NY] += self.recv_l
+            y[:NY] += self.recv_l.to(y.device)
         if self.right is not None:
-            y[-NY:] += self.recv_r
+            y[-NY:] += self.recv_r.to(y.device)
         return y
 
     def __call__(self, y):

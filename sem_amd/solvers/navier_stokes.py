@@ -32,8 +32,9 @@ class NavierStokesSolver:
     def __init__(self, L_x: float, L_y: float, Re: float, Gr: float, P: int, N_ex: int, N_ey: int,
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
-                 max_basis: int = 3000):
+                 max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True):
         self._iprint = iprint
+        self._velocity_interior, self._velocity_graph = velocity_interior, velocity_graph
         self._max_basis = max_basis
         self._velo = None
         self._Re, self._Gr = Re, Gr
@@ -167,13 +168,15 @@ class NavierStokesSolver:
             return self._velo
         tStart = time.perf_counter()
         m = self._mesh
-        vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device)
+        vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior)
         blocks = vs.empty_blocks()
         kw = self._sys_kw(self._Sys)
         m.velocity_blocks(blocks, juu=self._Jac_u_u._coeffs()[4], juv=self._Jac_u_v._coeffs()[4],
                           jvu=self._Jac_v_u._coeffs()[4], jvv=self._Jac_v_v._coeffs()[4],
                           dir_mask=self._dir.mask, dir_sides=self._dir.sides, **kw)
         vs.factor(blocks.pop("AII"), **blocks)
+        if self._velocity_graph:
+            vs.capture()
         self._velo = vs
         if 'LU_suc' in self._iprint:
             torch.cuda.synchronize(m.device)
@@ -184,7 +187,11 @@ class NavierStokesSolver:
         """Velocity solve + pressure Schur-complement Krylov solve (NavierStokes_Solver.py:162-236), on
         the device: the velocity Jacobian is factored once per linearisation (_velocity_solver) and the
         Schur system is solved by the device GMRES (sem_amd/krylov.py) with the reference's
-        mass-diagonal preconditioner (:208-212) and stopping rule ||r||_2 <= mtol sqrt(N) (:222-224)."""
+        mass-diagonal preconditioner (:208-212) and stopping rule ||r||_2 <= mtol sqrt(N) (:222-224).
+        The reference's inner_m = 0.3 N is "not a realistic inner_m" (:224): its LGMRES runs as an
+        unrestarted GMRES with outer augmentation.  A plain GMRES restarted at 0.3 N stagnates on small
+        meshes (the Schur complement carries the spurious pressure modes of the equal-order
+        discretisation), so the device GMRES runs unrestarted up to max_basis vectors."""
         vs = self._velocity_solver()
         ru, rv, rc = self._dev(dres_u), self._dev(dres_v), self._dev(dres_cont)
         Z = torch.zeros(self.N, dtype=torch.float64, device=self._mesh.device)
@@ -205,13 +212,15 @@ class NavierStokesSolver:
 
         it = [0]
 
+        prog = getattr(self, "_progress", 0)
+
         def cb(est):
             it[0] += 1
-            if 'LGMRES_iter' in self._iprint:
-                print(f'NavierStokes GMRES: {it[0]}\t{est}')
+            if 'LGMRES_iter' in self._iprint or (prog and it[0] % prog == 0):
+                print(f'NavierStokes GMRES: {it[0]}\t{est}', flush=True)
 
         r = gmres(schur_mv, b_schur, x0=self._dev(dp0), atol=self._mtol * np.sqrt(self.N), rtol=0.0,
-                  restart=max(1, min(int(self.N * 0.3), self._max_basis)), precond=precon, callback=cb)
+                  restart=max(1, min(self.N, self._max_basis)), precond=precon, callback=cb)
         if r.info != 0:
             raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {r.info} iterations')
         dp = r.x

@@ -28,11 +28,11 @@ import torch
 class VelocityJacobianSolver:
     """x = J^-1 b for the velocity Jacobian J of one linearisation, J given by its condensation pieces."""
 
-    def __init__(self, P, nex, ney, device, interior="lu"):
+    def __init__(self, P, nex, ney, device, interior="nested"):
         if P < 1 or nex < 1 or ney < 1:
             raise ValueError("bad mesh")
-        if interior not in ("lu", "inverse"):
-            raise ValueError("interior must be 'lu' or 'inverse'")
+        if interior not in ("nested", "lu", "inverse"):
+            raise ValueError("interior must be 'nested', 'lu' or 'inverse'")
         self.P, self.nex, self.ney = P, nex, ney
         self.NY, self.NX = ney * P + 1, nex * P + 1
         self.m = 2 * self.NY
@@ -57,13 +57,18 @@ class VelocityJacobianSolver:
         """Condense and factor.  AII is consumed (its storage is reused for the LU factors)."""
         P, nex, m = self.P, self.nex, self.m
         if P > 1:
-            LU, piv, info = torch.linalg.lu_factor_ex(AII)
-            del AII
-            if int(info.max().item()) > 0:
-                raise RuntimeError("velocity Jacobian: singular interior block")
             # dense A_IB (nex, nI, 2m): rows (l, r), column block s holds aIB[e, l, s, r] on its diagonal
             AIB = torch.diag_embed(aIB).permute(0, 1, 3, 2, 4).reshape(nex, self.nI, 2 * m)
-            W = torch.linalg.lu_solve(LU, piv, AIB)
+            if self.interior == "nested":
+                self._nested_factor(AII)
+                del AII
+                W = self._nested_solve(AIB)
+            else:
+                LU, piv, info = torch.linalg.lu_factor_ex(AII)
+                del AII
+                if int(info.max().item()) > 0:
+                    raise RuntimeError("velocity Jacobian: singular interior block")
+                W = torch.linalg.lu_solve(LU, piv, AIB)
             del AIB
             Wr = W.view(nex, P - 1, m, 2, m)
             # C[e, s, r, t, k] = sum_l aBI[e, s, l, r] W[e, l, r, t, k]: A_BI W for both interface lines
@@ -81,10 +86,10 @@ class VelocityJacobianSolver:
                 self.Ainv = torch.linalg.lu_solve(LU, piv, eye)
                 del LU, piv
                 self.LU = self.piv = None
-            else:
+            elif self.interior == "lu":
                 self.LU, self.piv = LU, piv
-            self.W = W.view(nex, self.nI, 2, m)
-            self.aBI = aBI
+            self.W = W.view(nex, self.nI, 2, m) if self.interior != "nested" else None
+            self.aBI, self.aIB = aBI, aIB
         else:
             S_diag, S_up, S_lo = D, torch.diag_embed(E), torch.diag_embed(F)
         # block Thomas on the interface lines: Dt[0] = S_diag[0], Uh[L] = Dt[L]^-1 S_up[L],
@@ -101,24 +106,87 @@ class VelocityJacobianSolver:
         self.Dinv, self.Uh, self.S_lo = Dinv, Uh, S_lo
         self.factored = True
 
+    # ------------------------------------------------------------------ nested interior (default)
+    # Inside one element column the interior unknowns split again: the interiors of its elements
+    # (y nodes strictly inside element n, on all P-1 interior lines: 2 (P-1)^2 unknowns) couple only
+    # to the horizontal element edges y = nP, (n+1)P of the same lines.  So A_II is eliminated in
+    # two levels -- batched inverses of the small element-interior blocks, then one dense block of
+    # the column's edge unknowns (2 (P-1)(N_ey+1)) -- the classical static condensation of SEM
+    # element interiors.  A column solve then reads ~100x fewer bytes than a dense A_II^-1.
+    def _nested_index(self):
+        P, ney, NY, m = self.P, self.ney, self.NY, self.m
+        dev = self.device
+        l = torch.arange(1, P, device=dev)
+        c = torch.arange(2, device=dev)
+        col = lambda ll, cc, gy: (ll - 1) * m + cc * NY + gy  # noqa: E731  column-interior ordering
+        # element interiors: (n, l, c, j) with gy = nP + j, j = 1..P-1
+        n = torch.arange(ney, device=dev)
+        j = torch.arange(1, P, device=dev)
+        pi = col(l[None, :, None, None], c[None, None, :, None], n[:, None, None, None] * P + j[None, None, None, :])
+        self._pi = pi.reshape(ney, -1)                                  # (ney, 2 (P-1)^2)
+        # edges: (k, l, c) with gy = kP, k = 0..ney
+        k = torch.arange(ney + 1, device=dev)
+        pe = col(l[None, :, None], c[None, None, :], k[:, None, None] * P)
+        self._ne1 = 2 * (P - 1)                                         # unknowns per edge row k
+        self._pe = pe.reshape(-1)                                       # (n_e,)
+        self._pe_el = torch.cat((pe[:-1].reshape(ney, -1), pe[1:].reshape(ney, -1)), dim=1)  # edges k=n, n+1
+
+    def _nested_factor(self, AII):
+        self._nested_index()
+        nex, ney = self.nex, self.ney
+        pi, pe, pel = self._pi, self._pe, self._pe_el
+        e = torch.arange(nex, device=self.device)[:, None, None, None]
+        A_ii = AII[e, pi[None, :, :, None], pi[None, :, None, :]]     # (nex, ney, ni, ni)
+        A_ie = AII[e, pi[None, :, :, None], pel[None, :, None, :]]    # (nex, ney, ni, 2 ne1)
+        A_ei = AII[e, pel[None, :, :, None], pi[None, :, None, :]]    # (nex, ney, 2 ne1, ni)
+        S_e = AII[e[:, :, 0], pe[None, :, None], pe[None, None, :]]   # (nex, n_e, n_e)
+        self._Xi = torch.linalg.inv(A_ii)
+        self._Yie = self._Xi @ A_ie
+        self._Aei = A_ei
+        C = (A_ei @ self._Yie).view(nex, ney, 2, self._ne1, 2, self._ne1)
+        S = S_e.view(nex, ney + 1, self._ne1, ney + 1, self._ne1)
+        n = torch.arange(ney, device=self.device)
+        for a in range(2):          # element n touches edge rows k = n + a, columns k = n + b
+            for b in range(2):
+                S[:, n + a, :, n + b, :] -= C[:, :, a, :, b, :].permute(1, 0, 2, 3)  # index dims lead
+        self._Se_inv = torch.linalg.inv(S_e)
+
+    def _nested_solve(self, R):
+        """A_II^-1 R for every column at once; R (nex, nI, k)."""
+        nex, ney, ne1 = self.nex, self.ney, self._ne1
+        k = R.shape[-1]
+        Ri = R[:, self._pi]                                             # (nex, ney, ni, k)
+        Re = R[:, self._pe].clone()                                     # (nex, n_e, k)
+        Ti = self._Xi @ Ri
+        Cn = self._Aei @ Ti                                             # (nex, ney, 2 ne1, k)
+        Rv = Re.view(nex, ney + 1, ne1, k)
+        Rv[:, :-1] -= Cn[:, :, :ne1]
+        Rv[:, 1:] -= Cn[:, :, ne1:]
+        Ye = self._Se_inv @ Re                                          # (nex, n_e, k)
+        Yv = Ye.view(nex, ney + 1, ne1, k)
+        Yi = Ti - self._Yie @ torch.cat((Yv[:, :-1], Yv[:, 1:]), dim=2)
+        Y = torch.empty_like(R)
+        Y[:, self._pi] = Yi
+        Y[:, self._pe] = Ye
+        return Y
+
     # ------------------------------------------------------------------ solve
-    def solve(self, bu, bv):
-        """(J^-1 [bu; bv]) split as (xu, xv); bu, bv are length-N vectors in the x-major numbering."""
-        if not self.factored:
-            raise RuntimeError("factor() first")
-        P, nex, m, NX, NY = self.P, self.nex, self.m, self.NX, self.NY
-        B = torch.stack((bu.reshape(NX, NY), bv.reshape(NX, NY)), dim=1).reshape(NX, m)
+    def _solve_lines(self, B):
+        """x = J^-1 b with b, x as (NX, 2 NY) line arrays (every line: u then v)."""
+        P, nex, m, NX = self.P, self.nex, self.m, self.NX
         g = B[0::P].clone()                                    # interface lines (nex+1, m)
         if P > 1:
             bI = B[:-1].reshape(nex, P, m)[:, 1:, :].reshape(nex, self.nI, 1)
-            if self.interior == "inverse":
+            if self.interior == "nested":
+                yI = self._nested_solve(bI)
+            elif self.interior == "inverse":
                 yI = torch.bmm(self.Ainv, bI)
             else:
                 yI = torch.linalg.lu_solve(self.LU, self.piv, bI)
             yIr = yI.view(nex, P - 1, m)
             g[:-1] -= (self.aBI[:, 0] * yIr).sum(1)
             g[1:] -= (self.aBI[:, 1] * yIr).sum(1)
-        # interface sweep
+        # interface sweep (block Thomas with the pivot blocks' explicit inverses)
         z = torch.empty_like(g)
         z[0] = self.Dinv[0] @ g[0]
         for L in range(1, nex + 1):
@@ -129,8 +197,54 @@ class VelocityJacobianSolver:
         out = torch.empty((NX, m), dtype=torch.float64, device=self.device)
         out[0::P] = xB
         if P > 1:
-            xI = yI.view(nex, self.nI) - (torch.bmm(self.W[:, :, 0, :], xB[:-1, :, None])
-                                          + torch.bmm(self.W[:, :, 1, :], xB[1:, :, None]))[..., 0]
+            if self.interior == "nested":   # x_I = A_II^-1 (b_I - A_IB x_B); A_IB is diagonal per line
+                rI = bI.view(nex, P - 1, m) - (self.aIB[:, :, 0, :] * xB[:-1, None, :]
+                                                + self.aIB[:, :, 1, :] * xB[1:, None, :])
+                xI = self._nested_solve(rI.reshape(nex, self.nI, 1))
+            else:
+                xI = yI.view(nex, self.nI) - (torch.bmm(self.W[:, :, 0, :], xB[:-1, :, None])
+                                              + torch.bmm(self.W[:, :, 1, :], xB[1:, :, None]))[..., 0]
             out[:-1].view(nex, P, m)[:, 1:, :] = xI.view(nex, P - 1, m)
-        out = out.view(NX, 2, NY)
+        return out
+
+    def capture(self):
+        """Capture the solve (about 3 (N_ex+1) + 10 launches) in a hipGraph: a Schur-complement
+        matvec then costs the kernels, not the Python and launch overhead of that many small ops.
+        Returns False (and the solve stays eager) if the device libraries refuse the capture."""
+        if self.device.type != "cuda" or not self.factored:
+            return False
+        if self.P > 1 and self.interior == "lu":
+            return False   # the batched LU solve (rocSOLVER getrs) cannot be stream-captured
+        self._bin = torch.zeros((self.NX, self.m), dtype=torch.float64, device=self.device)
+        cur = torch.cuda.current_stream(self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(cur)
+        try:
+            with torch.cuda.stream(s):
+                self._solve_lines(self._bin)      # warm-up outside the capture (library workspaces)
+            cur.wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._xout = self._solve_lines(self._bin)
+            self._graph = g
+            return True
+        except RuntimeError:
+            torch.cuda.synchronize(self.device)
+            self._graph = None
+            return False
+
+    def solve(self, bu, bv):
+        """(J^-1 [bu; bv]) split as (xu, xv); bu, bv are length-N vectors in the x-major numbering."""
+        if not self.factored:
+            raise RuntimeError("factor() first")
+        NX, NY = self.NX, self.NY
+        if getattr(self, "_graph", None) is not None:
+            b3 = self._bin.view(NX, 2, NY)
+            b3[:, 0, :] = bu.reshape(NX, NY)
+            b3[:, 1, :] = bv.reshape(NX, NY)
+            self._graph.replay()
+            out = self._xout.view(NX, 2, NY)
+            return out[:, 0, :].reshape(-1).clone(), out[:, 1, :].reshape(-1).clone()
+        B = torch.stack((bu.reshape(NX, NY), bv.reshape(NX, NY)), dim=1).reshape(NX, self.m)
+        out = self._solve_lines(B).view(NX, 2, NY)
         return out[:, 0, :].reshape(-1), out[:, 1, :].reshape(-1)

@@ -21,7 +21,7 @@ def test_pieces_describe_the_jacobian_exactly(P, nex, ney, Re):
 
 
 @pytest.mark.parametrize("P,nex,ney,Re", CASES)
-@pytest.mark.parametrize("interior", ["lu", "inverse"])
+@pytest.mark.parametrize("interior", ["nested", "lu", "inverse"])
 def test_condensed_solve_matches_sparse_lu(P, nex, ney, Re, interior):
     ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
     pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
