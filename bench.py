@@ -9,9 +9,13 @@ Dirichlet identity rows -- the LGMRES matvec of ConvectionDiffusion_Solver
 on a synthetic 64 x 64-element, P = 8 mesh per GPU (BASELINE.json configs[1];
 Pe = 40, T, u, v ~ U(-1, 1) from default_rng(2024)).  N = 263,169 DOFs per
 GPU; inputs resident in HBM before the timed region.  With --gpus N > 1 each
-rank holds one 64-element-column strip of a (64 N) x 64 mesh (weak scaling)
-and every step ends with the interface-line exchange (RCCL all-reduce of the
-shared-edge partial sums, or --exchange p2p: send/recv with the two neighbours).
+rank holds one element-column strip and every step assembles the interface lines
+(RCCL all-reduce of the shared-edge partial sums, or --exchange p2p: send/recv
+with the two neighbours), overlapped with the interior apply (--overlap 1: the
+strip's two interface positions are applied first, the exchange is started, the
+interior positions are applied while it runs).
+  --scaling weak   (default) a 64-element-column strip per rank of a (64 N) x 64 mesh
+  --scaling strong the 64 x 64 mesh (--ne) split into N strips (BASELINE.md's strong-scaling plan)
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N bench.py --gpus N ...
@@ -48,6 +52,9 @@ def parse():
     ap.add_argument("--hbm-ne", type=int, default=1024, help="HBM-regime mesh size (0 = skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the measured path); gloo only to rehearse N > 1 on a 1-GPU box")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --ne x --ne elements per GPU; strong: --ne x --ne elements over all GPUs")
+    ap.add_argument("--overlap", type=int, default=1, help="N > 1: overlap the interface exchange with the interior")
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "p2p"],
                     help="interface assembly for N > 1: one RCCL all-reduce, or send/recv with the two neighbours")
     return ap.parse_args()
@@ -223,10 +230,10 @@ def main():
 
     from sem_amd import _lib
     from sem_amd.device import get_mesh
-    from sem_amd.parallel import StripPartition
+    from sem_amd.parallel import StripApply, StripPartition
 
     P, ne, Pe = args.P, args.ne, args.Pe
-    nex, ney = ne * world, ne
+    nex, ney = (ne * world, ne) if args.scaling == "weak" else (ne, ne)
     d = 1.0 / ne
     part = StripPartition(nex, world)
     eb, ee = part.bounds[rank], part.bounds[rank + 1]
@@ -235,12 +242,13 @@ def main():
     y = torch.empty_like(T)
     sides = _lib.SIDE_W | _lib.SIDE_E
     kw = dict(c_stiff=1.0, c_gradx=Pe, cu=u, c_grady=Pe, cv=v, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides)
-    exch = part.exchanger(mesh, dist, kind=args.exchange) if world > 1 else None
+    strip = StripApply(part, mesh, dist, kind=args.exchange, overlap=bool(args.overlap)) if world > 1 else None
 
     def step():
-        mesh.apply(T, y, **kw)
-        if exch is not None:
-            exch(y)
+        if strip is None:
+            mesh.apply(T, y, **kw)
+        else:
+            strip(T, y, **kw)
 
     # N > 1 over RCCL: the whole step (apply, pack, RCCL all-reduce or send/recv, unpack) is captured
     # too -- RCCL collectives are stream-capturable -- so the per-step host cost (four launches and a
@@ -285,13 +293,16 @@ def main():
                 "matvec north_star targets (ConvectionDiffusion_Solver.py:104-121); the Laplacian-only K T "
                 "is reported under laplacian_only",
         "value": value, "unit": "DOF-updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "ms_per_step": ms, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (T,u,v ~ U(-1,1), default_rng(2024+rank); Pe=40; Dirichlet W/E rows)",
-        "config": {"workload": workload, "mesh_per_gpu": f"{ne}x{ne} elements", "P": P,
+        "config": {"workload": workload,
+                   "mesh_per_gpu": f"{ee - eb}x{ney} elements" + (" (rank 0)" if args.scaling == "strong" else ""),
+                   "P": P,
                    "global_mesh": f"{nex}x{ney}", "dofs_global": N_glob, "dofs_per_gpu": n_loc,
                    "partition": f"element-column strips x{world}" + (
                        {"allreduce": ", all-reduce of interface lines",
                         "p2p": ", send/recv of interface lines with neighbours"}[args.exchange]
+                       + (", overlapped with the interior apply" if args.overlap else "")
                        + (" (RCCL)" if args.dist_backend == "nccl" else " (gloo rehearsal)")
                        if world > 1 else ""),
                    "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": use_graph},

@@ -215,10 +215,10 @@ int sem_interface_unpack(sem_handle* h, const double* buf, const int* bounds, in
  * (ConvectionDiffusion_Solver.py:146-148, NavierStokes_Solver.py:222-224; SciPy's
  * lgmres inner loop) on a basis V of k rows of n doubles, row pitch ldv, in device memory.
  * sem_basis_dot2:   out[2j] = V_j . a, out[2j+1] = V_j . b (one pass over V; fixed summation
- *                   order, bitwise reproducible); work: sem_basis_dot2_work_size(k) doubles.
+ *                   order, bitwise reproducible); work: sem_basis_dot2_work_size(k, n) doubles.
  * sem_basis_update: w -= V^T c (one pass over V).
  * Stream-ordered; all pointers are device pointers. */
-int sem_basis_dot2_work_size(int k);
+int64_t sem_basis_dot2_work_size(int k, int64_t n);
 int sem_basis_dot2(const double* V, int64_t ldv, int k, int64_t n, const double* a, const double* b, double* work,
                    double* out, void* stream);
 int sem_basis_update(const double* V, int64_t ldv, int k, int64_t n, const double* c, double* w, void* stream);

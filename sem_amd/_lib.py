@@ -71,7 +71,7 @@ _SIGS = {
     "sem_interface_pack": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int), C.c_int, C.c_void_p, C.c_void_p]),
     "sem_interface_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int), C.c_int, C.c_void_p,
                                        C.c_void_p]),
-    "sem_basis_dot2_work_size": (C.c_int, [C.c_int]),
+    "sem_basis_dot2_work_size": (C.c_int64, [C.c_int, C.c_int64]),
     "sem_basis_dot2": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p]),
     "sem_basis_update": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),

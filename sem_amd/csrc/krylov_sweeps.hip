@@ -17,66 +17,71 @@
 
 namespace sem {
 
-constexpr int kDotChunks = 64;   // column chunks per row (grid.x); partial sums per row
-constexpr int kDotThreads = 256;
+// sem_basis_dot2: 2-D tiles.  Block (chunk c, row group g) reads the a / b chunk of kDotCols
+// columns into registers once and streams kDotRows basis rows against it, so a and b are read
+// k / kDotRows times instead of k times (V itself exactly once).  Per row, every thread forms its
+// partial products over its kDotPer columns; the partials go through LDS, are reduced over the
+// block in a fixed order, and one value per (row, a|b, chunk) goes to `work`.  basis_dot2_finish
+// then sums the chunks in order: results are bitwise reproducible.
+constexpr int kDotThreads = 256, kDotPer = 8, kDotCols = kDotThreads * kDotPer, kDotRows = 16;
 
-// Block (c, j): partial dot products of row j over column chunk c.
-__global__ __launch_bounds__(kDotThreads) void basis_dot2_kernel(const double* __restrict__ V, int64_t ldv, int64_t n,
-                                                                 const double* __restrict__ a,
+__global__ __launch_bounds__(kDotThreads) void basis_dot2_kernel(const double* __restrict__ V, int64_t ldv, int k,
+                                                                 int64_t n, int nchunks, const double* __restrict__ a,
                                                                  const double* __restrict__ b,
                                                                  double* __restrict__ work) {
-  const int c = blockIdx.x, j = blockIdx.y, t = threadIdx.x;
-  const int64_t len = (n + kDotChunks - 1) / kDotChunks;
-  const int64_t lo = c * len, hi = min(n, lo + len);
-  const double* row = V + j * ldv;
-  // four independent accumulator pairs: four rows-loads in flight per thread
-  double sa0 = 0.0, sb0 = 0.0, sa1 = 0.0, sb1 = 0.0, sa2 = 0.0, sb2 = 0.0, sa3 = 0.0, sb3 = 0.0;
-  int64_t i = lo + t;
-  for (; i + 3 * kDotThreads < hi; i += 4 * kDotThreads) {
-    const double v0 = row[i], v1 = row[i + kDotThreads], v2 = row[i + 2 * kDotThreads], v3 = row[i + 3 * kDotThreads];
-    sa0 = fma(v0, a[i], sa0);
-    sb0 = fma(v0, b[i], sb0);
-    sa1 = fma(v1, a[i + kDotThreads], sa1);
-    sb1 = fma(v1, b[i + kDotThreads], sb1);
-    sa2 = fma(v2, a[i + 2 * kDotThreads], sa2);
-    sb2 = fma(v2, b[i + 2 * kDotThreads], sb2);
-    sa3 = fma(v3, a[i + 3 * kDotThreads], sa3);
-    sb3 = fma(v3, b[i + 3 * kDotThreads], sb3);
+  __shared__ double part[2 * kDotRows][kDotThreads + 1];
+  const int c = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
+  const int64_t lo = static_cast<int64_t>(c) * kDotCols;
+  double av[kDotPer], bv[kDotPer];
+#pragma unroll
+  for (int q = 0; q < kDotPer; ++q) {
+    const int64_t i = lo + t + q * kDotThreads;
+    av[q] = i < n ? a[i] : 0.0;
+    bv[q] = i < n ? b[i] : 0.0;
   }
-  for (; i < hi; i += kDotThreads) {
-    const double v = row[i];
-    sa0 = fma(v, a[i], sa0);
-    sb0 = fma(v, b[i], sb0);
-  }
-  double sa = (sa0 + sa1) + (sa2 + sa3), sb = (sb0 + sb1) + (sb2 + sb3);
-  // wave reduction (fixed order), then the four waves in order
-  for (int off = 32; off > 0; off >>= 1) {
-    sa += __shfl_down(sa, off, 64);
-    sb += __shfl_down(sb, off, 64);
-  }
-  __shared__ double ra[kDotThreads / 64], rb[kDotThreads / 64];
-  if ((t & 63) == 0) {
-    ra[t >> 6] = sa;
-    rb[t >> 6] = sb;
+  const int r0 = g * kDotRows, nr = min(kDotRows, k - r0);
+  for (int r = 0; r < nr; ++r) {
+    const double* row = V + static_cast<int64_t>(r0 + r) * ldv;
+    double vv[kDotPer];
+#pragma unroll
+    for (int q = 0; q < kDotPer; ++q) {
+      const int64_t i = lo + t + q * kDotThreads;
+      vv[q] = i < n ? row[i] : 0.0;
+    }
+    double pa0 = 0.0, pb0 = 0.0, pa1 = 0.0, pb1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < kDotPer; q += 2) {
+      pa0 = fma(vv[q], av[q], pa0);
+      pb0 = fma(vv[q], bv[q], pb0);
+      pa1 = fma(vv[q + 1], av[q + 1], pa1);
+      pb1 = fma(vv[q + 1], bv[q + 1], pb1);
+    }
+    part[2 * r][t] = pa0 + pa1;
+    part[2 * r + 1][t] = pb0 + pb1;
   }
   __syncthreads();
-  if (t == 0) {
-    double xa = 0.0, xb = 0.0;
-    for (int w = 0; w < kDotThreads / 64; ++w) {
-      xa += ra[w];
-      xb += rb[w];
-    }
-    work[(static_cast<int64_t>(j) * kDotChunks + c) * 2 + 0] = xa;
-    work[(static_cast<int64_t>(j) * kDotChunks + c) * 2 + 1] = xb;
+  // 2 nr sums over 256 partials: 8 threads per value, 32 partials each, then 3 shuffle steps (fixed order)
+  const int v = t >> 3, s = t & 7;
+  double x = 0.0;
+  if (v < 2 * nr) {
+#pragma unroll 8
+    for (int q = 0; q < kDotThreads / 8; ++q) x += part[v][s * (kDotThreads / 8) + q];
+  }
+  x += __shfl_down(x, 4, 8);
+  x += __shfl_down(x, 2, 8);
+  x += __shfl_down(x, 1, 8);
+  if (s == 0 && v < 2 * nr) {
+    const int j = r0 + (v >> 1);
+    work[(static_cast<int64_t>(j) * nchunks + c) * 2 + (v & 1)] = x;
   }
 }
 
-__global__ void basis_dot2_finish(const double* __restrict__ work, int k, double* __restrict__ out) {
+__global__ void basis_dot2_finish(const double* __restrict__ work, int k, int nchunks, double* __restrict__ out) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;  // q = 2 j + (0: a, 1: b)
   if (q >= 2 * k) return;
   const int j = q >> 1, s = q & 1;
   double x = 0.0;
-  for (int c = 0; c < kDotChunks; ++c) x += work[(static_cast<int64_t>(j) * kDotChunks + c) * 2 + s];
+  for (int c = 0; c < nchunks; ++c) x += work[(static_cast<int64_t>(j) * nchunks + c) * 2 + s];
   out[q] = x;
 }
 
@@ -116,18 +121,24 @@ static int hip_check_k(hipError_t e, const char* what) {
 
 extern "C" {
 
-int sem_basis_dot2_work_size(int k) { return k > 0 ? 2 * k * sem::kDotChunks : 0; }
+// `work` holds one partial per (row, a|b, column chunk of kDotCols).
+static int dot2_chunks(int64_t n) { return static_cast<int>((n + sem::kDotCols - 1) / sem::kDotCols); }
+
+int64_t sem_basis_dot2_work_size(int k, int64_t n) { return k > 0 && n > 0 ? 2 * int64_t(k) * dot2_chunks(n) : 0; }
 
 int sem_basis_dot2(const double* V, int64_t ldv, int k, int64_t n, const double* a, const double* b, double* work,
                    double* out, void* stream) {
   if (k < 0 || n < 0 || ldv < n) return sem::set_error(SEM_EINVAL, "basis_dot2: bad shape");
   if (k == 0 || n == 0) return SEM_OK;
   if (!V || !a || !b || !work || !out) return sem::set_error(SEM_EINVAL, "basis_dot2: null argument");
-  if (k > 65535) return sem::set_error(SEM_EINVAL, "basis_dot2: more than 65535 basis vectors");
+  if (n > (int64_t(1) << 27)) return sem::set_error(SEM_EINVAL, "basis_dot2: rows longer than 2^27");
+  const int groups = (k + sem::kDotRows - 1) / sem::kDotRows;
+  if (groups > 65535) return sem::set_error(SEM_EINVAL, "basis_dot2: too many basis vectors");
   auto s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(sem::basis_dot2_kernel, dim3(sem::kDotChunks, k), dim3(sem::kDotThreads), 0, s, V, ldv, n, a, b,
+  const int nch = dot2_chunks(n);
+  hipLaunchKernelGGL(sem::basis_dot2_kernel, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n, nch, a, b,
                      work);
-  hipLaunchKernelGGL(sem::basis_dot2_finish, dim3((2 * k + 255) / 256), dim3(256), 0, s, work, k, out);
+  hipLaunchKernelGGL(sem::basis_dot2_finish, dim3((2 * k + 255) / 256), dim3(256), 0, s, work, k, nch, out);
   return sem::hip_check_k(hipGetLastError(), "basis_dot2 launch");
 }
 

@@ -8,9 +8,13 @@ Arnoldi orthogonalisation on the host (12.2 of 15.3 s at 32x32, P=8).
 
 Here the Krylov basis lives in device memory as one (m+1) x N matrix; each
 iteration applies the operator (one fused HIP kernel launch) and orthogonalises
-with classical Gram-Schmidt done twice (CGS2, as stable as modified Gram-Schmidt),
-the second pass's coefficients taken from the basis' Gram matrix: 3 GEMV sweeps over
-the basis per iteration (rocBLAS through torch) instead of 4, or 2k BLAS-1 calls for MGS.  Only the (m+1) x m Hessenberg least-squares problem (Givens
+with classical Gram-Schmidt done twice (CGS2), the second pass's coefficients taken from the
+basis' Gram matrix: (I - G) h equals V^T (w - V h) in exact arithmetic, so two sweeps over the
+basis per iteration instead of four (the HIP kernels sem_basis_dot2 / sem_basis_update).  That form
+cannot see the rounding error of the first subtraction, so when ||w|| collapses by more than
+REORTH_ETA = 1e-4 (severe cancellation, where the loss of orthogonality eps ||w|| / h_{k+1,k} would
+exceed ~1e-12) a true extra pass is made; tests/test_krylov.py checks ||I - V^T V|| on an
+ill-conditioned system.  Only the (m+1) x m Hessenberg least-squares problem (Givens
 rotations) runs on the host.  Vectors are torch tensors on any device, so the
 algorithm is unit-tested on CPU against SciPy.
 """
@@ -34,7 +38,8 @@ class _DeviceSweeps:
         self.V, self.ldv = V, V.stride(0)
         rows = V.shape[0]
         self.out = torch.empty((rows, 2), dtype=V.dtype, device=V.device)
-        self.work = torch.empty(max(1, self.lib.sem_basis_dot2_work_size(rows)), dtype=V.dtype, device=V.device)
+        self.work = torch.empty(max(1, self.lib.sem_basis_dot2_work_size(rows, V.shape[1])), dtype=V.dtype,
+                                device=V.device)
 
     def _stream(self):
         return torch.cuda.current_stream(self.V.device).cuda_stream
@@ -61,13 +66,17 @@ class _DeviceSweeps:
                                              w.data_ptr(), self._stream()))
 
 
+REORTH_ETA = 1e-4   # a true extra orthogonalisation pass when ||w|| drops below this fraction
+
+
 class GMRESResult:
-    def __init__(self, x, info, iters, res_norm, matvecs):
+    def __init__(self, x, info, iters, res_norm, matvecs, reorth=0):
         self.x, self.info, self.iters, self.res_norm, self.matvecs = x, info, iters, res_norm, matvecs
+        self.reorth = reorth
 
 
 def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, precond=None, callback=None,
-          inner=None):
+          inner=None, basis_out=None):
     """Right-preconditioned restarted GMRES.
 
     matvec(v) -> A v and precond(v) -> M^-1 v take and return 1-D tensors like b.
@@ -76,6 +85,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     inner(V, w) -> V @ w (k inner products) replaces the local products; a partitioned solve passes
     sem_amd.parallel.DistributedInner, so every rank sees the same Hessenberg entries and takes the
     same path through the iteration.
+    basis_out: a list that receives a copy of each cycle's orthonormal basis (tests).
     """
     proj = inner if inner is not None else (lambda A, w: A @ w)
 
@@ -97,14 +107,15 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     sweeps = _DeviceSweeps(V) if (inner is None and V.is_cuda and V.dtype == torch.float64) else None
     Z = torch.empty((restart, N), dtype=dt, device=dev) if precond is not None else None
     total, matvecs = 0, 0
+    self_reorth = [0]
     r = b - matvec(x) if x0 is not None else b.clone()
     matvecs += x0 is not None
     beta = vnorm(r)
     while True:
         if beta <= tol:
-            return GMRESResult(x, 0, total, beta, matvecs)
+            return GMRESResult(x, 0, total, beta, matvecs, self_reorth[0])
         if total >= maxiter:
-            return GMRESResult(x, total, total, beta, matvecs)
+            return GMRESResult(x, total, total, beta, matvecs, self_reorth[0])
         V[0] = r / beta
         H = np.zeros((restart + 1, restart))
         # Givens rotations and the rotated right-hand side as Python floats: the O(k) rotation
@@ -119,6 +130,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             if Z is not None:
                 Z[k] = zk
             w = matvec(zk)
+            w_in = w
             matvecs += 1
             Vk = V[:k + 1]
             # CGS2 in three sweeps over the basis instead of four: the second pass's coefficients
@@ -139,9 +151,28 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
                 sweeps.update(k + 1, hh.contiguous(), w)
             else:
                 w = w - Vk.T @ hh
-            col = hh.cpu().tolist()
-            hn = vnorm(w)
-            col.append(hn)
+            if inner is None:   # one device -> host transfer per step: coefficients, ||w|| after and before
+                col = torch.cat((hh, torch.linalg.vector_norm(w)[None],
+                                 torch.linalg.vector_norm(w_in)[None])).cpu().tolist()
+                h0 = col.pop()
+                hn = col[-1]
+            else:
+                col = hh.cpu().tolist()
+                hn = vnorm(w)
+                h0 = vnorm(w_in)
+                col.append(hn)
+            if hn < REORTH_ETA * h0:
+                # severe cancellation: the Gram-matrix form of the second pass cannot see the rounding
+                # error of the first subtraction, so make one true extra pass (it fires only when
+                # ||w|| collapses by 1e4 or more)
+                h2 = sweeps.dot2(k + 1, w, V[k])[:, 0].clone() if sweeps is not None else proj(Vk, w)
+                if sweeps is not None:
+                    sweeps.update(k + 1, h2.contiguous(), w)
+                else:
+                    w = w - Vk.T @ h2
+                hn = vnorm(w)
+                col = [a + b_ for a, b_ in zip(col[:-1], h2.cpu().tolist())] + [hn]
+                self_reorth[0] += 1
             for i in range(k):               # apply previous Givens rotations
                 c, s_ = cs[i], sn[i]
                 a, b_ = col[i], col[i + 1]
@@ -162,6 +193,8 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             if est <= tol or hn == 0.0 or total >= maxiter:
                 break
             V[k + 1] = w / hn
+        if basis_out is not None:
+            basis_out.append(V[:k_done].clone())
         # x += Z y  with  H[:k,:k] y = g[:k]
         y = np.linalg.solve(np.triu(H[:k_done, :k_done]), np.asarray(g[:k_done])) if k_done else np.zeros(0)
         yt = torch.as_tensor(y, dtype=dt, device=dev)
@@ -263,3 +296,167 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
             ptol_max = min(1.0, 1.5 * ptol_max)
         ptol = presid * min(ptol_max, tol / rnorm)
     return GMRESResult(x, 0 if rnorm <= tol else maxiter, total, rnorm, matvecs)
+
+
+class Recycle:
+    """Recycled Krylov subspace for a sequence of solves with ONE operator (GCRO, de Sturler 1999).
+
+    Holds U, C with A U = C and C^T C = I.  A solve first takes the part of b in span(C)
+    (x0 = U C^T b), keeps its Arnoldi vectors orthogonal to C, and afterwards appends its own search
+    space, so every later solve with the same operator starts where the previous ones ended.  The
+    coupled Newton-Krylov of the Boussinesq coupler applies each solver's block solve once per
+    outer GMRES iteration with a fixed linearisation -- tens of solves per operator.  The solver
+    resets it whenever its operator changes.  Device memory: 2 x capacity vectors."""
+
+    def __init__(self, n, dtype, device, capacity):
+        self.n, self.cap = n, int(capacity)
+        self.buf = torch.empty((self.cap, n), dtype=dtype, device=device)   # C rows, then a cycle's basis
+        self.U = torch.empty((self.cap, n), dtype=dtype, device=device)
+        self.k = 0
+        self.solves = 0
+        self.pending = None
+
+    def reset(self):
+        self.k = 0
+        self.pending = None
+
+    def absorb(self):
+        """Append the last cycle's search space (deferred until the space is used again, so a lone
+        solve pays nothing): A (Z_m - U E) = V_{m+1} H_m = (V_{m+1} Q) R  ->  C += V_{m+1} Q,
+        U += (Z_m - U E) R^-1."""
+        if self.pending is None:
+            return
+        kc, m, Zm, E, H0 = self.pending
+        self.pending = None
+        dt, dev = self.buf.dtype, self.buf.device
+        Q, R = torch.linalg.qr(torch.as_tensor(H0[:m + 1, :m], dtype=dt, device=dev))
+        if torch.diagonal(R).abs().min().item() == 0.0:
+            return
+        Cn = Q.T @ self.buf[kc:kc + m + 1]
+        Un = Zm - (E[:, :m].T @ self.U[:kc] if kc else 0.0)
+        Un = torch.linalg.solve_triangular(R.T, Un, upper=False)
+        self.buf[kc:kc + m] = Cn
+        self.U[kc:kc + m] = Un
+        self.k = kc + m
+
+
+def gcro(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, precond=None, callback=None,
+         recycle=None):
+    """GMRES with a recycled subspace (GCRO): same stopping rule and result contract as `gmres`
+    (||b - A x||_2 <= max(atol, rtol ||b||_2), info = 0 on convergence); right-preconditioned.
+    CGS2 as in `gmres`, over the combined basis [C; V]: one dot2 and one update sweep per step."""
+    if recycle is None:
+        return gmres(matvec, b, x0=x0, atol=atol, rtol=rtol, restart=restart, maxiter=maxiter, precond=precond,
+                     callback=callback)
+    N = b.numel()
+    dt, dev = b.dtype, b.device
+    restart = min(N, restart or 100)
+    maxiter = maxiter or 10 * N
+    vnorm = lambda t: torch.linalg.vector_norm(t).item()  # noqa: E731
+    x = torch.zeros_like(b) if x0 is None else x0.clone()
+    bnorm = vnorm(b)
+    tol = max(atol, rtol * bnorm)
+    rc = recycle
+    total, matvecs = 0, 0
+    r = b - matvec(x) if x0 is not None else b.clone()
+    matvecs += x0 is not None
+
+    def project(x, r):
+        if rc.k:
+            c = rc.buf[:rc.k] @ r
+            x = x + rc.U[:rc.k].T @ c
+            r = r - rc.buf[:rc.k].T @ c
+        return x, r
+
+    rc.absorb()
+    x, r = project(x, r)
+    beta = vnorm(r)
+    sweeps = _DeviceSweeps(rc.buf) if (rc.buf.is_cuda and dt == torch.float64) else None
+    while True:
+        if beta <= tol:
+            rc.solves += 1
+            return GMRESResult(x, 0, total, beta, matvecs)
+        if total >= maxiter:
+            return GMRESResult(x, total, total, beta, matvecs)
+        if total >= maxiter:
+            return GMRESResult(x, total, total, beta, matvecs)
+        if rc.pending is not None:                    # restart: the finished cycle joins C first
+            rc.absorb()
+            x, r = project(x, r)
+            beta = vnorm(r)
+        if rc.cap - rc.k - 1 < min(restart, 32):      # full: start a new recycle space
+            rc.reset()
+        kc = rc.k
+        m_max = min(restart, rc.cap - kc - 1)
+        full = rc.buf
+        V = full[kc:kc + m_max + 1]
+        Z = torch.empty((m_max, N), dtype=dt, device=dev) if precond is not None else None
+        Gr = torch.zeros((m_max + 1, kc + m_max + 1), dtype=dt, device=dev)   # Gram rows of the V vectors
+        E = torch.zeros((kc, m_max), dtype=dt, device=dev)                     # C^T A z_j
+        H0 = np.zeros((m_max + 1, m_max))                                      # Hessenberg (unrotated)
+        V[0] = r / beta
+        cs, sn = [0.0] * m_max, [0.0] * m_max
+        g = [0.0] * (m_max + 1)
+        g[0] = beta
+        Hr = np.zeros((m_max + 1, m_max))
+        m = 0
+        for j in range(m_max):
+            zj = precond(V[j]) if precond is not None else V[j]
+            if Z is not None:
+                Z[j] = zj
+            w = matvec(zj)
+            matvecs += 1
+            nb = kc + j + 1
+            if sweeps is not None:
+                S = sweeps.dot2(nb, w.contiguous(), V[j])
+                h, gr = S[:, 0].clone(), S[:, 1].clone()
+            else:
+                h, gr = full[:nb] @ w, full[:nb] @ V[j]
+            Gr[j, :nb] = gr
+            # (G h) with G_CC = I and the V rows' Gram rows Gr: both CGS passes' coefficients
+            hC, hV = h[:kc], h[kc:]
+            GV = Gr[:j + 1, :nb]
+            Gh_C = hC + GV[:, :kc].T @ hV
+            Gh_V = GV @ h
+            hh = torch.cat((2.0 * hC - Gh_C, 2.0 * hV - Gh_V))
+            w = w.clone()
+            if sweeps is not None:
+                sweeps.update(nb, hh.contiguous(), w)
+            else:
+                w = w - full[:nb].T @ hh
+            E[:, j] = hh[:kc]
+            col = torch.cat((hh[kc:], torch.linalg.vector_norm(w)[None])).cpu().tolist()
+            hn = col[-1]
+            H0[:j + 2, j] = col
+            for i in range(j):
+                c_, s_ = cs[i], sn[i]
+                a, b_ = col[i], col[i + 1]
+                col[i] = c_ * a + s_ * b_
+                col[i + 1] = -s_ * a + c_ * b_
+            den = math.hypot(col[j], col[j + 1])
+            cs[j], sn[j] = (1.0, 0.0) if den == 0.0 else (col[j] / den, col[j + 1] / den)
+            col[j] = cs[j] * col[j] + sn[j] * col[j + 1]
+            col[j + 1] = 0.0
+            Hr[:j + 2, j] = col
+            g[j + 1] = -sn[j] * g[j]
+            g[j] = cs[j] * g[j]
+            total += 1
+            m = j + 1
+            est = abs(g[j + 1])
+            if callback is not None:
+                callback(est)
+            if hn != 0.0:
+                V[j + 1] = w / hn      # also on the last step: the recycle update uses V_{m+1}
+            if est <= tol or hn == 0.0 or total >= maxiter:
+                break
+        y = np.linalg.solve(np.triu(Hr[:m, :m]), np.asarray(g[:m]))
+        yt = torch.as_tensor(y, dtype=dt, device=dev)
+        Zm = Z[:m] if Z is not None else V[:m]
+        Ey = E[:, :m] @ yt
+        x = x + Zm.T @ yt - (rc.U[:kc].T @ Ey if kc else 0.0)
+        if hn != 0.0 and m > 0:      # this cycle's search space joins the recycle space (deferred)
+            rc.pending = (kc, m, Zm, E, H0)
+        r = b - matvec(x)
+        matvecs += 1
+        x, r = project(x, r)
+        beta = vnorm(r)

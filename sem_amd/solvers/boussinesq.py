@@ -35,6 +35,7 @@ Gauss-Seidel pass of the subsystems' solve_nonlinear, then pure Newton steps.  C
 ||R||_2 <= mtol_nonlin * sqrt(DOF), DOF = 3 N_ns + N_cd (:61-63).
 """
 import math
+import time
 
 import numpy as np
 import torch
@@ -67,6 +68,15 @@ class BoussinesqCoupler:
         self.maxiter = maxiter if maxiter is not None else {'JNK': 100, 'NJ': 1000, 'GS': 1000}[mode]
         self._same_mesh = (cd._P, cd._N_ex, cd._N_ey) == (ns._P, ns._N_ex, ns._N_ey)
         self.iterations = 0
+        self.timing = {k: 0.0 for k in ("residuals", "jacobian_apply", "cd_update", "ns_update")}
+        self.calls = {k: 0 for k in self.timing}
+
+    def _timed(self, key, fn, *a, **kw):
+        t0 = time.perf_counter()
+        r = fn(*a, **kw)
+        self.timing[key] += time.perf_counter() - t0
+        self.calls[key] += 1
+        return r
 
     # ------------------------------------------------------------------ mesh transfers (change_inputs)
     def _to_cd(self, f_ns):
@@ -98,8 +108,11 @@ class BoussinesqCoupler:
     def residuals(self, x):
         """apply_nonlinear of both components (CD :38-39, NS :35-37)."""
         T, u, v, p = self._split(x)
+        t0 = time.perf_counter()
         rT = self.cd._get_residuals(T, self._to_cd(u), self._to_cd(v))
         ru, rv, rp = self.ns._get_residuals(u, v, p, self._to_ns(T))
+        self.timing["residuals"] += time.perf_counter() - t0
+        self.calls["residuals"] += 1
         return self._join(rT, ru, rv, rp)
 
     def linearize(self, x):
@@ -111,17 +124,20 @@ class BoussinesqCoupler:
     def jacobian_apply(self, dx):
         """apply_linear, fwd mode (CD :44-49, NS :42-50): the coupled Jacobian on dx."""
         dT, du, dv, dp = self._split(dx)
+        t0 = time.perf_counter()
         rT = self.cd._get_dresiduals(dT, self._to_cd(du), self._to_cd(dv))
         ru, rv, rp = self.ns._get_dresiduals(du, dv, dp, self._to_ns(dT))
+        self.timing["jacobian_apply"] += time.perf_counter() - t0
+        self.calls["jacobian_apply"] += 1
         return self._join(rT, ru, rv, rp)
 
     def block_jacobi(self, r):
         """LinearBlockJac(maxiter=1): each component's solve_linear on its own residual block
         (CD :51-57, NS :52-60), zero initial guesses."""
         rT, ru, rv, rp = self._split(r)
-        dT = self.cd._get_update(rT, dT0=np.zeros(self.Ncd))
+        dT = self._timed("cd_update", self.cd._get_update, rT, dT0=np.zeros(self.Ncd))
         z = np.zeros(self.Nns)
-        du, dv, dp = self.ns._get_update(ru, rv, rp, du0=z, dv0=z, dp0=z)
+        du, dv, dp = self._timed("ns_update", self.ns._get_update, ru, rv, rp, du0=z, dv0=z, dp0=z)
         return self._join(dT, du, dv, dp)
 
     def gauss_seidel_pass(self, x):
@@ -134,7 +150,7 @@ class BoussinesqCoupler:
     # ------------------------------------------------------------------ solvers
     def _log(self, msg):
         if self.iprint:
-            print(msg)
+            print(msg, flush=True)
 
     def solve(self, x0=None):
         """Run the coupled solve; returns (T, u, v, p) global vectors (NumPy)."""
@@ -177,8 +193,14 @@ class BoussinesqCoupler:
         """GMRES on the coupled Jacobian, block-Jacobi preconditioned (ScipyKrylov :89-91)."""
         mv = lambda t: torch.from_numpy(self.jacobian_apply(t.numpy()))  # noqa: E731
         pc = lambda t: torch.from_numpy(self.block_jacobi(t.numpy()))  # noqa: E731
+        it = [0]
+
+        def cb(presid):
+            it[0] += 1
+            self._log(f'  GMRES {it[0]} ; {presid}')
+
         res = gmres_left(mv, torch.from_numpy(np.ascontiguousarray(b)), atol=self.atol_gmres, rtol=0.0,
-                         restart=self.restart, maxiter=5000, precond=pc)
+                         restart=self.restart, maxiter=5000, precond=pc, callback=cb)
         if res.info != 0:
             raise RuntimeError(f'GMRES failed to converge in {res.info} restarts')
         return res.x.numpy()
@@ -207,5 +229,102 @@ def run(points_plot, L_x, L_y, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4, N_ex_cd=8, N_e
                           mtol_nonlin=mtol_nonlin, AGi=AGi, AGr=AGr, AGc=AGc, mtol_gmres=mtol_gmres, restart=restart,
                           mtol_internal=mtol_internal)
     T, u, v, _ = c.solve()
+    return (np.asarray(c.cd._get_interpol(T, points_plot)), np.asarray(c.ns._get_interpol(u, points_plot)),
+            np.asarray(c.ns._get_interpol(v, points_plot)))
+
+
+class ParallelBoussinesqCoupler(BoussinesqCoupler):
+    """OpenMDAO/Boussinesq_ParallelCoupler.py:12-121: the coupler's two components in an
+    om.ParallelGroup on two ranks -- rank 0 evaluates and solves the convection-diffusion block,
+    rank 1 the Navier-Stokes block, concurrently.  Every component map (residuals, linearize,
+    Jacobian apply, the block-Jacobi solve of the JNK / NJ preconditioner) runs on its owner rank only
+    and the two blocks are reassembled with one all-reduce of the coupled vector (the other rank
+    contributes zeros, so the sum is exact) -- torch.distributed: RCCL under "nccl", gloo on the
+    host.  The Krylov / Newton iteration on the coupled vector then runs identically on both ranks.
+
+    As in a ParallelGroup, the initial "solve_subsystems" pass (and every GS-mode pass) solves both
+    blocks at once from the previous coupling fields (block Jacobi), where the sequential coupler
+    uses the new temperature in the NS solve (block Gauss-Seidel)."""
+
+    def __init__(self, *args, dist=None, group=None, **kw):
+        super().__init__(*args, **kw)
+        if dist is None or dist.get_world_size(group) != 2:
+            raise ValueError("the parallel coupler runs on exactly two ranks (CD on rank 0, NS on rank 1)")
+        self.dist, self.group = dist, group
+        self.rank = dist.get_rank(group)
+
+    def _share(self, part):
+        """The coupled vector from this rank's block (rank 0: T block, rank 1: u, v, p blocks)."""
+        full = torch.zeros(self.DOF, dtype=torch.float64)
+        part = torch.as_tensor(np.asarray(part, dtype=np.float64))
+        if self.rank == 0:
+            full[:self.Ncd] = part
+        else:
+            full[self.Ncd:] = part
+        dev = None
+        if self.dist.get_backend(self.group) == "nccl":   # RCCL reduces device tensors
+            dev = torch.device("cuda", torch.cuda.current_device())
+            full = full.to(dev)
+        self.dist.all_reduce(full, group=self.group)
+        return full.cpu().numpy()
+
+    def residuals(self, x):
+        T, u, v, p = self._split(x)
+        t0 = time.perf_counter()
+        if self.rank == 0:
+            r = self.cd._get_residuals(T, self._to_cd(u), self._to_cd(v))
+        else:
+            r = self._join(*self.ns._get_residuals(u, v, p, self._to_ns(T)))
+        self.timing["residuals"] += time.perf_counter() - t0
+        self.calls["residuals"] += 1
+        return self._share(r)
+
+    def linearize(self, x):
+        T, u, v, _ = self._split(x)
+        if self.rank == 0:
+            self.cd._calc_jacobians(T)
+        else:
+            self.ns._calc_jacobians(u, v)
+
+    def jacobian_apply(self, dx):
+        dT, du, dv, dp = self._split(dx)
+        t0 = time.perf_counter()
+        if self.rank == 0:
+            r = self.cd._get_dresiduals(dT, self._to_cd(du), self._to_cd(dv))
+        else:
+            r = self._join(*self.ns._get_dresiduals(du, dv, dp, self._to_ns(dT)))
+        self.timing["jacobian_apply"] += time.perf_counter() - t0
+        self.calls["jacobian_apply"] += 1
+        return self._share(r)
+
+    def block_jacobi(self, r):
+        rT, ru, rv, rp = self._split(r)
+        if self.rank == 0:
+            d = self._timed("cd_update", self.cd._get_update, rT, dT0=np.zeros(self.Ncd))
+        else:
+            z = np.zeros(self.Nns)
+            d = self._join(*self._timed("ns_update", self.ns._get_update, ru, rv, rp, du0=z, dv0=z, dp0=z))
+        return self._share(d)
+
+    def gauss_seidel_pass(self, x):
+        T, u, v, p = self._split(x)
+        if self.rank == 0:
+            d = self.cd._get_solution(self._to_cd(u), self._to_cd(v), T0=T)
+        else:
+            d = self._join(*self.ns._get_solution(self._to_ns(T), u0=u, v0=v, p0=p))
+        return self._share(d)
+
+
+def run_parallel(points_plot, L_x, L_y, dist, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4, N_ex_cd=8, N_ey_cd=8, P_ns=4,
+                 N_ex_ns=8, N_ey_ns=8, mode='JNK', mtol_nonlin=1e-9, AGi=8, AGr=0.8, AGc=0.2, mtol_gmres=1e-10,
+                 restart=20, mtol_internal=1e-13, group=None):
+    """Drop-in for OpenMDAO/Boussinesq_ParallelCoupler.py:12-121 `run`: rank 0 returns
+    (T_plot, u_plot, v_plot), rank 1 returns (None, None, None), as the reference's MPI gather does."""
+    c = ParallelBoussinesqCoupler(L_x, L_y, Re, Ra, Pr, P_cd, N_ex_cd, N_ey_cd, P_ns, N_ex_ns, N_ey_ns, mode=mode,
+                                  mtol_nonlin=mtol_nonlin, AGi=AGi, AGr=AGr, AGc=AGc, mtol_gmres=mtol_gmres,
+                                  restart=restart, mtol_internal=mtol_internal, dist=dist, group=group)
+    T, u, v, _ = c.solve()
+    if dist.get_rank(group) != 0:
+        return None, None, None
     return (np.asarray(c.cd._get_interpol(T, points_plot)), np.asarray(c.ns._get_interpol(u, points_plot)),
             np.asarray(c.ns._get_interpol(v, points_plot)))

@@ -27,7 +27,7 @@ import torch
 
 from .. import SEM, _lib
 from ..device import get_mesh
-from ..krylov import gmres
+from ..krylov import Recycle, gcro, gmres
 from ..operators import ConvectionTensor, SEMOperator
 
 
@@ -82,7 +82,7 @@ class ConvectionDiffusionSolver:
     def __init__(self, L_x: float, L_y: float, Pe: float, P: int, N_ex: int, N_ey: int,
                  T_W: float = None, T_E: float = None, T_S: float = None, T_N: float = None,
                  mtol=1e-7, iprint: list = [], krylov: str = "device", max_basis: int = 2000,  # noqa: B006
-                 partition=None):
+                 partition=None, recycle_bytes: float = 8e9):
         """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip
         per rank, every apply ends with the interface exchange (overlapped with the interior) and
         the Krylov inner products are all-reduced; the reference methods still take and return
@@ -93,6 +93,9 @@ class ConvectionDiffusionSolver:
             raise ValueError("a partitioned solver needs krylov='device'")
         self._krylov, self._max_basis = krylov, max_basis
         self._part = partition
+        # recycled Krylov subspace across _get_update calls with one operator (sem_amd.krylov.Recycle):
+        # the Boussinesq coupler's block-Jacobi preconditioner solves with the same Sys tens of times
+        self._recycle_bytes, self._recycle = recycle_bytes, None
         self._iprint = iprint
         self._Pe = Pe
         self._mtol = mtol
@@ -151,6 +154,8 @@ class ConvectionDiffusionSolver:
         """res = Sys T, Dirichlet rows T - T_dir (ConvectionDiffusion_Solver.py:73-92)."""
         Conv = self._Pe * (SEM.tensordot(self._C_x, self._dev(u), (1, 0)) + SEM.tensordot(self._C_y, self._dev(v), (1, 0)))
         self._Sys = Conv + self._K
+        if self._recycle is not None:   # the update operator depends on Sys
+            self._recycle.reset()
         y = self._apply(self._dev(T), dir_mode=_lib.DIR_IDENTITY, dir_val=self._dir_val, **self._sys_kw(),
                         **self._dir.kw())
         return self._out(y, T)
@@ -197,9 +202,17 @@ class ConvectionDiffusionSolver:
             if "LGMRES_iter" in self._iprint:
                 print(f"ConvectionDiffusion GMRES: {it[0]}\t{est}")
 
-        r = gmres(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
-                  restart=max(1, min(int(self.N * 0.3), self._max_basis)), callback=cb,
-                  inner=None if self._part is None else self._part.inner)
+        restart = max(1, min(int(self.N * 0.3), self._max_basis))
+        if self._part is not None:
+            r = gmres(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
+                      restart=restart, callback=cb, inner=self._part.inner)
+        else:
+            if self._recycle_bytes and self._recycle is None:
+                n = self._mesh.n_local
+                cap = min(n, max(restart + 1, int(self._recycle_bytes // (16 * n))))
+                self._recycle = Recycle(n, torch.float64, self._mesh.device, cap)
+            r = gcro(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
+                     restart=restart, callback=cb, recycle=self._recycle)
         if r.info != 0:
             raise RuntimeError(f"ConvectionDiffusion LGMRES: Failed to converge in {r.info} iterations")
         self.matvecs = r.matvecs

@@ -23,7 +23,7 @@ import torch
 
 from .. import SEM, _lib
 from ..device import get_mesh
-from ..krylov import gmres
+from ..krylov import Recycle, gcro
 from .convection_diffusion import DirichletRows
 from .velocity_solve import VelocityJacobianSolver
 
@@ -32,8 +32,13 @@ class NavierStokesSolver:
     def __init__(self, L_x: float, L_y: float, Re: float, Gr: float, P: int, N_ex: int, N_ey: int,
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
-                 max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True):
+                 max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
+                 recycle_bytes: float = 16e9):
+        """recycle_bytes: device memory for the recycled Krylov subspace of the Schur-complement solves
+        (sem_amd.krylov.Recycle; 0 disables): consecutive _get_update calls with one linearisation --
+        the Boussinesq coupler's block-Jacobi preconditioner -- start from the earlier solves' spaces."""
         self._iprint = iprint
+        self._recycle_bytes, self._schur_recycle = recycle_bytes, None
         self._velocity_interior, self._velocity_graph = velocity_interior, velocity_graph
         self._max_basis = max_basis
         self._velo = None
@@ -114,6 +119,8 @@ class NavierStokesSolver:
         U, V, Pp, Tt = self._dev(u), self._dev(v), self._dev(p), self._dev(T)
         Conv = self._Re * (SEM.tensordot(self._C_x, U, (1, 0)) + SEM.tensordot(self._C_y, V, (1, 0)))
         self._Sys = self._K + Conv
+        if self._schur_recycle is not None:   # the Schur operator depends on Sys
+            self._schur_recycle.reset()
         kw = self._sys_kw(self._Sys)
         # res_u = Sys u + G_x p, Dirichlet rows u - u_dir
         ru = m.apply(Pp, c_gradx=1.0)
@@ -134,6 +141,8 @@ class NavierStokesSolver:
         self._Jac_u_v = Re * SEM.tensordot(self._C_y, U, (2, 0))
         self._Jac_v_u = Re * SEM.tensordot(self._C_x, V, (2, 0))
         self._velo = None  # factorised on first use, reused until the next linearisation
+        if self._schur_recycle is not None:
+            self._schur_recycle.reset()
 
     def _get_dresiduals(self, du, dv, dp, dT=None):
         """NavierStokes_Solver.py:138-160."""
@@ -219,8 +228,12 @@ class NavierStokesSolver:
             if 'LGMRES_iter' in self._iprint or (prog and it[0] % prog == 0):
                 print(f'NavierStokes GMRES: {it[0]}\t{est}', flush=True)
 
-        r = gmres(schur_mv, b_schur, x0=self._dev(dp0), atol=self._mtol * np.sqrt(self.N), rtol=0.0,
-                  restart=max(1, min(self.N, self._max_basis)), precond=precon, callback=cb)
+        restart = max(1, min(self.N, self._max_basis))
+        if self._recycle_bytes and self._schur_recycle is None:
+            cap = min(self.N, max(restart + 1, int(self._recycle_bytes // (16 * self.N))))
+            self._schur_recycle = Recycle(self.N, torch.float64, self._mesh.device, cap)
+        r = gcro(schur_mv, b_schur, x0=self._dev(dp0), atol=self._mtol * np.sqrt(self.N), rtol=0.0,
+                 restart=restart, precond=precon, callback=cb, recycle=self._schur_recycle)
         if r.info != 0:
             raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {r.info} iterations')
         dp = r.x

@@ -8,7 +8,11 @@ whose reference run is infeasible in this container: the reference's 8-D convect
         mtol = 1e-7) with SciPy LGMRES on the assembled CSR (ConvectionDiffusion_Solver.py:123-170).
         Saved: N, the solution norm, strided samples, the LGMRES matvec count.
 
-Usage:  python tests/golden/make_oracle_fixtures.py cd64      (about 10-20 minutes on one core)
+  ns8:  lid-driven cavity (Examples/NavierStokes_Example.py) at 8 x 8 elements, P = 8, Re = 400: the
+        oracle's Newton iteration with SuperLU velocity solves and the Schur-complement LGMRES
+        (NavierStokes_Solver.py:162-270).  Saved: u, v, p, the Newton count and residual history.
+
+Usage:  python tests/golden/make_oracle_fixtures.py cd64|ns8      (cd64: ~6 minutes, ns8: ~40 s)
 """
 import os
 import sys
@@ -48,5 +52,15 @@ def gen_cd64():
     print("cd64", ref.N, count[0], np.linalg.norm(T), time.perf_counter() - t0)
 
 
+def gen_ns8():
+    from oracle import sem_oracle as O
+    P, ne, Re = 8, 8, 400.0
+    ns = O.NSOracle(1.0, 1.0, Re, 0.0, P, ne, ne, u_N=1.0)
+    u, v, p, hist = ns.solution(np.zeros(ns.N), mtol=1e-7, mtol_newton=1e-5)
+    np.savez_compressed(os.path.join(HERE, "ns8_re400.npz"), u=u, v=v, p=p, newton_iters=np.array(len(hist) - 1),
+                        res_history=np.array([h[0] for h in hist]), schur_matvecs=np.array([h[1] for h in hist]))
+    print("ns8", ns.N, len(hist) - 1, [h[0] for h in hist])
+
+
 if __name__ == "__main__":
-    {"cd64": gen_cd64}[sys.argv[1]]()
+    {"cd64": gen_cd64, "ns8": gen_ns8}[sys.argv[1]]()

@@ -1,6 +1,7 @@
 """Device GMRES (sem_amd/krylov.py) on CPU tensors against SciPy, on the reference's own
 CD and NS-like systems built by the oracle (the algorithm is device-agnostic)."""
 import numpy as np
+import pytest
 import scipy.sparse.linalg as spla
 import torch
 
@@ -73,3 +74,54 @@ def test_gmres_left_cd_system():
     mv = lambda v: torch.from_numpy(A.matvec(v.numpy()))  # noqa: E731
     r = gmres_left(mv, torch.from_numpy(b), atol=atol, restart=20, maxiter=5000)
     assert r.info == 0 and np.linalg.norm(A.matvec(r.x.numpy()) - b) <= atol
+
+
+def test_gmres_basis_stays_orthonormal_on_ill_conditioned_system():
+    """the Gram-matrix second pass of CGS2 cannot see the rounding error of the first
+    subtraction.  On a badly conditioned, non-normal system (Krylov vectors nearly dependent, the
+    first pass cancelling strongly) the basis must stay orthonormal and the true residual must meet
+    the tolerance."""
+    import torch
+    from sem_amd.krylov import gmres
+    n = 400
+    g = torch.Generator().manual_seed(0)
+    Q, _ = torch.linalg.qr(torch.randn(n, n, dtype=torch.float64, generator=g))
+    ev = torch.logspace(-8, 0, n, dtype=torch.float64)              # cond 1e8
+    A = Q @ torch.diag(ev) @ Q.T + 1e-3 * torch.triu(torch.randn(n, n, dtype=torch.float64, generator=g), 1)
+    b = torch.randn(n, dtype=torch.float64, generator=g)
+    basis = []
+    r = gmres(lambda v: A @ v, b, atol=1e-10 * torch.linalg.vector_norm(b).item(), restart=n, basis_out=basis)
+    assert r.info == 0
+    assert torch.linalg.vector_norm(A @ r.x - b).item() <= 1.0001e-10 * torch.linalg.vector_norm(b).item()
+    for V in basis:
+        E = V @ V.T - torch.eye(V.shape[0], dtype=torch.float64)
+        assert E.abs().max().item() < 1e-10, E.abs().max().item()
+
+
+@pytest.mark.parametrize("precond", [False, True])
+def test_gcro_recycling_sequence(precond):
+    """sem_amd.krylov.gcro with a Recycle: every solve of a sequence with one operator meets the
+    tolerance, the recycle space keeps A U = C and C^T C = I, and later solves of related right-hand
+    sides take no more iterations than the first."""
+    import torch
+    from sem_amd.krylov import Recycle, gcro
+    n = 500
+    g = torch.Generator().manual_seed(3)
+    A = (torch.eye(n, dtype=torch.float64) * 2 + 0.3 * torch.randn(n, n, dtype=torch.float64, generator=g) / n ** 0.5
+         + torch.diag(torch.linspace(0, 5, n, dtype=torch.float64)))
+    M = 1.0 / torch.linspace(1, 3, n, dtype=torch.float64)
+    pc = (lambda v: M * v) if precond else None
+    rc = Recycle(n, torch.float64, "cpu", 400)
+    b = torch.randn(n, dtype=torch.float64, generator=g)
+    its = []
+    for _ in range(6):
+        r = gcro(lambda v: A @ v, b, atol=1e-10, restart=30, precond=pc, recycle=rc)
+        assert r.info == 0 and torch.linalg.vector_norm(A @ r.x - b).item() <= 1.0001e-10
+        its.append(r.iters)
+        b = b + 0.2 * torch.randn(n, dtype=torch.float64, generator=g)
+    rc.absorb()
+    C, U = rc.buf[:rc.k], rc.U[:rc.k]
+    assert (C @ C.T - torch.eye(rc.k, dtype=torch.float64)).abs().max().item() < 1e-12
+    AU = (A @ (U.T)).T
+    assert (AU - C).abs().max().item() < 1e-12
+    assert max(its[1:]) <= its[0]
