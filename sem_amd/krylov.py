@@ -315,29 +315,37 @@ class Recycle:
         self.k = 0
         self.solves = 0
         self.pending = None
+        # singular values kept when a cycle joins the space: U = (Z - U E) W S^-1 grows like 1 / s_min,
+        # and the rounding error of the projection x0 = U C^T b with it
+        self.rcond = 1e-4
+        self.first_iters = None   # iterations of the first solve after a reset (stagnation guard)
 
     def reset(self):
         self.k = 0
         self.pending = None
+        self.first_iters = None
 
     def absorb(self):
         """Append the last cycle's search space (deferred until the space is used again, so a lone
-        solve pays nothing): A (Z_m - U E) = V_{m+1} H_m = (V_{m+1} Q) R  ->  C += V_{m+1} Q,
-        U += (Z_m - U E) R^-1."""
+        solve pays nothing): A (Z_m - U E) = V_{m+1} H_m."""
         if self.pending is None:
             return
         kc, m, Zm, E, H0 = self.pending
         self.pending = None
         dt, dev = self.buf.dtype, self.buf.device
-        Q, R = torch.linalg.qr(torch.as_tensor(H0[:m + 1, :m], dtype=dt, device=dev))
-        if torch.diagonal(R).abs().min().item() == 0.0:
+        # H_m = P S W^T (thin SVD); directions with tiny singular values (the operator's near-null space,
+        # e.g. the spurious pressure modes of the NS Schur complement) are left out, so U stays bounded:
+        # A (Z_m - U E) W_r S_r^-1 = V_{m+1} P_r
+        P, S, Wt = torch.linalg.svd(torch.as_tensor(H0[:m + 1, :m], dtype=dt, device=dev), full_matrices=False)
+        keep = int((S > S[0] * self.rcond).sum().item())
+        if keep == 0:
             return
-        Cn = Q.T @ self.buf[kc:kc + m + 1]
+        Cn = P[:, :keep].T @ self.buf[kc:kc + m + 1]
         Un = Zm - (E[:, :m].T @ self.U[:kc] if kc else 0.0)
-        Un = torch.linalg.solve_triangular(R.T, Un, upper=False)
-        self.buf[kc:kc + m] = Cn
-        self.U[kc:kc + m] = Un
-        self.k = kc + m
+        Un = (Wt[:keep] / S[:keep, None]) @ Un
+        self.buf[kc:kc + keep] = Cn
+        self.U[kc:kc + keep] = Un
+        self.k = kc + keep
 
 
 def gcro(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, precond=None, callback=None,
@@ -375,11 +383,15 @@ def gcro(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pre
     while True:
         if beta <= tol:
             rc.solves += 1
+            if rc.first_iters is None:
+                rc.first_iters = total
             return GMRESResult(x, 0, total, beta, matvecs)
         if total >= maxiter:
             return GMRESResult(x, total, total, beta, matvecs)
-        if total >= maxiter:
-            return GMRESResult(x, total, total, beta, matvecs)
+        if rc.k and rc.first_iters is not None and total > 2 * rc.first_iters + restart:
+            # stagnation (the recycled space limits the attainable accuracy): continue as plain GMRES
+            rc.reset()
+            rc.first_iters = 0
         if rc.pending is not None:                    # restart: the finished cycle joins C first
             rc.absorb()
             x, r = project(x, r)
@@ -413,6 +425,7 @@ def gcro(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pre
             else:
                 h, gr = full[:nb] @ w, full[:nb] @ V[j]
             Gr[j, :nb] = gr
+            Gr[:j, kc + j] = gr[kc:kc + j]          # G_VV is symmetric: fill the new column too
             # (G h) with G_CC = I and the V rows' Gram rows Gr: both CGS passes' coefficients
             hC, hV = h[:kc], h[kc:]
             GV = Gr[:j + 1, :nb]

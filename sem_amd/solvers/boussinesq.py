@@ -135,9 +135,14 @@ class BoussinesqCoupler:
         """LinearBlockJac(maxiter=1): each component's solve_linear on its own residual block
         (CD :51-57, NS :52-60), zero initial guesses."""
         rT, ru, rv, rp = self._split(r)
+        t0 = time.perf_counter()
         dT = self._timed("cd_update", self.cd._get_update, rT, dT0=np.zeros(self.Ncd))
+        t1 = time.perf_counter()
         z = np.zeros(self.Nns)
         du, dv, dp = self._timed("ns_update", self.ns._get_update, ru, rv, rp, du0=z, dv0=z, dp0=z)
+        if self.iprint >= 2:
+            self._log(f'    block-Jacobi: CD {getattr(self.cd, "matvecs", "?")} matvecs {t1 - t0:.3f} s, '
+                      f'NS {getattr(self.ns, "schur_matvecs", "?")} Schur matvecs {time.perf_counter() - t1:.3f} s')
         return self._join(dT, du, dv, dp)
 
     def gauss_seidel_pass(self, x):

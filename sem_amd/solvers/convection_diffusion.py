@@ -82,7 +82,7 @@ class ConvectionDiffusionSolver:
     def __init__(self, L_x: float, L_y: float, Pe: float, P: int, N_ex: int, N_ey: int,
                  T_W: float = None, T_E: float = None, T_S: float = None, T_N: float = None,
                  mtol=1e-7, iprint: list = [], krylov: str = "device", max_basis: int = 2000,  # noqa: B006
-                 partition=None, recycle_bytes: float = 8e9):
+                 partition=None, recycle_bytes: float = 0.0):
         """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip
         per rank, every apply ends with the interface exchange (overlapped with the interior) and
         the Krylov inner products are all-reduced; the reference methods still take and return
@@ -197,10 +197,12 @@ class ConvectionDiffusionSolver:
         x0 = self._dev(dT0)
         it = [0]
 
+        prog = getattr(self, "_progress", 0)
+
         def cb(est):
             it[0] += 1
-            if "LGMRES_iter" in self._iprint:
-                print(f"ConvectionDiffusion GMRES: {it[0]}\t{est}")
+            if "LGMRES_iter" in self._iprint or (prog and it[0] % prog == 0):
+                print(f"ConvectionDiffusion GMRES: {it[0]}\t{est}", flush=True)
 
         restart = max(1, min(int(self.N * 0.3), self._max_basis))
         if self._part is not None:

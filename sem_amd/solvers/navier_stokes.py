@@ -33,10 +33,14 @@ class NavierStokesSolver:
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
                  max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
-                 recycle_bytes: float = 16e9):
-        """recycle_bytes: device memory for the recycled Krylov subspace of the Schur-complement solves
-        (sem_amd.krylov.Recycle; 0 disables): consecutive _get_update calls with one linearisation --
-        the Boussinesq coupler's block-Jacobi preconditioner -- start from the earlier solves' spaces."""
+                 recycle_bytes: float = 0.0):
+        """recycle_bytes: device memory for a recycled Krylov subspace of the Schur-complement solves
+        (sem_amd.krylov.Recycle, GCRO; 0 = off, the default): consecutive _get_update calls with one
+        linearisation -- the Boussinesq coupler's block-Jacobi preconditioner -- then start from the
+        earlier solves' spaces.  Measured (tools/recycle_probe.py, profiles/r02/bous): 5-8x fewer Schur
+        matvecs on consistent right-hand sides, but the Arnoldi-relation error of the recycled space
+        puts a floor near 1e-8 relative under the residual, above the couplers' mtol_internal = 1e-13,
+        so inside the coupler it stagnates; off by default."""
         self._iprint = iprint
         self._recycle_bytes, self._schur_recycle = recycle_bytes, None
         self._velocity_interior, self._velocity_graph = velocity_interior, velocity_graph

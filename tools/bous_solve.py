@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--continuation", default="")
     ap.add_argument("--mtol-internal", type=float, default=1e-13)
     ap.add_argument("--out", default="")
+    ap.add_argument("--iprint", type=int, default=1)
     ap.add_argument("--x0", default="", help="start from a saved state (.npy of [T, u, v, p])")
     ap.add_argument("--ckpt", default="", help="directory for each finished stage's state (bous_<ne>_<Ra>.npy)")
     args = ap.parse_args()
@@ -40,7 +41,9 @@ def main():
     for Ra in [float(r) for r in args.continuation.split(",") if r] + [args.Ra]:
         t0 = time.perf_counter()
         c = BoussinesqCoupler(1.0, 1.0, args.Re, Ra, args.Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
-                              mode=args.mode, mtol_internal=args.mtol_internal, iprint=1)
+                              mode=args.mode, mtol_internal=args.mtol_internal, iprint=args.iprint)
+        if args.iprint >= 2:
+            c.cd._progress = c.ns._progress = 500
         T, u, v, p = c.solve(x)
         x = np.concatenate((T, u, v, p))
         dt = time.perf_counter() - t0
