@@ -189,12 +189,21 @@ struct CList {
 
 template <int P, int NS>
 __device__ const typename CList<P, NS>::Tab kBandCoef = CList<P, NS>::make();
+// the same lists in the constant address space: read with wave-uniform compile-time offsets, they
+// become scalar-memory loads (s_load through the scalar cache) instead of two s_mov_b32 per fp64
+// immediate (coefficient mode CM = 2)
+template <int P, int NS>
+__constant__ typename CList<P, NS>::Tab kBandCoefC = CList<P, NS>::make();
 
-// acc + c * x: an immediate coefficient (c), or entry IDX of the split's DPP-broadcast list.  Only
-// valid with every lane of the wave active (a DPP read of a disabled lane does not return its value).
-template <bool DPP, int IDX, int NCV>
+// acc + c * x with the coefficient of entry IDX of split S's list: CM = 0 an fp64 immediate (two
+// s_mov_b32 into an SGPR pair), CM = 1 a DPP broadcast from the split's VGPR-resident list (only valid
+// with every lane of the wave active: a DPP read of a disabled lane does not return its value),
+// CM = 2 a scalar load from the constant-memory copy of the list.
+template <int CM, int P, int NS, int S, int IDX, int NCV>
 __device__ __forceinline__ double cfma(const double (&cv)[NCV], double c, double x, double acc) {
-  if constexpr (DPP) {
+  if constexpr (CM == 2) {
+    return fma(kBandCoefC<P, NS>.v[S * CList<P, NS>::NPAD + IDX], x, acc);
+  } else if constexpr (CM == 1) {
     asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
         : "+v"(acc)
         : "v"(cv[IDX / 16]), "v"(x), "n"(IDX % 16));
@@ -207,7 +216,7 @@ __device__ __forceinline__ double cfma(const double (&cv)[NCV], double c, double
 // Rows of split S of one element from a (2P+1)-node window t (t[P..2P] = the element, t[0..P] = the
 // left neighbour; absent elements are zero in the staged tile).  fk = hasL + hasR and
 // fg = hasR - hasL weight the shared node t[P] in row 0.  Results go to slots (EPlan order).
-template <int P, int NS, int S, bool DPP, int NR, int NCV>
+template <int P, int NS, int S, int CM, int NR, int NCV>
 __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk, double fg, double (&k)[NR],
                                         double (&g)[NR], const double (&cv)[NCV]) {
   using E = EOC<P>;
@@ -234,8 +243,8 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
         for_rows(std::make_integer_sequence<int, P>{}, [&](auto MI) {
           constexpr int m = decltype(MI)::value + 1;
           constexpr double km = E::Ks(0, m), gm = E::G(0, m);
-          kv = cfma<DPP, cb + 2 * (m - 1)>(cv, km, t[P + m] + t[P - m], kv);
-          gv = cfma<DPP, cb + 2 * (m - 1) + 1>(cv, gm, t[P + m] - t[P - m], gv);
+          kv = cfma<CM, P, NS, S, cb + 2 * (m - 1)>(cv, km, t[P + m] + t[P - m], kv);
+          gv = cfma<CM, P, NS, S, cb + 2 * (m - 1) + 1>(cv, gm, t[P + m] - t[P - m], gv);
         });
         k[sl] = kv;
         g[sl] = gv;
@@ -244,15 +253,15 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
         for_rows(std::make_integer_sequence<int, H>{}, [&](auto MI) {
           constexpr int m = decltype(MI)::value;
           constexpr double sk = E::SK(it, m), dk = E::DK(it, m), sg = E::SG(it, m), dg = E::DG(it, m);
-          Ek = cfma<DPP, cb + 4 * m>(cv, sk, e[m], Ek);
-          Ok = cfma<DPP, cb + 4 * m + 1>(cv, dk, o[m], Ok);
-          Eg = cfma<DPP, cb + 4 * m + 2>(cv, sg, e[m], Eg);
-          Og = cfma<DPP, cb + 4 * m + 3>(cv, dg, o[m], Og);
+          Ek = cfma<CM, P, NS, S, cb + 4 * m>(cv, sk, e[m], Ek);
+          Ok = cfma<CM, P, NS, S, cb + 4 * m + 1>(cv, dk, o[m], Ok);
+          Eg = cfma<CM, P, NS, S, cb + 4 * m + 2>(cv, sg, e[m], Eg);
+          Og = cfma<CM, P, NS, S, cb + 4 * m + 3>(cv, dg, o[m], Og);
         });
         if constexpr (E::EVEN) {
           constexpr double kc_ = E::Ks(it, E::c), gc_ = E::G(it, E::c);
-          Ek = cfma<DPP, cb + 4 * H>(cv, kc_, t[P + E::c], Ek);
-          Eg = cfma<DPP, cb + 4 * H + 1>(cv, gc_, t[P + E::c], Eg);
+          Ek = cfma<CM, P, NS, S, cb + 4 * H>(cv, kc_, t[P + E::c], Ek);
+          Eg = cfma<CM, P, NS, S, cb + 4 * H + 1>(cv, gc_, t[P + E::c], Eg);
         }
         k[sl] = Ek + Ok;
         k[sl + 1] = Ek - Ok;
@@ -263,12 +272,12 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
         for_rows(std::make_integer_sequence<int, H>{}, [&](auto MI) {
           constexpr int m = decltype(MI)::value;
           constexpr double sk = E::SK(E::c, m), dg = E::DG(E::c, m);
-          kv = cfma<DPP, cb + 2 * m>(cv, sk, e[m], kv);
-          gv = cfma<DPP, cb + 2 * m + 1>(cv, dg, o[m], gv);
+          kv = cfma<CM, P, NS, S, cb + 2 * m>(cv, sk, e[m], kv);
+          gv = cfma<CM, P, NS, S, cb + 2 * m + 1>(cv, dg, o[m], gv);
         });
         constexpr double kcc = E::Ks(E::c, E::c), gcc = E::G(E::c, E::c);
-        kv = cfma<DPP, cb + 2 * H>(cv, kcc, t[P + E::c], kv);
-        if constexpr (gcc != 0.0) gv = cfma<DPP, cb + 2 * H + 1>(cv, gcc, t[P + E::c], gv);
+        kv = cfma<CM, P, NS, S, cb + 2 * H>(cv, kcc, t[P + E::c], kv);
+        if constexpr (gcc != 0.0) gv = cfma<CM, P, NS, S, cb + 2 * H + 1>(cv, gcc, t[P + E::c], gv);
         k[sl] = kv;
         g[sl] = gv;
       }
@@ -416,7 +425,7 @@ __device__ __forceinline__ double gll_w(int J) {
 // the tile-mapping integers) arrive as separate values: from the struct (apply_band) or as leading
 // scalar kernel arguments that the command processor preloads into SGPRs (apply_band_kp, KP =
 // true), so the first staging load does not wait for a kernarg memory fetch.
-template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD, bool KP>
+template <int P, int TXE, int TYE, int NS, bool FULL, int CM, bool GRAD, bool KP>
 __device__ __forceinline__ void band_body(const double* __restrict__ px, const double* __restrict__ pcu,
                                           const double* __restrict__ pcv, int pNY, int plb0, int pex_begin,
                                           int pex_end, int pney, int pnblk, int ptiles_y, int pnbytes,
@@ -424,6 +433,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   using C = BCfg<P, TXE, TYE, NS>;
   using PL = EPlan<P, NS>;
   using CL = CList<P, NS>;
+  constexpr bool DPP = CM == 1;
   constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW;
   __shared__ double Ts[C::RX * PT];
   __shared__ double XK[BX * PY];
@@ -568,7 +578,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
 #pragma unroll
         for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
         double k[C::RP], g[C::RP];
-        eo_rows<P, NS, s, DPP>(t, fk, fg, k, g, cv);
+        eo_rows<P, NS, s, CM>(t, fk, fg, k, g, cv);
 #pragma unroll
         for (int sl = 0; sl < PL::nrows(s); ++sl) {
           const int i = PL::row(s, sl);
@@ -604,7 +614,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
 #pragma unroll
         for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
         double k[C::RP], g[C::RP];
-        eo_rows<P, NS, hh, DPP>(t, fk, fg, k, g, cv);
+        eo_rows<P, NS, hh, CM>(t, fk, fg, k, g, cv);
         if (yok) {
 #pragma unroll
           for (int sl = 0; sl < PL::nrows(hh); ++sl) {
@@ -668,7 +678,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
 #undef BSTAMP
 }
 
-template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD = true>
+template <int P, int TXE, int TYE, int NS, bool FULL, int CM, bool GRAD = true>
 __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(const BandArgs a) {
   BPIN(a.x);
   BPIN(a.y);
@@ -696,18 +706,18 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band(c
   if constexpr (kDiag) BPIN(a.stamps);
   BPIN(a.nblk);
   BPIN(a.cpol);
-  band_body<P, TXE, TYE, NS, FULL, DPP, GRAD, false>(a.x, (a.flags & 1) ? a.cu : nullptr, (a.flags & 2) ? a.cv : nullptr,
+  band_body<P, TXE, TYE, NS, FULL, CM, GRAD, false>(a.x, (a.flags & 1) ? a.cu : nullptr, (a.flags & 2) ? a.cv : nullptr,
                                                      a.NY, a.lb0, a.ex_begin, a.ex_end, a.ney, a.nblk, a.tiles_y,
                                                      a.nbytes, a);
 }
 
 // Same kernel with the prologue's fields as leading scalar arguments (14 SGPRs, preloaded by the
 // command processor when the code object asks for it: -amdgpu-kernarg-preload-count in build.py).
-template <int P, int TXE, int TYE, int NS, bool FULL, bool DPP, bool GRAD = true>
+template <int P, int TXE, int TYE, int NS, bool FULL, int CM, bool GRAD = true>
 __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band_kp(
     const double* px, const double* pcu, const double* pcv, int pNY, int plb0, int pex_begin, int pex_end, int pney,
     int pnblk, int ptiles_y, int pnbytes, const BandArgs a) {
-  band_body<P, TXE, TYE, NS, FULL, DPP, GRAD, true>(px, pcu, pcv, pNY, plb0, pex_begin, pex_end, pney, pnblk, ptiles_y,
+  band_body<P, TXE, TYE, NS, FULL, CM, GRAD, true>(px, pcu, pcv, pNY, plb0, pex_begin, pex_end, pney, pnblk, ptiles_y,
                                                     pnbytes, a);
 }
 
@@ -886,7 +896,7 @@ __global__ __launch_bounds__((BCfg<P, 1, TYE, NS>::THREADS)) void apply_march(co
 #pragma unroll
         for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
         double k[C::RP], g[C::RP];
-        eo_rows<P, NS, s, DPP>(t, fk, fg, k, g, cv);
+        eo_rows<P, NS, s, DPP ? 1 : 0>(t, fk, fg, k, g, cv);
 #pragma unroll
         for (int sl = 0; sl < PL::nrows(s); ++sl) {
           const int i = PL::row(s, sl);
@@ -918,7 +928,7 @@ __global__ __launch_bounds__((BCfg<P, 1, TYE, NS>::THREADS)) void apply_march(co
 #pragma unroll
           for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
           double k[C::RP], g[C::RP];
-          eo_rows<P, NS, hh, DPP>(t, fk, fg, k, g, cv);
+          eo_rows<P, NS, hh, DPP ? 1 : 0>(t, fk, fg, k, g, cv);
           if (yok) {
 #pragma unroll
             for (int sl = 0; sl < PL::nrows(hh); ++sl) {
@@ -995,7 +1005,7 @@ static int hip_check_b(hipError_t e, const char* what) {
 // that costs ~1 %, and non-temporal u, v loads (read once) are neutral to slightly better.
 static int band_cpol(long long n_local) { return 32LL * n_local < (128LL << 20) ? 3 : 256; }
 
-template <int P, int TXE, int TYE, int NS, bool DPP = false>
+template <int P, int TXE, int TYE, int NS, int CM = 0>
 static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   using C = BCfg<P, TXE, TYE, NS>;
   const int ncols = h->ex_end - h->ex_begin;
@@ -1051,24 +1061,24 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   if (tune(SEM_TUNE_BAND_KP) >= 0 && !ranged) {  // -1 (SEM_BAND_KP=0): struct-only arguments (A/B)
 #define SEM_KP_ARGS b.x, b.cu, b.cv, b.NY, b.lb0, b.ex_begin, b.ex_end, b.ney, b.nblk, b.tiles_y, b.nbytes, b
     if (full && grad)
-      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, DPP, true>), grid, block, 0, s, SEM_KP_ARGS);
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, CM, true>), grid, block, 0, s, SEM_KP_ARGS);
     else if (full)
-      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, DPP, false>), grid, block, 0, s, SEM_KP_ARGS);
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, true, CM, false>), grid, block, 0, s, SEM_KP_ARGS);
     else if (grad)
-      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, false, DPP, true>), grid, block, 0, s, SEM_KP_ARGS);
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, false, CM, true>), grid, block, 0, s, SEM_KP_ARGS);
     else
-      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, false, DPP, false>), grid, block, 0, s, SEM_KP_ARGS);
+      hipLaunchKernelGGL((apply_band_kp<P, TXE, TYE, NS, false, CM, false>), grid, block, 0, s, SEM_KP_ARGS);
 #undef SEM_KP_ARGS
     return hip_check_b(hipGetLastError(), "apply (band) launch");
   }
   if (full && grad)
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, DPP, true>), grid, block, 0, s, b);
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, CM, true>), grid, block, 0, s, b);
   else if (full)
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, DPP, false>), grid, block, 0, s, b);
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, true, CM, false>), grid, block, 0, s, b);
   else if (grad)
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, DPP, true>), grid, block, 0, s, b);
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, CM, true>), grid, block, 0, s, b);
   else
-    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, DPP, false>), grid, block, 0, s, b);
+    hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, CM, false>), grid, block, 0, s, b);
   return hip_check_b(hipGetLastError(), "apply (band) launch");
 }
 
@@ -1155,20 +1165,21 @@ static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStrea
   if constexpr (P == 8) {
     if (force == 1) return launch_band<P, 1, S::TYE, 4>(args, h, s);
     if (force == 2) return launch_band<P, 2, S::TYE, 4>(args, h, s);
-    if (force == 5) return launch_band<P, 2, S::TYE, 2, true>(args, h, s);
-    if (force == 6) return launch_band<P, 1, S::TYE, 1, true>(args, h, s);
+    if (force == 5) return launch_band<P, 2, S::TYE, 2, 1>(args, h, s);
+    if (force == 6) return launch_band<P, 1, S::TYE, 1, 1>(args, h, s);
   }
   if constexpr (P == 8 || P == 12) {  // the marching variant covers whole strips only
     if (force == 7 && args.pos1 == 0) return launch_march<P, S::TYE, S::NS, false>(args, h, s);
     if (force == 8 && args.pos1 == 0) return launch_march<P, S::TYE, S::NS, true>(args, h, s);
   }
-  if (force == 3) return launch_band<P, S::TXE, S::TYE, S::NS, true>(args, h, s);
-  if (force == 4) return launch_band<P, S::TXE, S::TYE, S::NS, false>(args, h, s);
+  if (force == 3) return launch_band<P, S::TXE, S::TYE, S::NS, 1>(args, h, s);
+  if (force == 4) return launch_band<P, S::TXE, S::TYE, S::NS, 0>(args, h, s);
+  if (force == 9) return launch_band<P, S::TXE, S::TYE, S::NS, 2>(args, h, s);  // scalar-load coefficients
   // DPP-broadcast coefficients: 2-4 % faster from ~1M DOFs up (the VALU-bound regime), 2-3 % slower on
   // the launch-latency-bound cfg2 mesh, whose extra coefficient loads sit on the critical path
   // (profiles/r01/band/dpp_ab.txt)
-  if (args.n_local32 >= (1 << 20)) return launch_band<P, S::TXE, S::TYE, S::NS, true>(args, h, s);
-  return launch_band<P, S::TXE, S::TYE, S::NS>(args, h, s);
+  if (args.n_local32 >= (1 << 20)) return launch_band<P, S::TXE, S::TYE, S::NS, 1>(args, h, s);
+  return launch_band<P, S::TXE, S::TYE, S::NS, 0>(args, h, s);
 }
 
 std::string band_kernel_name(int P, long long n_local) {
@@ -1176,12 +1187,13 @@ std::string band_kernel_name(int P, long long n_local) {
   const int NS = P >= 2 ? 2 : 1;
   const int force = tune(SEM_TUNE_BAND_TILE);
   const bool dpp = force == 3 || force == 8 || (force == 0 && n_local >= (1 << 20));
+  const bool smem = force == 9;
   if (force == 7 || force == 8)
     return "sem::apply_march<" + std::to_string(P) + ", " + std::to_string(TYE) + ", " + std::to_string(NS) +
            (dpp ? ", dpp" : "") + ">";
   const bool kp = tune(SEM_TUNE_BAND_KP) >= 0;
   return std::string(kp ? "sem::apply_band_kp<" : "sem::apply_band<") + std::to_string(P) + ", " + std::to_string(TXE) +
-         ", " + std::to_string(TYE) + ", " + std::to_string(NS) + (dpp ? ", dpp" : "") + ">";
+         ", " + std::to_string(TYE) + ", " + std::to_string(NS) + (dpp ? ", dpp" : "") + (smem ? ", smem" : "") + ">";
 }
 
 int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s) {

@@ -157,10 +157,14 @@ class BoussinesqCoupler:
         if self.iprint:
             print(msg, flush=True)
 
-    def solve(self, x0=None):
-        """Run the coupled solve; returns (T, u, v, p) global vectors (NumPy)."""
+    def solve(self, x0=None, checkpoint=None, resume=False):
+        """Run the coupled solve; returns (T, u, v, p) global vectors (NumPy).
+        checkpoint(x, k): called after every nonlinear iteration (long runs save their state);
+        resume=True: x0 is such a saved state -- continue the Newton iteration without the initial
+        subsystem pass."""
         x = np.zeros(self.DOF) if x0 is None else np.array(x0, dtype=np.float64)
-        x = self._solve_gs(x) if self.mode == 'GS' else self._solve_newton(x)
+        self._checkpoint = checkpoint
+        x = self._solve_gs(x) if self.mode == 'GS' else self._solve_newton(x, initial_pass=not resume)
         return tuple(np.array(a) for a in self._split(x))
 
     def _solve_gs(self, x):
@@ -173,8 +177,9 @@ class BoussinesqCoupler:
                 return x
         raise RuntimeError(f'NLBGS failed to converge in {self.maxiter} iterations')
 
-    def _solve_newton(self, x):
-        x = self.gauss_seidel_pass(x)  # solve_subsystems=True, max_sub_solves=0: at iteration 0 only
+    def _solve_newton(self, x, initial_pass=True):
+        if initial_pass:
+            x = self.gauss_seidel_pass(x)  # solve_subsystems=True, max_sub_solves=0: at iteration 0 only
         r = self.residuals(x)
         norm = np.linalg.norm(r)
         self._log(f'Newton 0 ; {norm}')
@@ -191,6 +196,8 @@ class BoussinesqCoupler:
                 x, r, norm = self._armijo_goldstein(x, self.block_jacobi(-r), norm)
             k += 1
             self._log(f'Newton {k} ; {norm}')
+            if getattr(self, "_checkpoint", None) is not None:
+                self._checkpoint(x, k)
         self.iterations = k
         return x
 

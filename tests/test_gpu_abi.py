@@ -72,7 +72,7 @@ def test_tuning_knobs_do_not_change_results(gpu, tuning):
               dir_sides=_lib.SIDE_W | _lib.SIDE_E)
     base = mesh.apply(X, **kw)
     for knob, vals in ((_lib.TUNE_BAND_CPOL, (1, 2, 3, 4, 256)), (_lib.TUNE_BAND_KP, (-1, 0)),
-                       (_lib.TUNE_BAND_TILE, (1, 2, 3, 4, 5, 6, 7, 8))):
+                       (_lib.TUNE_BAND_TILE, (1, 2, 3, 4, 5, 6, 7, 8, 9))):
         for v in vals:
             tuning(knob, v)
             assert torch.equal(mesh.apply(X, **kw), base), (knob, v)

@@ -70,9 +70,9 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
          (8, 17, 5), (9, 3, 4), (10, 2, 2), (11, 3, 1), (12, 5, 3), (13, 2, 3), (14, 1, 2), (15, 2, 2), (16, 3, 2)]
 
 
-ALGOS = [1, 2, 3, 4, "4dpp", "4m", "4mdpp"]  # VALU two-phase, MFMA, column kernel, assembled band (+ DPP coefficient variant)
+ALGOS = [1, 2, 3, 4, "4dpp", "4m", "4mdpp", "4smem"]  # VALU two-phase, MFMA, column kernel, assembled band (+ DPP coefficient variant)
 BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2", "4t5": "5", "4t6": "6", "4imm": "4",
-                 "4m": "7", "4mdpp": "8"}  # 4m*: marching kernel (P = 8, 12; other P fall back to the band tile)  # SEM_TUNE_BAND_TILE values
+                 "4m": "7", "4mdpp": "8", "4smem": "9"}  # 4m*: marching kernel (P = 8, 12; other P fall back to the band tile)  # SEM_TUNE_BAND_TILE values
 
 
 def _algo(algo, tuning):
@@ -178,7 +178,8 @@ def test_band_variants_bitwise_equal(gpu, P, nex, ney, tuning):
               dir_sides=_lib.SIDE_W | _lib.SIDE_E, algo=4)
     tuning(_lib.TUNE_BAND_TILE, 0)
     base = mesh.apply(X, **kw)
-    for name in (["4dpp", "4imm", "4t1", "4t2", "4t5", "4t6", "4m", "4mdpp"] if P in (8, 12) else ["4dpp", "4imm"]):
+    for name in (["4dpp", "4imm", "4t1", "4t2", "4t5", "4t6", "4m", "4mdpp", "4smem"] if P in (8, 12)
+                 else ["4dpp", "4imm", "4smem"]):
         tuning(_lib.TUNE_BAND_TILE, BAND_VARIANTS[name])
         assert torch.equal(mesh.apply(X, **kw), base), name
 

@@ -32,7 +32,9 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--iprint", type=int, default=1)
     ap.add_argument("--x0", default="", help="start from a saved state (.npy of [T, u, v, p])")
-    ap.add_argument("--ckpt", default="", help="directory for each finished stage's state (bous_<ne>_<Ra>.npy)")
+    ap.add_argument("--ckpt", default="", help="directory for each finished stage's state (bous_<ne>_<Ra>.npy) "
+                                                 "and each Newton step's (bous_<ne>_<Ra>_newton.npy)")
+    ap.add_argument("--resume", type=int, default=0, help="--x0 is a mid-stage Newton state: no initial pass")
     args = ap.parse_args()
     from sem_amd.solvers.boussinesq import BoussinesqCoupler
     stages = []
@@ -44,7 +46,13 @@ def main():
                               mode=args.mode, mtol_internal=args.mtol_internal, iprint=args.iprint)
         if args.iprint >= 2:
             c.cd._progress = c.ns._progress = 500
-        T, u, v, p = c.solve(x)
+        def ckpt(xs, k, Ra=Ra):
+            if args.ckpt:
+                os.makedirs(args.ckpt, exist_ok=True)
+                np.save(os.path.join(args.ckpt, f"bous_{args.ne}_{Ra:g}_newton.npy"), xs)
+                print(f"checkpoint: Ra={Ra:g} after Newton {k} ({time.perf_counter() - t0:.0f} s)", flush=True)
+
+        T, u, v, p = c.solve(x, checkpoint=ckpt, resume=bool(args.resume) and not stages)
         x = np.concatenate((T, u, v, p))
         dt = time.perf_counter() - t0
         xp, yp = np.meshgrid(np.linspace(0, 1, 101), np.linspace(0, 1, 101), indexing="ij")
