@@ -15,7 +15,7 @@ import torch
 
 from . import GLL, _lib
 from .device import get_mesh
-from .operators import ConvectionTensor, SEMOperator, tensordot  # noqa: F401  (re-exported API)
+from .operators import COO3, ConvectionTensor, SEMOperator, tensordot  # noqa: F401  (re-exported API)
 
 
 def xi2x(e, xi, dx):
@@ -83,8 +83,9 @@ def assemble(A_e):
     """Global vector / matrix from an element array (SEM.py:113-146).
 
     4-D element vectors are summed on the GPU (sem_dss, reference summation
-    order, bit-exact).  6-D element matrices are assembled to SciPy CSR on the
-    host (setup-time utility; the operators themselves never materialise)."""
+    order, bit-exact).  6-D element matrices are assembled to SciPy CSR and 8-D
+    element 3-tensors to a COO3 on the host (setup-time formats; the operators
+    themselves never materialise)."""
     if isinstance(A_e, torch.Tensor) and A_e.dim() == 4:
         return _mesh_for_element_array(A_e).dss(A_e)
     A_e = np.asarray(A_e, dtype=np.float64)
@@ -98,8 +99,14 @@ def assemble(A_e):
         rows = global_index(P, nex, ney, m, n, i, j)
         cols = global_index(P, nex, ney, m, n, k, l)
         return sp.coo_matrix((A_e[m, n, i, j, k, l], (rows, cols)), shape=(N, N)).tocsr()
-    raise ValueError("assemble supports 4-D (vector) and 6-D (matrix) element arrays; "
-                     "convection 3-tensors are provided matrix-free by global_convection_matrices")
+    if A_e.ndim == 8:  # SEM.py:139-145: a COO 3-tensor (host format; see operators.COO3)
+        nex, ney, P = A_e.shape[0], A_e.shape[1], A_e.shape[2] - 1
+        m, n, i, j, r, s, k, l = np.nonzero(A_e)
+        coords = np.vstack((global_index(P, nex, ney, m, n, i, j), global_index(P, nex, ney, m, n, r, s),
+                            global_index(P, nex, ney, m, n, k, l)))
+        N = (P * nex + 1) * (P * ney + 1)
+        return COO3(coords, A_e[m, n, i, j, r, s, k, l], (N, N, N))
+    raise ValueError("assemble supports 4-D (vector), 6-D (matrix) and 8-D (3-tensor) element arrays")
 
 
 def scatter(u, P, N_ex, N_ey):

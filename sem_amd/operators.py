@@ -259,15 +259,52 @@ class ConvectionTensor:
         raise ValueError("contraction axis must be 1 or 2")
 
 
+class COO3:
+    """Sparse 3-tensor in coordinate form: what SEM.assemble returns for an 8-D element array
+    (SEM.py:139-145, a pydata-sparse `COO(coords, data, shape)`).  A host-side format for consumers
+    that assemble their own 3-tensors; the convection operators of global_convection_matrices stay
+    matrix-free (ConvectionTensor).  Duplicate coordinates are kept and summed by every operation,
+    as pydata-sparse does."""
+
+    def __init__(self, coords, data, shape):
+        self.coords = np.asarray(coords, dtype=np.int64)
+        self.data = np.asarray(data, dtype=np.float64)
+        self.shape = tuple(int(d) for d in shape)
+        self.ndim = len(self.shape)
+
+    @property
+    def nnz(self):
+        return self.data.size
+
+    def contract(self, vec, axis):
+        """tensordot(self, vec, (axis, 0)): the 2-tensor over the remaining axes, as SciPy CSR
+        (coordinates summed in entry order, as pydata-sparse's COO -> CSR)."""
+        x = vec.detach().cpu().numpy() if isinstance(vec, torch.Tensor) else np.asarray(vec, dtype=np.float64)
+        if x.ndim != 1 or x.shape[0] != self.shape[axis]:
+            raise ValueError("vector length does not match the contracted axis")
+        keep = [d for d in range(3) if d != axis]
+        data = self.data * x[self.coords[axis]]
+        return sp.coo_matrix((data, (self.coords[keep[0]], self.coords[keep[1]])),
+                             shape=(self.shape[keep[0]], self.shape[keep[1]])).tocsr()
+
+    def todense(self):
+        out = np.zeros(self.shape)
+        np.add.at(out, tuple(self.coords), self.data)
+        return out
+
+
 def tensordot(a, b, axes, return_type=None):
-    """pydata-sparse `tensordot(C, x, (1|2, 0), return_type=...)` for the convection tensors."""
+    """pydata-sparse `tensordot(C, x, (1|2, 0), return_type=...)` for the convection tensors
+    (matrix-free ConvectionTensor -> SEMOperator) and for assembled COO3 tensors (-> SciPy CSR)."""
     del return_type
-    if isinstance(a, ConvectionTensor):
+    if isinstance(a, (ConvectionTensor, COO3)):
         ax, bx = axes
         if bx != 0:
             raise ValueError("only contraction with a vector's axis 0 is supported")
+        if isinstance(a, COO3) and ax not in (0, 1, 2):
+            raise ValueError("contraction axis must be 0, 1 or 2")
         return a.contract(b, ax)
-    raise TypeError("tensordot is provided for ConvectionTensor operands")
+    raise TypeError("tensordot is provided for ConvectionTensor and COO3 operands")
 
 
 # device-side Dirichlet helpers re-exported for solver counterparts

@@ -139,3 +139,28 @@ def test_loader_refuses_library_from_other_sources(monkeypatch):
     monkeypatch.setattr(build, "source_hash", lambda: "0" * 16)
     with pytest.raises(RuntimeError, match="not built from the sources"):
         _lib._check_build_id(lib)
+
+
+@pytest.mark.parametrize("key", ["P4_4x4", "P4_3x2"])
+def test_assemble_8d_convection_tensor_matches_reference(key):
+    """SEM.assemble of an 8-D element array returns the reference's COO 3-tensor (SEM.py:139-145);
+    its contractions tensordot(C, u, (1,0)) / tensordot(C, T, (2,0)) reproduce the reference's own
+    CSR results (tests/golden/matrices.npz, made from the reference's COO triplets) bit for bit.
+    The element tensors are built as SEM.global_convection_matrices does (SEM.py:240-244)."""
+    P, nex, ney, Lx, Ly = MESHES[key]
+    dx, dy = Lx / nex, Ly / ney
+    g = golden("matrices.npz")
+    F_s, C_s = GLL.standard_product_matrix(P), GLL.standard_convection_matrix(P)
+    F_ex = np.multiply.outer(np.full(nex, dx / 2), F_s)
+    F_ey = np.multiply.outer(np.full(ney, dy / 2), F_s)
+    C_x_e = np.einsum('m,irk,njsl->mnijrskl', np.ones(nex), C_s, F_ey, optimize=True)
+    C_y_e = np.einsum('mirk,n,jsl->mnijrskl', F_ex, np.ones(ney), C_s, optimize=True)
+    Cx, Cy = SEM.assemble(C_x_e), SEM.assemble(C_y_e)
+    N = (P * nex + 1) * (P * ney + 1)
+    assert Cx.shape == (N, N, N)
+    for nm, C, vec, ax in (("uCx", Cx, g[key + "_u"], 1), ("vCy", Cy, g[key + "_v"], 1),
+                           ("CxT", Cx, g[key + "_T"], 2), ("CyT", Cy, g[key + "_T"], 2)):
+        A = SEM.tensordot(C, vec, (ax, 0)).tocsr()
+        assert np.array_equal(A.indptr, g[f"{key}_{nm}_indptr"]), nm
+        assert np.array_equal(A.indices, g[f"{key}_{nm}_indices"]), nm
+        assert np.array_equal(A.data, g[f"{key}_{nm}_data"]), nm
