@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 2
+#define SEM_ABI_VERSION 3
 
 enum sem_status {
   SEM_OK = 0,
@@ -249,6 +249,42 @@ typedef struct sem_velocity_desc {
 int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes);
 int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* A_II, double* D, double* aIB, double* aBI,
                         double* E, double* F, void* stream);
+
+/* ---- Navier-Stokes residuals (fused) ------------------------------------ */
+/* All three outputs of NavierStokes_Solver._get_residuals (NavierStokes_Solver.py:93-121) or
+ * _get_dresiduals (:138-160) in one launch, instead of one sem_apply per operand:
+ *     Sys = c_mass M + c_stiff K + c_gradx diag(cu) G_x + c_grady diag(cv) G_y
+ *     ru  = Sys u + diag(juu) u + diag(juv) v + G_x p
+ *     rv  = diag(jvu) u + Sys v + diag(jvv) v + G_y p + c_T M T
+ *     rc  = c_div (G_x u + G_y v)
+ * Rows in the Dirichlet set (dir_mask, or dir_sides when dir_mask is NULL): ru = u - dval_u,
+ * rv = v - dval_v, rc = (K p).  Row `pin` (-1: none): rc = p - pin_val, written before the Dirichlet
+ * rows when pin_first (the residual's statement order, :116-120) and after them otherwise (:159-160).
+ * u, v, p, T, cu, cv, j**, dval_* are nullable (NULL = zeros; cu, cv: ones); a NULL output is not
+ * computed.  u, v, ru, rv hold node (gx, gy) at gx * uv_pitch + gy (0 = NY: plain vectors; 2 NY: the
+ * line-interleaved [u | v] layout of the velocity solve).  Whole-mesh handles only. */
+typedef struct sem_ns_desc {
+  double c_mass, c_stiff, c_gradx, c_grady;
+  const double* cu;
+  const double* cv;
+  const double* juu;
+  const double* juv;
+  const double* jvu;
+  const double* jvv;
+  double c_T;
+  const double* T;
+  double c_div;
+  const double* dval_u;
+  const double* dval_v;
+  const uint8_t* dir_mask;
+  unsigned dir_sides;
+  int pin_first;
+  int64_t pin;
+  double pin_val;
+  int64_t uv_pitch;
+} sem_ns_desc;
+int sem_ns_apply(sem_handle* h, const sem_ns_desc* d, const double* u, const double* v, const double* p, double* ru,
+                 double* rv, double* rc, void* stream);
 
 #ifdef __cplusplus
 }

@@ -158,6 +158,46 @@ class Mesh:
                                                  self.stream_ptr(stream)))
         return blocks
 
+    def _line_view(self, t, name):
+        """u, v, ru, rv of sem_ns_apply: a plain vector, or an (NX, NY) view with row stride >= NY."""
+        if t is None:
+            return None, 0
+        if t.dim() == 1:
+            return self._vec(t, name), 0
+        if (not isinstance(t, torch.Tensor) or t.device != self.device or t.dtype != torch.float64
+                or tuple(t.shape) != (self.NX, self.NY) or t.stride(1) != 1 or t.stride(0) < self.NY):
+            raise ValueError(f"{name} must be a float64 ({self.NX}, {self.NY}) line view on {self.device}")
+        return t, t.stride(0)
+
+    def ns_apply(self, u=None, v=None, p=None, ru=None, rv=None, rc=None, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0,
+                 c_grady=0.0, cu=None, cv=None, juu=None, juv=None, jvu=None, jvv=None, c_T=0.0, T=None, c_div=1.0,
+                 dval_u=None, dval_v=None, dir_mask=None, dir_sides=0, pin=-1, pin_val=0.0, pin_first=False,
+                 stream=None):
+        """Fused Navier-Stokes residuals (include/sem_ops.h, sem_ns_apply): ru, rv, rc in one launch.
+        u, v, ru, rv are plain vectors or (NX, NY) line views sharing one row stride (the velocity
+        solve's interleaved [u | v] lines); a None output is not computed."""
+        pitch = set()
+        views = []
+        for nm, t in (("u", u), ("v", v), ("ru", ru), ("rv", rv)):
+            t, s = self._line_view(t, nm)
+            views.append(t)
+            if t is not None:
+                pitch.add(s)
+        if len(pitch) > 1:
+            raise ValueError("u, v, ru, rv must share one layout")
+        for nm, t in (("p", p), ("rc", rc), ("T", T), ("cu", cu), ("cv", cv), ("juu", juu), ("juv", juv),
+                      ("jvu", jvu), ("jvv", jvv), ("dval_u", dval_u), ("dval_v", dval_v)):
+            self._vec(t, nm)
+        if dir_mask is not None and (dir_mask.dtype != torch.uint8 or dir_mask.numel() != self.n_local):
+            raise ValueError("dir_mask must be a uint8 tensor of n_local entries")
+        d = _lib.SemNsDesc(float(c_mass), float(c_stiff), float(c_gradx), float(c_grady), _ptr(cu), _ptr(cv),
+                           _ptr(juu), _ptr(juv), _ptr(jvu), _ptr(jvv), float(c_T), _ptr(T), float(c_div),
+                           _ptr(dval_u), _ptr(dval_v), _ptr(dir_mask), int(dir_sides), int(bool(pin_first)), int(pin),
+                           float(pin_val), pitch.pop() if pitch else 0)
+        _lib.check(self._lib.sem_ns_apply(self._h, C.byref(d), *(_ptr(t) for t in views[:2]), _ptr(p),
+                                          *(_ptr(t) for t in views[2:]), _ptr(rc), self.stream_ptr(stream)))
+        return views[2], views[3], rc
+
     # ------------------------------------------------------------------ host-side 1-D tables
     def weights_1d(self):
         """Assembled 1-D GLL weights over the locally held lines (x) and all columns (y)."""

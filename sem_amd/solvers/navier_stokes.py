@@ -6,9 +6,9 @@ the GPU as fused launches:
 
   * `_get_residuals`  (:93-121): res_u = Sys u + G_x p, res_v = Sys v + G_y p - Gr/Re M T,
     res_cont = G_x u + G_y v, with the reference's Dirichlet / pinned-pressure /
-    artificial-Neumann (`K[mask,:] @ p`) rows -- 7 fused launches, no host round trip.
+    artificial-Neumann (`K[mask,:] @ p`) rows -- one sem_ns_apply launch for all three outputs.
   * `_calc_jacobians` (:123-136): Re diag(G_x u) ... as closed-form operators.
-  * `_get_dresiduals` (:138-160): the velocity Jacobian blocks applied matrix-free.
+  * `_get_dresiduals` (:138-160): the velocity Jacobian blocks applied matrix-free, one launch.
 
 `_get_update` keeps the reference's algorithm -- a direct velocity solve inside a pressure
 Schur-complement Krylov solve with the mass-diagonal preconditioner (NavierStokes_Solver.py:162-236)
@@ -33,7 +33,7 @@ class NavierStokesSolver:
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
                  max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
-                 recycle_bytes: float = 0.0):
+                 recycle_bytes: float = 0.0, velocity_sweep: str = "cr"):
         """recycle_bytes: device memory for a recycled Krylov subspace of the Schur-complement solves
         (sem_amd.krylov.Recycle, GCRO; 0 = off, the default): consecutive _get_update calls with one
         linearisation -- the Boussinesq coupler's block-Jacobi preconditioner -- then start from the
@@ -44,6 +44,7 @@ class NavierStokesSolver:
         self._iprint = iprint
         self._recycle_bytes, self._schur_recycle = recycle_bytes, None
         self._velocity_interior, self._velocity_graph = velocity_interior, velocity_graph
+        self._velocity_sweep = velocity_sweep
         self._max_basis = max_basis
         self._velo = None
         self._Re, self._Gr = Re, Gr
@@ -65,6 +66,7 @@ class NavierStokesSolver:
         self._C_x, self._C_y = SEM.global_convection_matrices(P, N_ex, N_ey, dx, dy)
         self._Sys = None
         self._Jac_u_u = self._Jac_u_v = self._Jac_v_u = self._Jac_v_v = None
+        self._jac_kw, self._schur = None, None
 
         # Dirichlet values and masks, exactly as NavierStokes_Solver.py:78-94 builds them
         x, y = self.points
@@ -85,9 +87,11 @@ class NavierStokesSolver:
         self._dir = DirichletRows(m, self._mask_bound, all_sides)
         self._dval_u = m.to_device(np.where(self._mask_bound, du, 0.0))
         self._dval_v = m.to_device(np.where(self._mask_bound, dv, 0.0))
-        self._pidx = torch.as_tensor(np.nonzero(self._mask_dir_p)[0], device=m.device)
-        self._pin_on_boundary = bool(self._mask_bound[self._mask_dir_p].any())
-        self._dval_p = m.to_device(np.where(self._mask_dir_p, dpp, 0.0))
+        pins = np.nonzero(self._mask_dir_p)[0]
+        if len(pins) > 1:
+            raise ValueError("one pinned pressure node is supported")
+        self._pin = int(pins[0]) if len(pins) else -1
+        self._pin_val = float(dpp[self._pin]) if len(pins) else 0.0
         self._Mdiag = m.to_device(self._M.diagonal())
 
     # ------------------------------------------------------------------ helpers
@@ -102,73 +106,48 @@ class NavierStokesSolver:
         cX, cu, cY, cv, d = Sys._coeffs()
         return dict(c_stiff=Sys.cK, c_mass=Sys.cM, c_gradx=cX, cu=cu, c_grady=cY, cv=cv)
 
-    def _continuity(self, u, v, p, pdir=None):
-        """G_x u + G_y v with the artificial Neumann rows (K p)[mask_bound] fused into the launch
-        (SEM_DIR_REPLACE) and the pinned-pressure row; row order as the reference: residual
-        (:119-122) pins first and the Neumann rows win, dres (:160-161) the pinned row wins."""
-        m = self._mesh
-        kp = m.apply(p, c_stiff=1.0)
-        r = m.apply(u, c_gradx=1.0)
-        r = m.apply(v, r, c_grady=1.0, c_acc=1.0, dir_mode=_lib.DIR_REPLACE, dir_val=kp, **self._dir.kw())
-        if pdir is None:
-            r[self._pidx] = p[self._pidx]
-        elif not self._pin_on_boundary:
-            r[self._pidx] = p[self._pidx] - pdir[self._pidx]
-        return r
+    def _ns_kw(self, pin_first):
+        """Row replacements of sem_ns_apply: Dirichlet rows (mask_bound) and the pinned-pressure row."""
+        return dict(pin=self._pin, pin_val=0.0 if not pin_first else self._pin_val, pin_first=pin_first,
+                    **self._dir.kw())
 
     # ------------------------------------------------------------------ reference methods
     def _get_residuals(self, u, v, p, T):
-        """NavierStokes_Solver.py:93-121."""
+        """NavierStokes_Solver.py:93-121: one fused launch (sem_ns_apply) for res_u, res_v, res_cont."""
         m = self._mesh
         U, V, Pp, Tt = self._dev(u), self._dev(v), self._dev(p), self._dev(T)
         Conv = self._Re * (SEM.tensordot(self._C_x, U, (1, 0)) + SEM.tensordot(self._C_y, V, (1, 0)))
         self._Sys = self._K + Conv
         if self._schur_recycle is not None:   # the Schur operator depends on Sys
             self._schur_recycle.reset()
-        kw = self._sys_kw(self._Sys)
-        # res_u = Sys u + G_x p, Dirichlet rows u - u_dir
-        ru = m.apply(Pp, c_gradx=1.0)
-        ru = m.apply(U, ru, c_acc=1.0, dir_mode=_lib.DIR_IDENTITY, dir_val=self._dval_u, **kw, **self._dir.kw())
-        # res_v = Sys v + G_y p - Gr/Re M T
-        rv = m.apply(Pp, c_grady=1.0)
-        rv = m.apply(Tt, rv, c_mass=-self._Gr_over_Re, c_acc=1.0)
-        rv = m.apply(V, rv, c_acc=1.0, dir_mode=_lib.DIR_IDENTITY, dir_val=self._dval_v, **kw, **self._dir.kw())
-        rc = self._continuity(U, V, Pp, pdir=self._dval_p)
+        ru, rv, rc = (torch.empty_like(U) for _ in range(3))
+        m.ns_apply(U, V, Pp, ru, rv, rc, **self._sys_kw(self._Sys), c_T=-self._Gr_over_Re, T=Tt,
+                   dval_u=self._dval_u, dval_v=self._dval_v, **self._ns_kw(pin_first=True))
         return self._out(ru, u), self._out(rv, u), self._out(rc, u)
 
     def _calc_jacobians(self, u, v):
-        """NavierStokes_Solver.py:123-136."""
+        """NavierStokes_Solver.py:123-136.  The Jacobians keep the Sys of this linearisation, as the
+        reference's J_uu = Sys + ... does, even if _get_residuals runs again before they are used."""
         U, V = self._dev(u), self._dev(v)
         Re = self._Re
         self._Jac_u_u = self._Sys + Re * SEM.tensordot(self._C_x, U, (2, 0))
         self._Jac_v_v = self._Sys + Re * SEM.tensordot(self._C_y, V, (2, 0))
         self._Jac_u_v = Re * SEM.tensordot(self._C_y, U, (2, 0))
         self._Jac_v_u = Re * SEM.tensordot(self._C_x, V, (2, 0))
+        self._jac_kw = dict(self._sys_kw(self._Sys), juu=self._Jac_u_u._coeffs()[4], jvv=self._Jac_v_v._coeffs()[4],
+                            juv=self._Jac_u_v._coeffs()[4], jvu=self._Jac_v_u._coeffs()[4])
         self._velo = None  # factorised on first use, reused until the next linearisation
+        self._schur = None
         if self._schur_recycle is not None:
             self._schur_recycle.reset()
 
     def _get_dresiduals(self, du, dv, dp, dT=None):
-        """NavierStokes_Solver.py:138-160."""
+        """NavierStokes_Solver.py:138-160: one fused launch (sem_ns_apply) for the three differentials."""
         m = self._mesh
         DU, DV, DP = self._dev(du), self._dev(dv), self._dev(dp)
-        kw = self._sys_kw(self._Sys)
-        juu = self._Jac_u_u._coeffs()[4]   # Re G_x u  (the diagonal part beyond Sys)
-        jvv = self._Jac_v_v._coeffs()[4]   # Re G_y v
-        juv = self._Jac_u_v._coeffs()[4]   # Re G_y u
-        jvu = self._Jac_v_u._coeffs()[4]   # Re G_x v
-        # dres_u = Sys du + (Re G_x u).du + (Re G_y u).dv + G_x dp
-        ru = m.apply(DP, c_gradx=1.0)
-        ru = m.apply(DU, ru, c_acc=1.0, c_extra=1.0, ea=juu, eb=DU, ec=juv, ed=DV, dir_mode=_lib.DIR_IDENTITY,
-                     **kw, **self._dir.kw())
-        # dres_v = (Re G_x v).du + Sys dv + (Re G_y v).dv + G_y dp - Gr/Re M dT
-        rv = m.apply(DP, c_grady=1.0)
-        if dT is not None:
-            rv = m.apply(self._dev(dT), rv, c_mass=-self._Gr_over_Re, c_acc=1.0)
-        rv = m.apply(DV, rv, c_acc=1.0, c_extra=1.0, ea=jvu, eb=DU, ec=jvv, ed=DV, dir_mode=_lib.DIR_IDENTITY,
-                     **kw, **self._dir.kw())
-        # dres_cont = G_x du + G_y dv; [mask_bound] = (K dp)[mask_bound]; [mask_p] = dp[mask_p]
-        rc = self._continuity(DU, DV, DP)
+        ru, rv, rc = (torch.empty_like(DU) for _ in range(3))
+        m.ns_apply(DU, DV, DP, ru, rv, rc, **self._jac_kw, c_T=-self._Gr_over_Re if dT is not None else 0.0,
+                   T=self._dev(dT), **self._ns_kw(pin_first=False))
         return self._out(ru, du), self._out(rv, du), self._out(rc, du)
 
     def _velocity_solver(self):
@@ -181,12 +160,10 @@ class NavierStokesSolver:
             return self._velo
         tStart = time.perf_counter()
         m = self._mesh
-        vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior)
+        vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior,
+                                    sweep=self._velocity_sweep)
         blocks = vs.empty_blocks()
-        kw = self._sys_kw(self._Sys)
-        m.velocity_blocks(blocks, juu=self._Jac_u_u._coeffs()[4], juv=self._Jac_u_v._coeffs()[4],
-                          jvu=self._Jac_v_u._coeffs()[4], jvv=self._Jac_v_v._coeffs()[4],
-                          dir_mask=self._dir.mask, dir_sides=self._dir.sides, **kw)
+        m.velocity_blocks(blocks, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
         vs.factor(blocks.pop("AII"), **blocks)
         if self._velocity_graph:
             vs.capture()
@@ -206,21 +183,26 @@ class NavierStokesSolver:
         meshes (the Schur complement carries the spurious pressure modes of the equal-order
         discretisation), so the device GMRES runs unrestarted up to max_basis vectors."""
         vs = self._velocity_solver()
+        m = self._mesh
         ru, rv, rc = self._dev(dres_u), self._dev(dres_v), self._dev(dres_cont)
-        Z = torch.zeros(self.N, dtype=torch.float64, device=self._mesh.device)
-        b_schur = rc - self._get_dresiduals(*vs.solve(ru, rv), Z)[2]
+        fu, fv = vs.solve(ru, rv)
+        c0 = torch.empty_like(rc)
+        m.ns_apply(fu, fv, None, rc=c0, **self._ns_kw(pin_first=False))   # dres_cont(J^-1 [ru; rv], 0)
+        b_schur = rc - c0
+        if self._schur is None:
+            self._schur = _SchurComplement(self, vs, graph=self._velocity_graph)
         count = [0]
 
         def schur_mv(dp):
             count[0] += 1
-            f_x, f_y = vs.solve(*self._get_dresiduals(Z, Z, dp)[:2])
-            return self._get_dresiduals(-f_x, -f_y, dp)[2]
+            return self._schur(dp)
 
-        mp = self._pidx
+        pin = self._pin
 
         def precon(c):
             z = c / self._Mdiag
-            z[mp] = c[mp]
+            if pin >= 0:
+                z[pin] = c[pin]
             return z
 
         it = [0]
@@ -245,7 +227,8 @@ class NavierStokesSolver:
         if 'LGMRES_suc' in self._iprint:
             res = (schur_mv(dp) - b_schur).abs().max().item()
             print(f'NavierStokes GMRES: Converged in {count[0]} evaluations with max-norm {res}')
-        b_u, b_v = self._get_dresiduals(Z, Z, dp)[:2]
+        b_u, b_v = torch.empty_like(dp), torch.empty_like(dp)
+        m.ns_apply(None, None, dp, b_u, b_v, **self._ns_kw(pin_first=False))
         du, dv = vs.solve(ru - b_u, rv - b_v)
         return self._out(du, dres_u), self._out(dv, dres_u), self._out(dp, dres_u)
 
@@ -292,3 +275,53 @@ class NavierStokesSolver:
         u, v, p = self._get_solution(T)
         return self._get_interpol(u, points_plot), self._get_interpol(v, points_plot), self._get_interpol(p,
                                                                                                          points_plot)
+
+
+class _SchurComplement:
+    """The pressure Schur-complement operator of _get_update (NavierStokes_Solver.py:194-203):
+    S dp = dres_cont(-J^-1 [G_x dp; G_y dp]_D, dp), i.e. two fused sem_ns_apply launches around one
+    velocity solve.  The gradients are written straight into the solve's line-interleaved [u | v]
+    layout and the divergence reads the solution from it (uv_pitch = 2 N_y), and the whole matvec is
+    captured in one hipGraph per linearisation: a Krylov iteration then costs one graph launch."""
+
+    def __init__(self, ns, vs, graph=True):
+        self.ns, self.vs = ns, vs
+        m = ns._mesh
+        self._B = torch.zeros((m.NX, 2 * m.NY), dtype=torch.float64, device=m.device)
+        self._x = torch.zeros(m.n_local, dtype=torch.float64, device=m.device)
+        self._graph = None
+        if graph and m.device.type == "cuda" and (vs.P == 1 or vs.interior != "lu"):
+            self._capture()
+
+    def _body(self, dp):
+        ns, m, NY = self.ns, self.ns._mesh, self.ns._mesh.NY
+        B = self._B
+        m.ns_apply(None, None, dp, B[:, :NY], B[:, NY:], **ns._ns_kw(pin_first=False))
+        X = self.vs._solve_lines(B)
+        rc = torch.empty_like(dp)
+        m.ns_apply(X[:, :NY], X[:, NY:], dp, rc=rc, c_div=-1.0, **ns._ns_kw(pin_first=False))
+        return rc
+
+    def _capture(self):
+        dev = self.ns._mesh.device
+        cur = torch.cuda.current_stream(dev)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(cur)
+        try:
+            with torch.cuda.stream(s):
+                self._body(self._x)   # warm-up outside the capture (library workspaces)
+            cur.wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._out = self._body(self._x)
+            self._graph = g
+        except RuntimeError:
+            torch.cuda.synchronize(dev)
+            self._graph = None
+
+    def __call__(self, dp):
+        if self._graph is None:
+            return self._body(dp)
+        self._x.copy_(dp)
+        self._graph.replay()
+        return self._out.clone()

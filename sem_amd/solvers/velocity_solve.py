@@ -14,8 +14,8 @@ Schur-complement matvec) with a static condensation that fits the structured SEM
 * Factor: batched pivoted LU of the A_II blocks (rocSOLVER through torch), W = A_II^-1 A_IB, the
   interface Schur complement S = A_BB - A_BI W (block tridiagonal over the N_ex+1 interface lines,
   blocks of 2 N_y), and its block-LU (block Thomas) with explicit inverses of the pivot blocks.
-* Solve: interior forward solve, the interface sweep (2 (N_ex+1) small GEMVs), interior back
-  substitution.
+* Solve: interior forward solve, the interface sweep (block cyclic reduction: ~3 batched launches
+  per level, log2(N_ex+1) levels; or block Thomas, 2 N_ex dependent GEMVs), interior back substitution.
 
 Everything is device memory: cfg3 (32^2, P = 8) holds 3.3 GB of A_II factors, cfg4 (48^2, P = 8)
 11 GB, well inside one MI355X's 288 GB.  The algebra runs on any torch device, so the
@@ -28,11 +28,18 @@ import torch
 class VelocityJacobianSolver:
     """x = J^-1 b for the velocity Jacobian J of one linearisation, J given by its condensation pieces."""
 
-    def __init__(self, P, nex, ney, device, interior="nested"):
+    def __init__(self, P, nex, ney, device, interior="nested", sweep="cr"):
+        """interior: elimination of the element-column interiors ("nested" static condensation, or
+        one dense block per column: "lu" factors, "inverse" explicit inverses).  sweep: solve of the
+        block-tridiagonal interface system ("cr": block cyclic reduction, about 2 log2(N_ex) batched
+        launches; "thomas": block Thomas, 2 N_ex sequential steps)."""
         if P < 1 or nex < 1 or ney < 1:
             raise ValueError("bad mesh")
         if interior not in ("nested", "lu", "inverse"):
             raise ValueError("interior must be 'nested', 'lu' or 'inverse'")
+        if sweep not in ("cr", "thomas"):
+            raise ValueError("sweep must be 'cr' or 'thomas'")
+        self.sweep = sweep
         self.P, self.nex, self.ney = P, nex, ney
         self.NY, self.NX = ney * P + 1, nex * P + 1
         self.m = 2 * self.NY
@@ -92,6 +99,10 @@ class VelocityJacobianSolver:
             self.aBI, self.aIB = aBI, aIB
         else:
             S_diag, S_up, S_lo = D, torch.diag_embed(E), torch.diag_embed(F)
+        if self.sweep == "cr":
+            self._cr_factor(S_diag, S_up, S_lo)
+            self.factored = True
+            return
         # block Thomas on the interface lines: Dt[0] = S_diag[0], Uh[L] = Dt[L]^-1 S_up[L],
         # Dt[L+1] = S_diag[L+1] - S_lo[L] Uh[L]; explicit (pivoted) inverses of the pivot blocks
         Dinv = torch.empty((nex + 1, m, m), dtype=torch.float64, device=self.device)
@@ -105,6 +116,71 @@ class VelocityJacobianSolver:
                 Uh[L] = Dinv[L] @ S_up[L]
         self.Dinv, self.Uh, self.S_lo = Dinv, Uh, S_lo
         self.factored = True
+
+    # ------------------------------------------------------------------ interface sweep: cyclic reduction
+    # Block cyclic reduction of the block-tridiagonal interface system (rows L = 0..N_ex, diagonal
+    # blocks B_L = S_diag[L], couplings A_L = S_lo[L-1] to row L-1 and C_L = S_up[L] to row L+1).
+    # Each level eliminates every other remaining row j with the explicit inverse of its pivot block:
+    # a kept row i with neighbours l < i < r takes
+    #     alpha_i = -A_i B_l^-1, gamma_i = -C_i B_r^-1,  B_i += alpha_i C_l + gamma_i A_r,
+    #     A_i <- alpha_i A_l, C_i <- gamma_i C_r,        g_i += alpha_i g_l + gamma_i g_r,
+    # and back substitution recovers x_j = B_j^-1 g_j - (B_j^-1 A_j) x_l - (B_j^-1 C_j) x_r.  Missing
+    # neighbours get zero blocks, so every level is one batched product per direction: the solve is
+    # ~3 launches per level and log2(N_ex + 1) levels, against the 2 N_ex dependent steps of Thomas.
+    def _cr_factor(self, S_diag, S_up, S_lo):
+        n, m = S_diag.shape[0], S_diag.shape[1]
+        dev, f64 = self.device, torch.float64
+        B = S_diag.clone()
+        A = torch.zeros_like(B)
+        C = torch.zeros_like(B)
+        if n > 1:
+            A[1:] = S_lo
+            C[:-1] = S_up
+        rows = torch.arange(n, device=dev)
+        self._cr = []
+        while rows.numel() > 1:
+            keep, elim = rows[0::2], rows[1::2]
+            k = keep.numel()
+            # neighbours of the kept rows (-1: none) and of the eliminated rows (always kept rows)
+            left = torch.full((k,), -1, dtype=torch.long, device=dev)
+            right = torch.full((k,), -1, dtype=torch.long, device=dev)
+            left[1:] = elim[:k - 1]
+            right[:elim.numel()] = elim
+            Binv = torch.linalg.inv(B[elim])
+            hasl, hasr = left >= 0, right >= 0
+            zl, zr = left.clamp(min=0), right.clamp(min=0)
+            pos = torch.full((n,), -1, dtype=torch.long, device=dev)
+            pos[elim] = torch.arange(elim.numel(), device=dev)
+            Bl = torch.where(hasl[:, None, None], Binv[pos[zl].clamp(min=0)], torch.zeros((), dtype=f64, device=dev))
+            Br = torch.where(hasr[:, None, None], Binv[pos[zr].clamp(min=0)], torch.zeros((), dtype=f64, device=dev))
+            alpha = -(A[keep] @ Bl)
+            gamma = -(C[keep] @ Br)
+            B[keep] += alpha @ C[zl] + gamma @ A[zr]
+            # back-substitution operator of the eliminated rows: [B^-1 | -B^-1 A | -B^-1 C]
+            back = torch.cat((Binv, -(Binv @ A[elim]), -(Binv @ C[elim])), dim=2)
+            nA, nC = alpha @ A[zl], gamma @ C[zr]
+            A[keep], C[keep] = nA, nC
+            fwd = torch.cat((alpha, gamma), dim=2)
+            # gather index of [g_l; g_r] for the kept rows (missing neighbours read row 0, times zero)
+            # back substitution reads [g_j; x_l; x_r]; a missing right neighbour (zero block) reads x_l
+            e = elim.numel()
+            br = torch.cat((keep[1:], keep[-1:]))[:e]
+            self._cr.append((keep, fwd, torch.stack((zl, zr)), elim, back, torch.stack((elim, keep[:e], br))))
+            rows = keep
+        self._cr_top = (rows, torch.linalg.inv(B[rows]))
+
+    def _cr_solve(self, g):
+        """x = S^-1 g for the interface system; g (N_ex + 1, m) is overwritten."""
+        for keep, fwd, idx, _, _, _ in self._cr:
+            gl = g[idx.reshape(-1)].view(2, keep.numel(), -1).permute(1, 0, 2).reshape(keep.numel(), -1, 1)
+            g.index_add_(0, keep, torch.bmm(fwd, gl)[..., 0])
+        top, Tinv = self._cr_top
+        x = torch.zeros_like(g)
+        x[top] = torch.bmm(Tinv, g[top][..., None])[..., 0]
+        for _, _, _, elim, back, idx in reversed(self._cr):
+            rhs = torch.cat((g[idx[0]], x[idx[1]], x[idx[2]]), dim=1)[..., None]
+            x[elim] = torch.bmm(back, rhs)[..., 0]
+        return x
 
     # ------------------------------------------------------------------ nested interior (default)
     # Inside one element column the interior unknowns split again: the interiors of its elements
@@ -186,14 +262,16 @@ class VelocityJacobianSolver:
             yIr = yI.view(nex, P - 1, m)
             g[:-1] -= (self.aBI[:, 0] * yIr).sum(1)
             g[1:] -= (self.aBI[:, 1] * yIr).sum(1)
-        # interface sweep (block Thomas with the pivot blocks' explicit inverses)
-        z = torch.empty_like(g)
-        z[0] = self.Dinv[0] @ g[0]
-        for L in range(1, nex + 1):
-            z[L] = self.Dinv[L] @ (g[L] - self.S_lo[L - 1] @ z[L - 1])
-        xB = z
-        for L in range(nex - 1, -1, -1):
-            xB[L] = z[L] - self.Uh[L] @ xB[L + 1]
+        if self.sweep == "cr":
+            xB = self._cr_solve(g)
+        else:   # block Thomas with the pivot blocks' explicit inverses
+            z = torch.empty_like(g)
+            z[0] = self.Dinv[0] @ g[0]
+            for L in range(1, nex + 1):
+                z[L] = self.Dinv[L] @ (g[L] - self.S_lo[L - 1] @ z[L - 1])
+            xB = z
+            for L in range(nex - 1, -1, -1):
+                xB[L] = z[L] - self.Uh[L] @ xB[L + 1]
         out = torch.empty((NX, m), dtype=torch.float64, device=self.device)
         out[0::P] = xB
         if P > 1:

@@ -10,7 +10,8 @@ import torch
 from velocity_blocks import assemble, extract, oracle_velocity_jacobian
 from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
 
-CASES = [(4, 3, 2, 100.0), (2, 2, 3, 400.0), (1, 4, 3, 10.0), (6, 2, 2, 1000.0), (3, 1, 1, 1.0)]
+CASES = [(4, 3, 2, 100.0), (2, 2, 3, 400.0), (1, 4, 3, 10.0), (6, 2, 2, 1000.0), (3, 1, 1, 1.0), (2, 7, 2, 300.0),
+         (3, 6, 2, 50.0)]
 
 
 @pytest.mark.parametrize("P,nex,ney,Re", CASES)
@@ -21,11 +22,11 @@ def test_pieces_describe_the_jacobian_exactly(P, nex, ney, Re):
 
 
 @pytest.mark.parametrize("P,nex,ney,Re", CASES)
-@pytest.mark.parametrize("interior", ["nested", "lu", "inverse"])
-def test_condensed_solve_matches_sparse_lu(P, nex, ney, Re, interior):
+@pytest.mark.parametrize("interior,sweep", [("nested", "cr"), ("nested", "thomas"), ("lu", "cr"), ("inverse", "thomas")])
+def test_condensed_solve_matches_sparse_lu(P, nex, ney, Re, interior, sweep):
     ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
     pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
-    vs = VelocityJacobianSolver(P, nex, ney, "cpu", interior=interior)
+    vs = VelocityJacobianSolver(P, nex, ney, "cpu", interior=interior, sweep=sweep)
     vs.factor(pcs.get("AII"), pcs["D"], pcs.get("aIB"), pcs.get("aBI"), pcs["E"], pcs["F"])
     r = np.random.default_rng(5)
     bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)

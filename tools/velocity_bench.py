@@ -1,6 +1,7 @@
 """Velocity-Jacobian device solve timings (sem_amd/solvers/velocity_solve.py): factorisation and
-solve per configuration (interior LU solve vs explicit interior inverse, eager vs hipGraph) at a
-smooth linearisation state, with the solve's residual checked through the matrix-free Jacobian.
+solve per configuration (interior elimination x interface sweep, eager vs hipGraph) at a smooth
+linearisation state, with the solve's residual checked through the matrix-free Jacobian, and the
+Schur-complement matvec of _get_update (eager vs one captured graph).
 
 python tools/velocity_bench.py --ne 32 --P 8 --Re 1000
 """
@@ -22,14 +23,16 @@ def main():
     ap.add_argument("--P", type=int, default=8)
     ap.add_argument("--Re", type=float, default=1000.0)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--interiors", default="nested,inverse")
+    ap.add_argument("--configs", default="nested:cr,nested:thomas", help="interior:sweep,...")
     args = ap.parse_args()
     from sem_amd.solvers import NavierStokesSolver
     from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
     out = {"mesh": f"{args.ne}x{args.ne}", "P": args.P, "Re": args.Re}
-    for interior in args.interiors.split(","):
+    from sem_amd.solvers.navier_stokes import _SchurComplement
+    for cfg in args.configs.split(","):
+        interior, sweep = cfg.split(":")
         ns = NavierStokesSolver(1.0, 1.0, args.Re, 0.0, args.P, args.ne, args.ne, u_N=1.0, iprint=[],
-                                velocity_interior=interior, velocity_graph=False)
+                                velocity_interior=interior, velocity_sweep=sweep, velocity_graph=False)
         x, y = ns.points
         u = np.sin(np.pi * x) * np.sin(np.pi * y) * (y ** 2)
         v = -np.sin(np.pi * x) * np.sin(2 * np.pi * y) * 0.3
@@ -65,9 +68,22 @@ def main():
             res[f"{mode}_rel_residual"] = max((ru - bu).abs().max().item(), (rv - bv).abs().max().item()) / max(
                 xu.abs().max().item(), xv.abs().max().item())
         res["factor_s"] = t_factor
+        # the Schur-complement matvec of _get_update: eager, and captured whole in one graph
+        dp = ns._dev(r.uniform(-1, 1, ns.N))
+        for graph in (False, True):
+            S = _SchurComplement(ns, vs, graph=graph)
+            y0 = S(dp)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.reps):
+                y = S(dp)
+            torch.cuda.synchronize()
+            res[f"schur_{'graph' if graph else 'eager'}_ms"] = (time.perf_counter() - t0) / args.reps * 1e3
+            if graph:
+                res["schur_graph_vs_eager"] = (y - y0).abs().max().item() / y0.abs().max().item()
         res["mem_GB"] = torch.cuda.max_memory_allocated() / 1e9
-        out[interior] = res
-        print(json.dumps({interior: res}), flush=True)
+        out[cfg] = res
+        print(json.dumps({cfg: res}), flush=True)
         del vs, ns
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats()
