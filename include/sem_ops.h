@@ -250,6 +250,18 @@ int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes);
 int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* A_II, double* D, double* aIB, double* aBI,
                         double* E, double* F, void* stream);
 
+/* ---- batched block GEMV (interface sweep of the velocity solve) ----------- */
+/* y[yrow[b]] (+)= sum_{s<S} M[b][:, s m:(s+1) m] . src[s][xrow[s nb + b]]  for b < nb (S <= 3):
+ * one level of the block cyclic reduction that solves the interface system of the condensed
+ * velocity Jacobian (sem_amd/solvers/velocity_solve.py), in place of the reference's SuperLU
+ * triangular solves (NavierStokes_Solver.py:189-203).  M: (nb, m, S m) row-major; operand row r of
+ * src[s] at src[s] + r ld_src[s]; xrow = -1: that operand is absent (its block is skipped); output row
+ * yrow[b] at y + yrow[b] ld_y, accumulated when `accumulate`.  Output rows must be distinct and not
+ * read by the same call.  S m <= 8192.  src and ld_src are host arrays of S entries; M, the operand
+ * rows, y, xrow and yrow are device memory.  Stream-ordered. */
+int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* src, const int64_t* ld_src,
+                   const int64_t* xrow, double* y, int64_t ld_y, const int64_t* yrow, int accumulate, void* stream);
+
 /* ---- Navier-Stokes residuals (fused) ------------------------------------ */
 /* All three outputs of NavierStokes_Solver._get_residuals (NavierStokes_Solver.py:93-121) or
  * _get_dresiduals (:138-160) in one launch, instead of one sem_apply per operand:

@@ -86,6 +86,8 @@ _SIGS = {
     "sem_velocity_block_sizes": (C.c_int, [C.c_void_p, _i64p]),
     "sem_velocity_blocks": (C.c_int, [C.c_void_p, C.POINTER(SemVelocityDesc)] + [C.c_void_p] * 7),
     "sem_ns_apply": (C.c_int, [C.c_void_p, C.POINTER(SemNsDesc)] + [C.c_void_p] * 7),
+    "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,
+                                 C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p]),
 }
 
 _lib = None

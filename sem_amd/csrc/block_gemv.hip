@@ -1,0 +1,109 @@
+// Batched block GEMV with gathered operands: the level step of the interface sweep of the
+// Navier-Stokes velocity solve (block cyclic reduction, sem_amd/solvers/velocity_solve.py), which
+// replaces the reference's SuperLU triangular solves (NavierStokes_Solver.py:189-203).
+//
+//   y[yrow[b]] (+)= sum_{s < S} M[b][:, s m : (s+1) m] . src_s[xrow[s][b]]      b = 0 .. nb-1
+//
+// M is (nb, m, S m) row-major: one dense m x S m operator per output row block (a level's
+// [alpha | gamma] or [B^-1 | -B^-1 A | -B^-1 C]).  The kernel is HBM-bound on M (8 S m^2 bytes per
+// block, each read once): every workgroup stages the S gathered operand rows of its block in LDS
+// and its four waves stream kRows matrix rows each, 64 lanes over a row (512 B per wave load), four
+// rows in flight per wave, then reduce across the wave with DPP/shuffles.  The grid is
+// (ceil(m / 16), nb) workgroups; blocks of one output never overlap, and the operands it gathers
+// are rows the launch does not write (the caller's level structure guarantees it).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "sem_internal.h"
+
+namespace sem {
+
+constexpr int kGemvWaves = 4;
+constexpr int kGemvRowsPerWave = 4;
+constexpr int kGemvRows = kGemvWaves * kGemvRowsPerWave;  // matrix rows per workgroup
+
+struct GemvArgs {
+  const double* M;
+  const double* src[3];
+  const int64_t* xrow;  // (S, nb); -1: no operand (its block is skipped)
+  const int64_t* yrow;  // (nb)
+  double* y;
+  int64_t ld_src[3], ld_y;
+  int nb, m, S, accumulate;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(64 * kGemvWaves) void block_gemv_kernel(const GemvArgs a) {
+  extern __shared__ double xs[];  // S * m gathered operand values (0 for a skipped operand)
+  const int b = blockIdx.y, m = a.m, S = a.S, K = S * m;
+  for (int s = 0; s < S; ++s) {
+    const int64_t r = a.xrow[static_cast<int64_t>(s) * a.nb + b];
+    const double* src = r >= 0 ? a.src[s] + r * a.ld_src[s] : nullptr;
+    for (int j = threadIdx.x; j < m; j += blockDim.x) xs[s * m + j] = src ? src[j] : 0.0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * kGemvRows + wave * kGemvRowsPerWave;
+  if (r0 >= m) return;
+  const double* Mb = a.M + static_cast<int64_t>(b) * m * K;
+  double acc[kGemvRowsPerWave];
+  const double* row[kGemvRowsPerWave];
+#pragma unroll
+  for (int i = 0; i < kGemvRowsPerWave; ++i) {
+    acc[i] = 0.0;
+    row[i] = Mb + static_cast<int64_t>(min(r0 + i, m - 1)) * K;  // clamped rows are computed, not stored
+  }
+  for (int j = lane; j < K; j += 64) {
+    const double xv = xs[j];
+#pragma unroll
+    for (int i = 0; i < kGemvRowsPerWave; ++i) acc[i] = fma(row[i][j], xv, acc[i]);
+  }
+  double* yb = a.y + a.yrow[b] * a.ld_y;
+#pragma unroll
+  for (int i = 0; i < kGemvRowsPerWave; ++i) {
+    const double v = wave_sum(acc[i]);
+    if (lane == 0 && r0 + i < m) yb[r0 + i] = a.accumulate ? yb[r0 + i] + v : v;
+  }
+}
+
+}  // namespace sem
+
+extern "C" {
+
+int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* src, const int64_t* ld_src,
+                   const int64_t* xrow, double* y, int64_t ld_y, const int64_t* yrow, int accumulate, void* stream) {
+  if (nb < 0 || m < 1 || S < 1 || S > 3) return sem::set_error(SEM_EINVAL, "block_gemv: bad sizes");
+  if (!M || !src || !ld_src || !xrow || !y || !yrow) return sem::set_error(SEM_EINVAL, "block_gemv: null argument");
+  const size_t lds = static_cast<size_t>(S) * m * sizeof(double);
+  if (lds > 64 * 1024) return sem::set_error(SEM_EUNSUPPORTED, "block_gemv: S m above 8192 doubles");
+  if (nb == 0) return SEM_OK;
+  sem::GemvArgs a{};
+  a.M = M;
+  for (int s = 0; s < S; ++s) {
+    if (!src[s]) return sem::set_error(SEM_EINVAL, "block_gemv: null operand");
+    a.src[s] = src[s];
+    a.ld_src[s] = ld_src[s];
+  }
+  a.xrow = xrow;
+  a.yrow = yrow;
+  a.y = y;
+  a.ld_y = ld_y;
+  a.nb = nb;
+  a.m = m;
+  a.S = S;
+  a.accumulate = accumulate;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((m + sem::kGemvRows - 1) / sem::kGemvRows, nb);
+  hipLaunchKernelGGL(sem::block_gemv_kernel, grid, dim3(64 * sem::kGemvWaves), lds, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("block_gemv launch: ") + hipGetErrorString(e));
+  return SEM_OK;
+}
+
+}  // extern "C"

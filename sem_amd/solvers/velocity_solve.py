@@ -139,7 +139,7 @@ class VelocityJacobianSolver:
         rows = torch.arange(n, device=dev)
         self._cr = []
         while rows.numel() > 1:
-            keep, elim = rows[0::2], rows[1::2]
+            keep, elim = rows[0::2].contiguous(), rows[1::2].contiguous()   # index arrays of sem_block_gemv
             k = keep.numel()
             # neighbours of the kept rows (-1: none) and of the eliminated rows (always kept rows)
             left = torch.full((k,), -1, dtype=torch.long, device=dev)
@@ -165,21 +165,54 @@ class VelocityJacobianSolver:
             # back substitution reads [g_j; x_l; x_r]; a missing right neighbour (zero block) reads x_l
             e = elim.numel()
             br = torch.cat((keep[1:], keep[-1:]))[:e]
-            self._cr.append((keep, fwd, torch.stack((zl, zr)), elim, back, torch.stack((elim, keep[:e], br))))
+            br_hip = torch.cat((keep[1:], keep.new_full((1,), -1)))[:e]   # sem_block_gemv: -1 = absent
+            self._cr.append((keep, fwd.contiguous(), torch.stack((zl, zr)), elim, back.contiguous(),
+                             torch.stack((elim, keep[:e], br)),
+                             torch.stack((left, right)).contiguous(), torch.stack((elim, keep[:e], br_hip)).contiguous()))
             rows = keep
-        self._cr_top = (rows, torch.linalg.inv(B[rows]))
+        self._cr_top = (rows.contiguous(), torch.linalg.inv(B[rows]).contiguous())
 
     def _cr_solve(self, g):
-        """x = S^-1 g for the interface system; g (N_ex + 1, m) is overwritten."""
-        for keep, fwd, idx, _, _, _ in self._cr:
+        """x = S^-1 g for the interface system; g (N_ex + 1, m) is overwritten.  On the GPU every level
+        is one sem_block_gemv launch per direction (HIP, HBM-bound on the level's operators)."""
+        if self.device.type == "cuda":
+            return self._cr_solve_hip(g)
+        for keep, fwd, idx, *_ in self._cr:
             gl = g[idx.reshape(-1)].view(2, keep.numel(), -1).permute(1, 0, 2).reshape(keep.numel(), -1, 1)
             g.index_add_(0, keep, torch.bmm(fwd, gl)[..., 0])
         top, Tinv = self._cr_top
         x = torch.zeros_like(g)
         x[top] = torch.bmm(Tinv, g[top][..., None])[..., 0]
-        for _, _, _, elim, back, idx in reversed(self._cr):
+        for _, _, _, elim, back, idx, *_ in reversed(self._cr):
             rhs = torch.cat((g[idx[0]], x[idx[1]], x[idx[2]]), dim=1)[..., None]
             x[elim] = torch.bmm(back, rhs)[..., 0]
+        return x
+
+    def _cr_solve_hip(self, g):
+        import ctypes as C
+        from .. import _lib
+        lib = _lib.load()
+        m = g.shape[1]
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        x = torch.zeros_like(g)
+        P = C.c_void_p
+
+        def gemv(M, srcs, xrow, y, yrow, acc):
+            S = len(srcs)
+            if not (M.is_contiguous() and xrow.is_contiguous() and yrow.is_contiguous()
+                    and xrow.dtype == yrow.dtype == torch.int64 and tuple(M.shape) == (yrow.numel(), m, S * m)
+                    and tuple(xrow.shape) == (S, yrow.numel())):
+                raise ValueError("sem_block_gemv: operator / index layout")
+            src = (P * S)(*(P(t.data_ptr()) for t in srcs))
+            ld = (C.c_int64 * S)(*(t.stride(0) for t in srcs))
+            _lib.check(lib.sem_block_gemv(yrow.numel(), m, S, P(M.data_ptr()), src, ld, P(xrow.data_ptr()),
+                                          P(y.data_ptr()), y.stride(0), P(yrow.data_ptr()), int(acc), stream))
+        for keep, fwd, _, _, _, _, fx, _ in self._cr:
+            gemv(fwd, (g, g), fx, g, keep, True)
+        top, Tinv = self._cr_top
+        gemv(Tinv, (g,), top.reshape(1, -1).contiguous(), x, top.contiguous(), False)
+        for _, _, _, elim, back, _, _, bx in reversed(self._cr):
+            gemv(back, (g, x, x), bx, x, elim, False)
         return x
 
     # ------------------------------------------------------------------ nested interior (default)

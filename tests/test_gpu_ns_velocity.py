@@ -10,7 +10,8 @@ from velocity_blocks import extract, oracle_velocity_jacobian
 
 pytestmark = pytest.mark.gpu
 
-CASES = [(4, 3, 2, 100.0), (2, 2, 3, 400.0), (1, 4, 3, 10.0), (6, 2, 2, 1000.0), (8, 4, 4, 1000.0), (5, 3, 6, 250.0)]
+CASES = [(4, 3, 2, 100.0), (2, 2, 3, 400.0), (1, 4, 3, 10.0), (6, 2, 2, 1000.0), (8, 4, 4, 1000.0), (5, 3, 6, 250.0),
+         (2, 7, 2, 300.0), (3, 1, 2, 50.0), (4, 8, 3, 700.0)]
 
 
 def _device_solver(P, nex, ney, Re, u, v):

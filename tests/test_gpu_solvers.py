@@ -118,7 +118,7 @@ def test_cd_device_solve_cfg2_full_size(gpu):
     """cfg2 (64x64, P=8, N=263,169): the reference example's CD problem (Pe=40, circular flow,
     T_W/T_E = +-0.5, mtol = 1e-7) solved fully on the device, against the oracle's SciPy LGMRES
     solution on the assembled CSR (tests/golden/make_oracle_fixtures.py cd64: 2,177 matvecs, 6 min on
-    one core).  Both stop at ||res||_2 <= 1e-7 sqrt(N), so the solutions agree to ~1e-6."""
+    one core).  Both stop at ||res||_2 <= 1e-7 sqrt(N); the pin is the oracle's residual at the device solution."""
     import time
     from sem_amd.solvers import ConvectionDiffusionSolver
     g = golden("cd64_checksums.npz")
@@ -131,8 +131,9 @@ def test_cd_device_solve_cfg2_full_size(gpu):
     dt = time.perf_counter() - t0
     # the two Krylov methods stop at the same residual bound, not at the same iterate: the solutions
     # agree to the solve's accuracy, and both satisfy the reference's discrete equations
+    # (measured: samples within 1e-3, norms 1.3e-4 apart relative -- a coherent ~3e-5 per-node shift)
     assert np.abs(T[g["sample_idx"]] - g["sample_T"]).max() < 1e-3
-    assert abs(np.linalg.norm(T) - float(g["norm_T"])) < 1e-5 * float(g["norm_T"])
+    assert abs(np.linalg.norm(T) - float(g["norm_T"])) < 5e-4 * float(g["norm_T"])
     from oracle import sem_oracle as O
     ref = O.CDOracle(1.0, 1.0, 40.0, 8, 64, 64, T_W=0.5, T_E=-0.5)
     assert np.linalg.norm(ref.residuals(T, u, v)) <= 1.0001e-7 * np.sqrt(cd.N)
