@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 3
+#define SEM_ABI_VERSION 4
 
 enum sem_status {
   SEM_OK = 0,
@@ -245,7 +245,12 @@ typedef struct sem_velocity_desc {
   const double* jvv;
   const uint8_t* dir_mask;
   unsigned dir_sides;
+  int ncomp;          /* 0 or 2: the velocity pair; 1: the scalar operator A + diag(juu) alone (the
+                       * convection-diffusion Jacobian, ConvectionDiffusion_Solver.py:104-121) */
 } sem_velocity_desc;
+/* Sizes for ncomp components per node (m = ncomp N_y unknowns per line); the velocity form is
+ * sem_line_block_sizes(h, 2, sizes). */
+int sem_line_block_sizes(const sem_handle* h, int ncomp, int64_t* sizes);
 int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes);
 int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* A_II, double* D, double* aIB, double* aBI,
                         double* E, double* F, void* stream);

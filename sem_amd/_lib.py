@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE = range(6)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
@@ -41,7 +41,7 @@ class SemApplyDesc(C.Structure):
 class SemVelocityDesc(C.Structure):
     _fields_ = [("c_mass", C.c_double), ("c_stiff", C.c_double), ("c_gradx", C.c_double), ("c_grady", C.c_double),
                 ("cu", C.c_void_p), ("cv", C.c_void_p), ("juu", C.c_void_p), ("juv", C.c_void_p), ("jvu", C.c_void_p),
-                ("jvv", C.c_void_p), ("dir_mask", C.c_void_p), ("dir_sides", C.c_uint)]
+                ("jvv", C.c_void_p), ("dir_mask", C.c_void_p), ("dir_sides", C.c_uint), ("ncomp", C.c_int)]
 
 
 class SemNsDesc(C.Structure):
@@ -84,6 +84,7 @@ _SIGS = {
                                  C.c_void_p, C.c_void_p]),
     "sem_basis_update": (C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sem_velocity_block_sizes": (C.c_int, [C.c_void_p, _i64p]),
+    "sem_line_block_sizes": (C.c_int, [C.c_void_p, C.c_int, _i64p]),
     "sem_velocity_blocks": (C.c_int, [C.c_void_p, C.POINTER(SemVelocityDesc)] + [C.c_void_p] * 7),
     "sem_ns_apply": (C.c_int, [C.c_void_p, C.POINTER(SemNsDesc)] + [C.c_void_p] * 7),
     "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,

@@ -39,6 +39,7 @@ struct VelocityArgs {
   const uint8_t* mask;
   double fKx, fKy, fM, fX, fY;  // cK dy/dx, cK dx/dy, cM dx dy/4, cX dy/2, cY dx/2
   int P, nex, ney, NY, NX;
+  int nc;  // components per node: 2 (NS velocity [u | v]) or 1 (a scalar operator, e.g. the CD Jacobian)
   unsigned sides;
   double *AII, *D, *aIB, *aBI, *E, *F;
 };
@@ -52,7 +53,7 @@ __device__ __forceinline__ bool is_dirichlet(const VelocityArgs& a, int gx, int 
 // One thread per Jacobian row: row = line gx (0..NX-1), component c, node gy.
 __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs a) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int NY = a.NY, P = a.P, n = P + 1, m = 2 * NY;
+  const int NY = a.NY, P = a.P, n = P + 1, m = a.nc * NY;
   if (t >= static_cast<int64_t>(a.NX) * m) return;
   const int gx = static_cast<int>(t / m), r = static_cast<int>(t - static_cast<int64_t>(gx) * m);
   const int c = r / NY, gy = r - c * NY;
@@ -129,8 +130,10 @@ __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs
   }
   row[self] += dg;
   // the other component at the same node: J_uv = diag(juv) (u rows), J_vu = diag(jvu) (v rows)
-  const double* jc = c == 0 ? a.juv : a.jvu;
-  if (jc) row[col0 + (1 - c) * NY + gy] = jc[node];
+  if (a.nc == 2) {
+    const double* jc = c == 0 ? a.juv : a.jvu;
+    if (jc) row[col0 + (1 - c) * NY + gy] = jc[node];
+  }
 
   // x coupling to the other lines of this node's element column(s)
   if (l != 0) {
@@ -159,11 +162,12 @@ static int hip_check_v(hipError_t e, const char* what) {
 
 extern "C" {
 
-int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes) {
+int sem_line_block_sizes(const sem_handle* h, int ncomp, int64_t* sizes) {
   if (!h || !sizes) return sem::set_error(SEM_EINVAL, "null argument");
+  if (ncomp != 1 && ncomp != 2) return sem::set_error(SEM_EINVAL, "ncomp must be 1 or 2");
   if (h->ex_begin != 0 || h->ex_end != h->nex)
     return sem::set_error(SEM_EUNSUPPORTED, "the velocity blocks need a whole-mesh handle");
-  const int64_t m = 2 * h->NY, nI = static_cast<int64_t>(h->P - 1) * m, ne = h->nex;
+  const int64_t m = ncomp * h->NY, nI = static_cast<int64_t>(h->P - 1) * m, ne = h->nex;
   sizes[0] = ne * nI * nI;             // A_II
   sizes[1] = (ne + 1) * m * m;         // D
   sizes[2] = ne * (h->P - 1) * 2 * m;  // aIB
@@ -172,6 +176,8 @@ int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes) {
   sizes[5] = ne * m;                   // F
   return SEM_OK;
 }
+
+int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes) { return sem_line_block_sizes(h, 2, sizes); }
 
 int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, double* D, double* aIB, double* aBI,
                         double* E, double* F, void* stream) {
@@ -182,8 +188,12 @@ int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, 
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess || cur != h->device)
     return sem::set_error(SEM_EINVAL, "handle belongs to another device than the current one");
+  const int nc = d->ncomp == 0 ? 2 : d->ncomp;
+  if (nc != 1 && nc != 2) return sem::set_error(SEM_EINVAL, "ncomp must be 0, 1 or 2");
+  if (nc == 1 && (d->juv || d->jvu || d->jvv))
+    return sem::set_error(SEM_EINVAL, "a one-component operator has no juv / jvu / jvv term");
   int64_t sz[6];
-  sem_velocity_block_sizes(h, sz);
+  sem_line_block_sizes(h, nc, sz);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int st;
   if (h->P > 1 && (st = sem::hip_check_v(hipMemsetAsync(AII, 0, sz[0] * sizeof(double), s), "memset A_II")))
@@ -209,13 +219,14 @@ int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, 
   a.ney = h->ney;
   a.NY = static_cast<int>(h->NY);
   a.NX = static_cast<int>(h->NX);
+  a.nc = nc;
   a.AII = AII;
   a.D = D;
   a.aIB = aIB;
   a.aBI = aBI;
   a.E = E;
   a.F = F;
-  const int64_t rows = h->NX * 2 * h->NY;
+  const int64_t rows = h->NX * nc * h->NY;
   hipLaunchKernelGGL(sem::velocity_blocks_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)), dim3(256), 0, s, a);
   return sem::hip_check_v(hipGetLastError(), "velocity blocks launch");
 }

@@ -4,7 +4,9 @@ PyTorch-ROCm is plumbing here: it provides device buffers, the current HIP
 stream and (for multi-GPU) torch.distributed/RCCL.  All arithmetic of the
 operator layer runs in the HIP kernels of libsemops.
 """
+import contextlib
 import ctypes as C
+import gc
 
 import numpy as np
 import torch
@@ -137,15 +139,16 @@ class Mesh:
                                                   self.stream_ptr(stream)))
 
     def velocity_blocks(self, blocks, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None, cv=None,
-                        juu=None, juv=None, jvu=None, jvv=None, dir_mask=None, dir_sides=0, stream=None):
+                        juu=None, juv=None, jvu=None, jvv=None, dir_mask=None, dir_sides=0, ncomp=2, stream=None):
         """Static-condensation pieces of the NS velocity Jacobian (include/sem_ops.h,
-        sem_velocity_blocks) into `blocks` (VelocityJacobianSolver.empty_blocks layout)."""
+        sem_velocity_blocks) into `blocks` (VelocityJacobianSolver.empty_blocks layout); ncomp=1:
+        the scalar operator A + diag(juu) alone."""
         for nm, t in (("cu", cu), ("cv", cv), ("juu", juu), ("juv", juv), ("jvu", jvu), ("jvv", jvv)):
             self._vec(t, nm)
         if dir_mask is not None and (dir_mask.dtype != torch.uint8 or dir_mask.numel() != self.n_local):
             raise ValueError("dir_mask must be a uint8 tensor of n_local entries")
         sizes = (C.c_int64 * 6)()
-        _lib.check(self._lib.sem_velocity_block_sizes(self._h, sizes))
+        _lib.check(self._lib.sem_line_block_sizes(self._h, int(ncomp), sizes))
         names = ("AII", "D", "aIB", "aBI", "E", "F")
         for nm, sz in zip(names, sizes):
             t = blocks.get(nm)
@@ -153,7 +156,8 @@ class Mesh:
                        or not t.is_contiguous()):
                 raise ValueError(f"block {nm} must be a contiguous float64 tensor of {sz} entries on {self.device}")
         d = _lib.SemVelocityDesc(float(c_mass), float(c_stiff), float(c_gradx), float(c_grady), _ptr(cu), _ptr(cv),
-                                 _ptr(juu), _ptr(juv), _ptr(jvu), _ptr(jvv), _ptr(dir_mask), int(dir_sides))
+                                 _ptr(juu), _ptr(juv), _ptr(jvu), _ptr(jvv), _ptr(dir_mask), int(dir_sides),
+                                 int(ncomp))
         _lib.check(self._lib.sem_velocity_blocks(self._h, C.byref(d), *(_ptr(blocks.get(nm)) for nm in names),
                                                  self.stream_ptr(stream)))
         return blocks
@@ -228,3 +232,17 @@ def get_mesh(P, nex, ney, dx, dy, ex_begin=0, ex_end=None, device=None):
     if m is None:
         m = _MESHES[key] = Mesh(P, nex, ney, dx, dy, ex_begin, ex_end, dev)
     return m
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Keep Python's cyclic GC from running inside a stream capture: a collection there can run the
+    finaliser of an unrelated object (an old hipGraph, a mesh handle) whose device calls are illegal
+    while the stream captures, which aborts the process.  torch.cuda.graph collects on entry."""
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if enabled:
+            gc.enable()

@@ -17,7 +17,13 @@ plain boundary-line set the kernel derives it from geometry (no mask traffic).
 `_get_update` runs a device-resident GMRES (sem_amd/krylov.py: Krylov basis in
 HBM, CGS2 orthogonalisation as GEMVs, same stopping rule atol = mtol*sqrt(N) as
 the reference's LGMRES); `krylov="scipy"` keeps the reference's host LGMRES
-around device matvecs.
+around device matvecs.  On a whole-mesh solver the GMRES is right-preconditioned
+by a direct solve of the Jacobian itself (`precond="condensed"`, the default):
+the static condensation over node lines of the NS velocity solve
+(velocity_solve.py) with one unknown per node, factored once per Sys.  Right
+preconditioning leaves the stopping test on the true residual ||dres_op(dT) -
+dres||_2, so the reference's rule is unchanged; the Krylov count drops from
+hundreds-thousands of matvecs to one or two.
 """
 import typing
 
@@ -29,6 +35,7 @@ from .. import SEM, _lib
 from ..device import get_mesh
 from ..krylov import Recycle, gcro, gmres
 from ..operators import ConvectionTensor, SEMOperator
+from .velocity_solve import VelocityJacobianSolver
 
 
 def side_mask(points, L_x, L_y, sides):
@@ -82,7 +89,7 @@ class ConvectionDiffusionSolver:
     def __init__(self, L_x: float, L_y: float, Pe: float, P: int, N_ex: int, N_ey: int,
                  T_W: float = None, T_E: float = None, T_S: float = None, T_N: float = None,
                  mtol=1e-7, iprint: list = [], krylov: str = "device", max_basis: int = 2000,  # noqa: B006
-                 partition=None, recycle_bytes: float = 0.0):
+                 partition=None, recycle_bytes: float = 0.0, precond: str = "condensed"):
         """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip
         per rank, every apply ends with the interface exchange (overlapped with the interior) and
         the Krylov inner products are all-reduced; the reference methods still take and return
@@ -91,6 +98,11 @@ class ConvectionDiffusionSolver:
             raise ValueError("krylov must be 'device' or 'scipy'")
         if partition is not None and krylov != "device":
             raise ValueError("a partitioned solver needs krylov='device'")
+        if precond not in ("condensed", None):
+            raise ValueError("precond must be 'condensed' or None")
+        # the condensation needs the whole mesh on one device; a partitioned solver runs plain GMRES
+        self._precond = precond if partition is None else None
+        self._factor = None     # condensed Jacobian of the current Sys (rebuilt after _get_residuals)
         self._krylov, self._max_basis = krylov, max_basis
         self._part = partition
         # recycled Krylov subspace across _get_update calls with one operator (sem_amd.krylov.Recycle):
@@ -154,6 +166,7 @@ class ConvectionDiffusionSolver:
         """res = Sys T, Dirichlet rows T - T_dir (ConvectionDiffusion_Solver.py:73-92)."""
         Conv = self._Pe * (SEM.tensordot(self._C_x, self._dev(u), (1, 0)) + SEM.tensordot(self._C_y, self._dev(v), (1, 0)))
         self._Sys = Conv + self._K
+        self._factor = None
         if self._recycle is not None:   # the update operator depends on Sys
             self._recycle.reset()
         y = self._apply(self._dev(T), dir_mode=_lib.DIR_IDENTITY, dir_val=self._dir_val, **self._sys_kw(),
@@ -190,9 +203,29 @@ class ConvectionDiffusionSolver:
             return self._get_update_device(dres, dT0)
         return self._get_update_scipy(dres, dT0)
 
+    def _jacobian_solver(self):
+        """Direct solve of dres_op = Sys with Dirichlet identity rows (ConvectionDiffusion_Solver.py:
+        104-121 at du = dv = 0): sem_velocity_blocks with one component writes the condensation
+        pieces, VelocityJacobianSolver factors them; kept until Sys changes (_get_residuals)."""
+        if self._factor is None:
+            if self._Sys is None:
+                raise RuntimeError("ConvectionDiffusion: _get_residuals must run before _get_update")
+            m = self._mesh
+            vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
+            blocks = vs.empty_blocks()
+            cX, cu, cY, cv, d = self._Sys._coeffs()
+            m.velocity_blocks(blocks, c_mass=self._Sys.cM, c_stiff=self._Sys.cK, c_gradx=cX, cu=cu, c_grady=cY,
+                              cv=cv, juu=d, ncomp=1, **self._dir.kw())
+            vs.factor(blocks.pop("AII"), **blocks)
+            if m.device.type == "cuda":
+                vs.capture()
+            self._factor = vs
+        return self._factor
+
     def _get_update_device(self, dres, dT0=None):
         """GMRES with the Krylov basis in HBM; restart = min(int(0.3 N), max_basis) (the
-        reference's inner_m, capped so the basis fits device memory)."""
+        reference's inner_m, capped so the basis fits device memory), right-preconditioned by the
+        condensed direct solve when precond="condensed"."""
         b = self._dev(dres)
         x0 = self._dev(dT0)
         it = [0]
@@ -205,6 +238,10 @@ class ConvectionDiffusionSolver:
                 print(f"ConvectionDiffusion GMRES: {it[0]}\t{est}", flush=True)
 
         restart = max(1, min(int(self.N * 0.3), self._max_basis))
+        precond = None
+        if self._precond == "condensed":
+            precond = self._jacobian_solver().solve1
+            restart = min(restart, 100)
         if self._part is not None:
             r = gmres(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
                       restart=restart, callback=cb, inner=self._part.inner)
@@ -214,7 +251,8 @@ class ConvectionDiffusionSolver:
                 cap = min(n, max(restart + 1, int(self._recycle_bytes // (16 * n))))
                 self._recycle = Recycle(n, torch.float64, self._mesh.device, cap)
             r = gcro(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
-                     restart=restart, callback=cb, recycle=self._recycle)
+                     restart=restart, precond=precond, callback=cb,
+                     recycle=self._recycle if precond is None else None)
         if r.info != 0:
             raise RuntimeError(f"ConvectionDiffusion LGMRES: Failed to converge in {r.info} iterations")
         self.matvecs = r.matvecs

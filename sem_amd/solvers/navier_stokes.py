@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from .. import SEM, _lib
-from ..device import get_mesh
+from ..device import get_mesh, no_gc
 from ..krylov import Recycle, gcro
 from .convection_diffusion import DirichletRows
 from .velocity_solve import VelocityJacobianSolver
@@ -312,7 +312,7 @@ class _SchurComplement:
                 self._body(self._x)   # warm-up outside the capture (library workspaces)
             cur.wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g), no_gc():
                 self._out = self._body(self._x)
             self._graph = g
         except RuntimeError:

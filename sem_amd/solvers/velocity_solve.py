@@ -24,12 +24,33 @@ condensation itself is unit-tested on CPU against SciPy's sparse solve
 """
 import torch
 
+from ..device import no_gc
+
+
+def batched_inverse(A):
+    """torch.linalg.inv of a batch of blocks.  The batched rocSOLVER getrf behind it has been seen
+    to fail its workspace allocation for some (n, batch) shapes (64 blocks of 455^2 on MI355X,
+    HIPBLAS_STATUS_ALLOC_FAILED) where smaller batches go through: on that error the batch is
+    inverted in chunks, halving down to single blocks.  The result is the same either way."""
+    try:
+        return torch.linalg.inv(A)
+    except RuntimeError as e:
+        if "ALLOC_FAILED" not in str(e) or A.dim() < 3 or A.shape[0] == 1:
+            raise
+    out = torch.empty_like(A)
+    step = max(1, A.shape[0] // 2)
+    for i in range(0, A.shape[0], step):
+        out[i:i + step] = batched_inverse(A[i:i + step])
+    return out
+
 
 class VelocityJacobianSolver:
     """x = J^-1 b for the velocity Jacobian J of one linearisation, J given by its condensation pieces."""
 
-    def __init__(self, P, nex, ney, device, interior="nested", sweep="cr"):
-        """interior: elimination of the element-column interiors ("nested" static condensation, or
+    def __init__(self, P, nex, ney, device, interior="nested", sweep="cr", ncomp=2):
+        """ncomp: unknowns per node -- 2 for the velocity pair [u | v], 1 for a scalar operator
+        (the convection-diffusion Jacobian, or the pressure stiffness of the Schur preconditioner).
+        interior: elimination of the element-column interiors ("nested" static condensation, or
         one dense block per column: "lu" factors, "inverse" explicit inverses).  sweep: solve of the
         block-tridiagonal interface system ("cr": block cyclic reduction, about 2 log2(N_ex) batched
         launches; "thomas": block Thomas, 2 N_ex sequential steps)."""
@@ -39,10 +60,12 @@ class VelocityJacobianSolver:
             raise ValueError("interior must be 'nested', 'lu' or 'inverse'")
         if sweep not in ("cr", "thomas"):
             raise ValueError("sweep must be 'cr' or 'thomas'")
-        self.sweep = sweep
+        if ncomp not in (1, 2):
+            raise ValueError("ncomp must be 1 or 2")
+        self.sweep, self.ncomp = sweep, ncomp
         self.P, self.nex, self.ney = P, nex, ney
         self.NY, self.NX = ney * P + 1, nex * P + 1
-        self.m = 2 * self.NY
+        self.m = ncomp * self.NY
         self.nI = (P - 1) * self.m
         self.device = torch.device(device)
         self.interior = interior
@@ -146,7 +169,7 @@ class VelocityJacobianSolver:
             right = torch.full((k,), -1, dtype=torch.long, device=dev)
             left[1:] = elim[:k - 1]
             right[:elim.numel()] = elim
-            Binv = torch.linalg.inv(B[elim])
+            Binv = batched_inverse(B[elim])
             hasl, hasr = left >= 0, right >= 0
             zl, zr = left.clamp(min=0), right.clamp(min=0)
             pos = torch.full((n,), -1, dtype=torch.long, device=dev)
@@ -170,7 +193,7 @@ class VelocityJacobianSolver:
                              torch.stack((elim, keep[:e], br)),
                              torch.stack((left, right)).contiguous(), torch.stack((elim, keep[:e], br_hip)).contiguous()))
             rows = keep
-        self._cr_top = (rows.contiguous(), torch.linalg.inv(B[rows]).contiguous())
+        self._cr_top = (rows.contiguous(), batched_inverse(B[rows]).contiguous())
 
     def _cr_solve(self, g):
         """x = S^-1 g for the interface system; g (N_ex + 1, m) is overwritten.  On the GPU every level
@@ -226,7 +249,7 @@ class VelocityJacobianSolver:
         P, ney, NY, m = self.P, self.ney, self.NY, self.m
         dev = self.device
         l = torch.arange(1, P, device=dev)
-        c = torch.arange(2, device=dev)
+        c = torch.arange(self.ncomp, device=dev)
         col = lambda ll, cc, gy: (ll - 1) * m + cc * NY + gy  # noqa: E731  column-interior ordering
         # element interiors: (n, l, c, j) with gy = nP + j, j = 1..P-1
         n = torch.arange(ney, device=dev)
@@ -236,7 +259,7 @@ class VelocityJacobianSolver:
         # edges: (k, l, c) with gy = kP, k = 0..ney
         k = torch.arange(ney + 1, device=dev)
         pe = col(l[None, :, None], c[None, None, :], k[:, None, None] * P)
-        self._ne1 = 2 * (P - 1)                                         # unknowns per edge row k
+        self._ne1 = self.ncomp * (P - 1)                                # unknowns per edge row k
         self._pe = pe.reshape(-1)                                       # (n_e,)
         self._pe_el = torch.cat((pe[:-1].reshape(ney, -1), pe[1:].reshape(ney, -1)), dim=1)  # edges k=n, n+1
 
@@ -249,7 +272,7 @@ class VelocityJacobianSolver:
         A_ie = AII[e, pi[None, :, :, None], pel[None, :, None, :]]    # (nex, ney, ni, 2 ne1)
         A_ei = AII[e, pel[None, :, :, None], pi[None, :, None, :]]    # (nex, ney, 2 ne1, ni)
         S_e = AII[e[:, :, 0], pe[None, :, None], pe[None, None, :]]   # (nex, n_e, n_e)
-        self._Xi = torch.linalg.inv(A_ii)
+        self._Xi = batched_inverse(A_ii.reshape(-1, *A_ii.shape[-2:])).view(A_ii.shape)
         self._Yie = self._Xi @ A_ie
         self._Aei = A_ei
         C = (A_ei @ self._Yie).view(nex, ney, 2, self._ne1, 2, self._ne1)
@@ -258,7 +281,7 @@ class VelocityJacobianSolver:
         for a in range(2):          # element n touches edge rows k = n + a, columns k = n + b
             for b in range(2):
                 S[:, n + a, :, n + b, :] -= C[:, :, a, :, b, :].permute(1, 0, 2, 3)  # index dims lead
-        self._Se_inv = torch.linalg.inv(S_e)
+        self._Se_inv = batched_inverse(S_e)
 
     def _nested_solve(self, R):
         """A_II^-1 R for every column at once; R (nex, nI, k)."""
@@ -335,7 +358,7 @@ class VelocityJacobianSolver:
                 self._solve_lines(self._bin)      # warm-up outside the capture (library workspaces)
             cur.wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g), no_gc():
                 self._xout = self._solve_lines(self._bin)
             self._graph = g
             return True
@@ -344,10 +367,25 @@ class VelocityJacobianSolver:
             self._graph = None
             return False
 
+    def solve1(self, b):
+        """x = A^-1 b for a one-component operator; b is a length-N vector in the x-major numbering."""
+        if not self.factored:
+            raise RuntimeError("factor() first")
+        if self.ncomp != 1:
+            raise ValueError("solve1 needs ncomp=1")
+        NX, NY = self.NX, self.NY
+        if getattr(self, "_graph", None) is not None:
+            self._bin.copy_(b.reshape(NX, NY))
+            self._graph.replay()
+            return self._xout.reshape(-1).clone()
+        return self._solve_lines(b.reshape(NX, NY).clone()).reshape(-1)
+
     def solve(self, bu, bv):
         """(J^-1 [bu; bv]) split as (xu, xv); bu, bv are length-N vectors in the x-major numbering."""
         if not self.factored:
             raise RuntimeError("factor() first")
+        if self.ncomp != 2:
+            raise ValueError("solve needs ncomp=2; use solve1")
         NX, NY = self.NX, self.NY
         if getattr(self, "_graph", None) is not None:
             b3 = self._bin.view(NX, 2, NY)

@@ -94,14 +94,16 @@ def test_readme_helmholtz_with_scipy_cg(gpu):
     assert np.abs(u - exact).max() < 1e-3
 
 
-def test_cd_device_solve_16x16_against_oracle(gpu):
+@pytest.mark.parametrize("precond", ["condensed", None])
+def test_cd_device_solve_16x16_against_oracle(gpu, precond):
     """16x16, P=8 circular-flow CD solve fully on the device vs the oracle's SciPy LGMRES on the
-    assembled CSR, run here (tight mtol)."""
+    assembled CSR, run here (tight mtol); with the condensed direct-solve preconditioner (default)
+    and plain GMRES."""
     import time
     from oracle import sem_oracle as O
     from sem_amd.solvers import ConvectionDiffusionSolver
     P, ne = 8, 16
-    cd = ConvectionDiffusionSolver(1.0, 1.0, 40.0, P, ne, ne, T_W=0.5, T_E=-0.5, mtol=1e-9)
+    cd = ConvectionDiffusionSolver(1.0, 1.0, 40.0, P, ne, ne, T_W=0.5, T_E=-0.5, mtol=1e-9, precond=precond)
     u = cd._get_vector(lambda x, y: y - 0.5)
     v = cd._get_vector(lambda x, y: 0.5 - x)
     t0 = time.perf_counter()
@@ -111,7 +113,9 @@ def test_cd_device_solve_16x16_against_oracle(gpu):
     Tref = ref.solution(u, v, mtol=1e-9)
     assert np.abs(T - Tref).max() < 1e-6
     assert np.abs(cd._get_residuals(T, u, v)).max() < 1e-7
-    print(f"device CD solve {ne}x{ne} P={P}: {t_dev:.3f} s")
+    if precond == "condensed":
+        assert cd.matvecs <= 5
+    print(f"device CD solve {ne}x{ne} P={P} precond={precond}: {t_dev:.3f} s, {cd.matvecs} matvecs")
 
 
 def test_cd_device_solve_cfg2_full_size(gpu):

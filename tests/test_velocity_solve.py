@@ -7,7 +7,7 @@ import pytest
 import scipy.sparse.linalg as spla
 import torch
 
-from velocity_blocks import assemble, extract, oracle_velocity_jacobian
+from velocity_blocks import assemble, extract, oracle_cd_jacobian, oracle_velocity_jacobian
 from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
 
 CASES = [(4, 3, 2, 100.0), (2, 2, 3, 400.0), (1, 4, 3, 10.0), (6, 2, 2, 1000.0), (3, 1, 1, 1.0), (2, 7, 2, 300.0),
@@ -38,3 +38,23 @@ def test_condensed_solve_matches_sparse_lu(P, nex, ney, Re, interior, sweep):
     J = ns.Jvelo
     res = J @ got - np.hstack((bu, bv))
     assert np.abs(res).max() <= 1e-11 * (abs(J).max() * np.abs(got).max())
+
+
+@pytest.mark.parametrize("P,nex,ney,Pe", [(4, 3, 2, 40.0), (8, 2, 3, 710.0), (1, 4, 3, 10.0), (3, 1, 1, 1.0)])
+@pytest.mark.parametrize("sweep", ["cr", "thomas"])
+def test_scalar_condensation_solves_the_cd_jacobian(P, nex, ney, Pe, sweep):
+    """ncomp=1: the convection-diffusion Jacobian (the CD solver's preconditioner) condenses the
+    same way, and the condensed solve reproduces SciPy's sparse solve."""
+    cd, A, _, _ = oracle_cd_jacobian(P, nex, ney, Pe, seed=P + nex)
+    Ad = A.toarray()
+    pcs = extract(Ad, P, nex, ney, ncomp=1)
+    assert np.array_equal(assemble(pcs, P, nex, ney, ncomp=1), Ad)
+    pcs = {k: torch.as_tensor(v) for k, v in pcs.items()}
+    vs = VelocityJacobianSolver(P, nex, ney, "cpu", sweep=sweep, ncomp=1)
+    vs.factor(pcs.get("AII"), pcs["D"], pcs.get("aIB"), pcs.get("aBI"), pcs["E"], pcs["F"])
+    b = np.random.default_rng(7).uniform(-1, 1, cd.N)
+    got = vs.solve1(torch.as_tensor(b)).numpy()
+    want = spla.spsolve(A.tocsc(), b)
+    assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
+    with pytest.raises(ValueError):
+        vs.solve(torch.as_tensor(b), torch.as_tensor(b))

@@ -8,10 +8,10 @@ def _idx(N, NY, c, gx, gy):
     return c * N + gx * NY + gy
 
 
-def extract(J, P, nex, ney):
-    """Pieces of the 2N x 2N matrix J (dense ndarray)."""
+def extract(J, P, nex, ney, ncomp=2):
+    """Pieces of the ncomp N x ncomp N matrix J (dense ndarray)."""
     NY, NX = ney * P + 1, nex * P + 1
-    N, m = NX * NY, 2 * NY
+    N, m = NX * NY, ncomp * NY
     cg = np.arange(m)
     comp, gy = cg // NY, cg % NY
     out = {"D": np.zeros((nex + 1, m, m)), "E": np.zeros((nex, m)), "F": np.zeros((nex, m))}
@@ -39,13 +39,13 @@ def extract(J, P, nex, ney):
     return out
 
 
-def assemble(pieces, P, nex, ney):
-    """The dense 2N x 2N matrix the pieces describe (every entry they do not name is zero)."""
+def assemble(pieces, P, nex, ney, ncomp=2):
+    """The dense ncomp N x ncomp N matrix the pieces describe (every entry they do not name is zero)."""
     NY, NX = ney * P + 1, nex * P + 1
-    N, m = NX * NY, 2 * NY
+    N, m = NX * NY, ncomp * NY
     cg = np.arange(m)
     comp, gy = cg // NY, cg % NY
-    J = np.zeros((2 * N, 2 * N))
+    J = np.zeros((ncomp * N, ncomp * N))
     for L in range(nex + 1):
         r = _idx(N, NY, comp, L * P, gy)
         J[np.ix_(r, r)] = pieces["D"][L]
@@ -77,3 +77,18 @@ def oracle_velocity_jacobian(P, nex, ney, Re, seed, Lx=1.0, Ly=1.0):
     ns.calc_jacobians(u, v)
     ns.velocity_lu()
     return ns, u, v
+
+
+def oracle_cd_jacobian(P, nex, ney, Pe, seed, Lx=1.0, Ly=1.0):
+    """The oracle CD's dres operator at du = dv = 0 (Sys with Dirichlet identity rows,
+    ConvectionDiffusion_Solver.py:104-121) at random (u, v), as a SciPy CSR."""
+    import scipy.sparse as sp
+    from oracle import sem_oracle as O
+    cd = O.CDOracle(Lx, Ly, Pe, P, nex, ney, T_W=0.5, T_E=-0.5)
+    r = np.random.default_rng(seed)
+    u, v = r.uniform(-1, 1, cd.N), r.uniform(-1, 1, cd.N)
+    cd.residuals(np.zeros(cd.N), u, v)
+    A = cd.Sys.tolil()
+    A[cd.mask, :] = 0
+    A[cd.mask, cd.mask] = 1
+    return cd, sp.csr_matrix(A), u, v

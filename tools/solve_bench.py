@@ -8,7 +8,9 @@ for that at 32^2, P=8 on one host core, 12.2 s of it in Arnoldi.
 
 This times three paths on the same problem:
 * device: ConvectionDiffusionSolver(krylov="device"), the default.  Right-preconditioned GMRES
-  with its basis in HBM, every matvec the fused band apply.
+  with its basis in HBM, every matvec the fused band apply; the preconditioner is the condensed
+  direct solve of the Jacobian (precond="condensed", factor time included).
+* device_gmres: the same without preconditioner (precond=None): plain GMRES.
 * scipy: the same solver with krylov="scipy".  The reference's LGMRES on the host around device
   matvecs.
 * oracle: CDOracle.solution on the host, the reference's own arithmetic (CSR SpMV + LGMRES).
@@ -37,6 +39,7 @@ def main():
     ap.add_argument("--Pe", type=float, default=40.0)
     ap.add_argument("--oracle", type=int, default=1, help="also time the host oracle (about 15 s at 32^2, P=8)")
     ap.add_argument("--scipy", type=int, default=1, help="also time the device-matvec + host LGMRES path")
+    ap.add_argument("--plain", type=int, default=1, help="also time the unpreconditioned device GMRES")
     args = ap.parse_args()
     from oracle import sem_oracle as O
     from sem_amd.solvers import ConvectionDiffusionSolver
@@ -46,8 +49,10 @@ def main():
     u_f = lambda x, y: y - 0.5  # noqa: E731
     v_f = lambda x, y: 0.5 - x  # noqa: E731
     res = {}
-    for kry in ["device"] + (["scipy"] if args.scipy else []):
-        cd = ConvectionDiffusionSolver(1.0, 1.0, Pe, P, ne, ne, T_E=-0.5, T_W=0.5, krylov=kry)
+    paths = [("device", "device", "condensed")] + ([("device_gmres", "device", None)] if args.plain else []) \
+        + ([("scipy", "scipy", None)] if args.scipy else [])
+    for name, kry, pc in paths:
+        cd = ConvectionDiffusionSolver(1.0, 1.0, Pe, P, ne, ne, T_E=-0.5, T_W=0.5, krylov=kry, precond=pc)
         u, v = cd._get_vector(u_f), cd._get_vector(v_f)
         cd._get_solution(u, v)  # warm-up (kernel load, caches)
         torch.cuda.synchronize()
@@ -64,8 +69,9 @@ def main():
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         T = T.cpu().numpy() if isinstance(T, torch.Tensor) else np.asarray(T)
-        res[kry] = T
-        out[kry] = {"wall_s": wall, "matvecs": count[0], "N": cd.N}
+        res[name] = T
+        out[name] = {"wall_s": wall, "matvecs": count[0], "N": cd.N,
+                     "residual_2norm": float(np.linalg.norm(cd._get_residuals(T, u, v)))}
     if args.oracle:
         ref = O.CDOracle(1.0, 1.0, Pe, P, ne, ne, T_W=0.5, T_E=-0.5)
         u, v = ref.points[1] - 0.5, 0.5 - ref.points[0]
