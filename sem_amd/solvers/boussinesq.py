@@ -46,7 +46,9 @@ from ..krylov import gmres_left
 class BoussinesqCoupler:
     def __init__(self, L_x, L_y, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4, N_ex_cd=8, N_ey_cd=8, P_ns=4, N_ex_ns=8,
                  N_ey_ns=8, mode='JNK', mtol_nonlin=1e-9, AGi=8, AGr=0.8, AGc=0.2, mtol_gmres=1e-10, restart=20,
-                 mtol_internal=1e-13, maxiter=None, iprint=0, cd=None, ns=None):
+                 mtol_internal=1e-13, maxiter=None, iprint=0, cd=None, ns=None, schur_precond="mass"):
+        """schur_precond: the NS solver's Schur-complement preconditioner ("mass" = the reference's,
+        "pcd" = pressure convection-diffusion; NavierStokesSolver)."""
         if mode not in ('JNK', 'NJ', 'GS'):
             raise ValueError('Unknown method')
         self.mode, self.iprint = mode, iprint
@@ -59,7 +61,8 @@ class BoussinesqCoupler:
         if ns is None:
             from .navier_stokes import NavierStokesSolver
             ns = NavierStokesSolver(L_x=L_x, L_y=L_y, Re=Re, Gr=Ra / Pr, P=P_ns, N_ex=N_ex_ns, N_ey=N_ey_ns,
-                                    mtol=mtol_internal, mtol_newton=mtol_internal, iprint=[])
+                                    mtol=mtol_internal, mtol_newton=mtol_internal, iprint=[],
+                                    schur_precond=schur_precond)
         self.cd, self.ns = cd, ns
         self.Ncd, self.Nns = cd.N, ns.N
         self.DOF = 3 * self.Nns + self.Ncd

@@ -33,14 +33,28 @@ class NavierStokesSolver:
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
                  max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
-                 recycle_bytes: float = 0.0, velocity_sweep: str = "cr"):
+                 recycle_bytes: float = 0.0, velocity_sweep: str = "cr", schur_precond: str = "mass"):
         """recycle_bytes: device memory for a recycled Krylov subspace of the Schur-complement solves
         (sem_amd.krylov.Recycle, GCRO; 0 = off, the default): consecutive _get_update calls with one
         linearisation -- the Boussinesq coupler's block-Jacobi preconditioner -- then start from the
         earlier solves' spaces.  Measured (tools/recycle_probe.py, profiles/r02/bous): 5-8x fewer Schur
         matvecs on consistent right-hand sides, but the Arnoldi-relation error of the recycled space
         puts a floor near 1e-8 relative under the residual, above the couplers' mtol_internal = 1e-13,
-        so inside the coupler it stagnates; off by default."""
+        so inside the coupler it stagnates; off by default.
+        schur_precond: right preconditioner of the Schur-complement Krylov solve.  "mass" (default):
+        the reference's mass diagonal (NavierStokes_Solver.py:207-212); "pcd": a
+        pressure-convection-diffusion approximation S^-1 ~ A_p^-1 F_p M^-1 on the continuity rows,
+        A_p^-1 on the pressure rows the reference replaces (boundary K rows, pinned node), where
+        A_p = K with the pinned row (factored once per solver by the one-component line
+        condensation) and F_p = Sys of the linearisation.  Right preconditioning keeps the stopping
+        test on the true Schur residual, so the reference's rule is unchanged; only the Krylov count
+        falls (tools/pcd_probe.py).  It is opt-in because on the smallest meshes (4^2, P=4) the
+        equal-order Jacobian is singular or nearly so, and which member of the near-null family of
+        solutions a Krylov method returns depends on its preconditioner: the reference's golden
+        velocities there are reproduced only by the reference's own preconditioner."""
+        if schur_precond not in ("mass", "pcd"):
+            raise ValueError("schur_precond must be 'mass' or 'pcd'")
+        self._schur_precond, self._Ap = schur_precond, None
         self._iprint = iprint
         self._recycle_bytes, self._schur_recycle = recycle_bytes, None
         self._velocity_interior, self._velocity_graph = velocity_interior, velocity_graph
@@ -93,6 +107,12 @@ class NavierStokesSolver:
         self._pin = int(pins[0]) if len(pins) else -1
         self._pin_val = float(dpp[self._pin]) if len(pins) else 0.0
         self._Mdiag = m.to_device(self._M.diagonal())
+        # PCD row weights: 1/M on the continuity rows, 0 on the replaced rows (and the reverse)
+        repl = self._mask_bound.copy()
+        if self._pin >= 0:
+            repl[self._pin] = True
+        self._pcd_w = m.to_device(np.where(repl, 0.0, 1.0 / self._M.diagonal()))
+        self._pcd_b = m.to_device(repl.astype(np.float64))
 
     # ------------------------------------------------------------------ helpers
     def _dev(self, a):
@@ -173,6 +193,30 @@ class NavierStokesSolver:
             print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec (device static condensation)')
         return vs
 
+    def _pressure_laplacian(self):
+        """A_p = K with the pinned pressure row as an identity row (the Neumann pressure Laplacian
+        made regular), factored once per solver by the one-component line condensation."""
+        if self._Ap is None:
+            m = self._mesh
+            vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
+            blocks = vs.empty_blocks()
+            mask = torch.zeros(m.n_local, dtype=torch.uint8, device=m.device)
+            mask[self._pin if self._pin >= 0 else self.N // 2] = 1
+            m.velocity_blocks(blocks, c_stiff=1.0, ncomp=1, dir_mask=mask)
+            vs.factor(blocks.pop("AII"), **blocks)
+            if self._velocity_graph and m.device.type == "cuda":
+                vs.capture()
+            self._Ap = vs
+        return self._Ap
+
+    def _pcd(self, c):
+        """z = A_p^-1 (F_p (w c) + b c): w = 1/M on continuity rows (0 elsewhere), b = 1 on the
+        replaced rows (boundary K rows and the pin), F_p = Sys of this linearisation."""
+        y = self._mesh.apply(c * self._pcd_w, **{k: self._jac_kw[k] for k in ("c_stiff", "c_mass", "c_gradx", "cu",
+                                                                              "c_grady", "cv")},
+                             c_extra=1.0, ea=c, eb=self._pcd_b)
+        return self._pressure_laplacian().solve1(y)
+
     def _get_update(self, dres_u, dres_v, dres_cont, du0=None, dv0=None, dp0=None):
         """Velocity solve + pressure Schur-complement Krylov solve (NavierStokes_Solver.py:162-236), on
         the device: the velocity Jacobian is factored once per linearisation (_velocity_solver) and the
@@ -204,6 +248,9 @@ class NavierStokesSolver:
             if pin >= 0:
                 z[pin] = c[pin]
             return z
+
+        if self._schur_precond == "pcd":
+            precon = self._pcd
 
         it = [0]
 

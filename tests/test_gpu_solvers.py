@@ -145,7 +145,8 @@ def test_cd_device_solve_cfg2_full_size(gpu):
           f"{float(g['seconds']):.0f} s)")
 
 
-def test_ns_lid_driven_8x8_re400_against_oracle(gpu):
+@pytest.mark.parametrize("schur_precond", ["pcd", "mass"])
+def test_ns_lid_driven_8x8_re400_against_oracle(gpu, schur_precond):
     """Lid-driven cavity 8x8, P=8, Re=400 (the reference's measured NS case): the
     device Newton iteration (device velocity solves, device Schur GMRES) against the oracle's
     (SuperLU + LGMRES, tests/golden/make_oracle_fixtures.py ns8): same Newton count, same velocity;
@@ -154,17 +155,24 @@ def test_ns_lid_driven_8x8_re400_against_oracle(gpu):
     from oracle import sem_oracle as O
     from sem_amd.solvers import NavierStokesSolver
     g = golden("ns8_re400.npz")
-    ns = NavierStokesSolver(1.0, 1.0, 400.0, 0.0, 8, 8, 8, u_N=1.0, iprint=[])
+    ns = NavierStokesSolver(1.0, 1.0, 400.0, 0.0, 8, 8, 8, u_N=1.0, iprint=[], schur_precond=schur_precond)
     u, v, p = ns._get_solution(np.zeros(ns.N))
     assert ns._k == int(g["newton_iters"])
-    # both Newton iterations stop at ||res||_2 <= 1e-5 sqrt(3N): velocities agree to that level
-    assert np.abs(u - g["u"]).max() < 1e-4 and np.abs(v - g["v"]).max() < 1e-4
     ref = O.NSOracle(1.0, 1.0, 400.0, 0.0, 8, 8, 8, u_N=1.0)
     res = ref.residuals(u, v, p, np.zeros(ns.N))
     assert np.linalg.norm(res) <= 1e-5 * np.sqrt(3 * ns.N)
+    du, dv = np.abs(u - g["u"]), np.abs(v - g["v"])
+    print(f"schur_precond={schur_precond}: |res| {np.linalg.norm(res):.3e}, max |u - u_ref| {du.max():.3e} at node "
+          f"{int(du.argmax())} {ns.points[:, int(du.argmax())]}, max |v - v_ref| {dv.max():.3e} at {int(dv.argmax())}, "
+          f"Newton history {ns.newton_history}")
+    if schur_precond == "mass":
+        # the reference's own preconditioner: both Newton iterations stop at ||res||_2 <= 1e-5 sqrt(3N)
+        # along the same Krylov path; velocities agree to that level
+        assert du.max() < 1e-4 and dv.max() < 1e-4
 
 
-def test_ns_cfg3_lid_driven_re1000(gpu):
+@pytest.mark.parametrize("schur_precond", ["mass", "pcd"])
+def test_ns_cfg3_lid_driven_re1000(gpu, schur_precond):
     """cfg3: lid-driven cavity Re=1000, 32x32 elements, P=8 (N=66,049) end to end on the device.
     Newton from rest diverges at Re=1000 (for the oracle as for the device), so the solve continues
     in Re through the reference API's initial guesses (_get_solution u0, v0, p0): 100 -> 400 -> 1000.
@@ -179,7 +187,7 @@ def test_ns_cfg3_lid_driven_re1000(gpu):
     from sem_amd.solvers import NavierStokesSolver
     u = v = p = None
     for Re in (100.0, 400.0, 1000.0):
-        ns = NavierStokesSolver(1.0, 1.0, Re, 0.0, 8, 32, 32, u_N=1.0, iprint=[])
+        ns = NavierStokesSolver(1.0, 1.0, Re, 0.0, 8, 32, 32, u_N=1.0, iprint=[], schur_precond=schur_precond)
         u, v, p = ns._get_solution(np.zeros(ns.N), u0=u, v0=v, p0=p)
     assert ns._k <= 6
     ref = O.NSOracle(1.0, 1.0, 1000.0, 0.0, 8, 32, 32, u_N=1.0)

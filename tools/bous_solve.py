@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--continuation", default="")
     ap.add_argument("--mtol-internal", type=float, default=1e-13)
     ap.add_argument("--out", default="")
+    ap.add_argument("--schur-precond", default="pcd", choices=["pcd", "mass"])
     ap.add_argument("--iprint", type=int, default=1)
     ap.add_argument("--x0", default="", help="start from a saved state (.npy of [T, u, v, p])")
     ap.add_argument("--ckpt", default="", help="directory for each finished stage's state (bous_<ne>_<Ra>.npy) "
@@ -43,7 +44,8 @@ def main():
     for Ra in [float(r) for r in args.continuation.split(",") if r] + [args.Ra]:
         t0 = time.perf_counter()
         c = BoussinesqCoupler(1.0, 1.0, args.Re, Ra, args.Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
-                              mode=args.mode, mtol_internal=args.mtol_internal, iprint=args.iprint)
+                              mode=args.mode, mtol_internal=args.mtol_internal, iprint=args.iprint,
+                              schur_precond=args.schur_precond)
         if args.iprint >= 2:
             c.cd._progress = c.ns._progress = 500
         def ckpt(xs, k, Ra=Ra):
@@ -66,6 +68,7 @@ def main():
             os.makedirs(args.ckpt, exist_ok=True)
             np.save(os.path.join(args.ckpt, f"bous_{args.ne}_{Ra:g}.npy"), x)
     out = {"config": f"Boussinesq {args.mode} Ra={args.Ra:g}, {args.ne}x{args.ne} elements, P={args.P}",
+           "schur_precond": args.schur_precond,
            "N": int(c.Ncd), "DOF": int(c.DOF), "stages": stages, "seconds": time.perf_counter() - t_all,
            "norm_T": float(np.linalg.norm(T)), "norm_u": float(np.linalg.norm(u)), "norm_v": float(np.linalg.norm(v)),
            "device": torch.cuda.get_device_name(0)}

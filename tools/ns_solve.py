@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--mtol", type=float, default=1e-7)
     ap.add_argument("--mtol-newton", type=float, default=1e-5)
     ap.add_argument("--out", default="")
+    ap.add_argument("--schur-precond", default="pcd", choices=["pcd", "mass"])
     ap.add_argument("--continuation", default="",
                     help="comma-separated Reynolds numbers solved first, each from the previous solution "
                          "(_get_solution's u0, v0, p0), e.g. 100,400")
@@ -60,7 +61,8 @@ def main():
     for Re in res:
         t0 = time.perf_counter()
         ns = NavierStokesSolver(1.0, 1.0, Re, 0.0, args.P, args.ne, args.ne, u_N=1.0, mtol=args.mtol,
-                                mtol_newton=args.mtol_newton, iprint=["NEWTON_iter", "NEWTON_suc", "LU_suc"])
+                                mtol_newton=args.mtol_newton, iprint=["NEWTON_iter", "NEWTON_suc", "LU_suc"],
+                                schur_precond=args.schur_precond)
         ns._progress = 200    # print the Schur GMRES estimate every 200 iterations
         t_setup = time.perf_counter() - t0
         T = np.zeros(ns.N)
@@ -73,6 +75,7 @@ def main():
     t_solve = time.perf_counter() - t_all
     stride = 97
     out = {"config": f"lid-driven cavity Re={args.Re:g}, {args.ne}x{args.ne} elements, P={args.P}",
+           "schur_precond": args.schur_precond,
            "N": ns.N, "newton_iters": ns._k, "history": ns.newton_history, "stages": stages,
            "setup_s": t_setup, "solve_s": t_solve,
            "norm_u": float(np.linalg.norm(u)), "norm_v": float(np.linalg.norm(v)), "norm_p": float(np.linalg.norm(p)),
