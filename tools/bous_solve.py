@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--continuation", default="")
     ap.add_argument("--mtol-internal", type=float, default=1e-13)
     ap.add_argument("--out", default="")
-    ap.add_argument("--schur-precond", default="pcd", choices=["pcd", "mass"])
+    ap.add_argument("--schur-precond", default="mass", choices=["pcd", "mass"])
     ap.add_argument("--iprint", type=int, default=1)
     ap.add_argument("--x0", default="", help="start from a saved state (.npy of [T, u, v, p])")
     ap.add_argument("--ckpt", default="", help="directory for each finished stage's state (bous_<ne>_<Ra>.npy) "

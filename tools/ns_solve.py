@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--mtol", type=float, default=1e-7)
     ap.add_argument("--mtol-newton", type=float, default=1e-5)
     ap.add_argument("--out", default="")
-    ap.add_argument("--schur-precond", default="pcd", choices=["pcd", "mass"])
+    ap.add_argument("--schur-precond", default="mass", choices=["pcd", "mass"])
     ap.add_argument("--continuation", default="",
                     help="comma-separated Reynolds numbers solved first, each from the previous solution "
                          "(_get_solution's u0, v0, p0), e.g. 100,400")
