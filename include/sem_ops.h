@@ -255,6 +255,38 @@ int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes);
 int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* A_II, double* D, double* aIB, double* aBI,
                         double* E, double* F, void* stream);
 
+/* ---- nested interior solve of the condensation (velocity / CD Jacobian) ---- */
+/* y = A_II^-1 r for every element column at once, from the factor VelocityJacobianSolver keeps
+ * (sem_amd/solvers/velocity_solve.py; layouts in sem_amd/csrc/ns_condense.hip): per element the
+ * interior inverse Xi (ni x ni), A_ei (2 ne1 x ni) and Xi A_ie (ni x 2 ne1), per column the inverse
+ * edge Schur block Se (n_e x n_e), every block stored column-major; pi (N_ey, ni) and pe (n_e) are the column-interior offsets of
+ * the element interiors and edges; T, C, Ye are work arrays of nex N_ey ni, nex N_ey 2 ne1 and
+ * nex n_e doubles.  ni = nc (P-1)^2, ne1 = nc (P-1), n_e = (N_ey+1) ne1, m = nc N_y.  Replaces the
+ * reference's SuperLU triangular solves (NavierStokes_Solver.py:189-203). */
+typedef struct sem_nested_desc {
+  int P, nex, ney, nc;
+  int64_t NY;
+  const double* Xi;
+  const double* Aei;
+  const double* Yie;
+  const double* Se;
+  const int64_t* pi;
+  const int64_t* pe;
+  double* T;
+  double* C;
+  double* Ye;
+} sem_nested_desc;
+/* Column e's right-hand side at R + e ld_r (interior offsets o = (l-1) m + c N_y + gy), minus
+ * aIB[e][l-1][s][.] xB[e+s][.] when aIB and xB are given (the back substitution r = b - A_IB x_B);
+ * the solution goes to Y + e ld_y at the same offsets.  Three launches, stream-ordered. */
+int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB, const double* xB,
+                     double* Y, int64_t ld_y, void* stream);
+/* g[L] = B[L P] - sum_l aBI[L][0][l] yI[L][l] - sum_l aBI[L-1][1][l] yI[L-1][l] (L = 0..nex, rows
+ * of m doubles; B rows ld_b apart, yI columns ld_yI apart): the interface right-hand side of the
+ * condensed solve. */
+int sem_interface_rhs(int P, int nex, int m, const double* B, int64_t ld_b, const double* aBI, const double* yI,
+                      int64_t ld_yI, double* g, void* stream);
+
 /* ---- batched block GEMV (interface sweep of the velocity solve) ----------- */
 /* y[yrow[b]] (+)= sum_{s<S} M[b][:, s m:(s+1) m] . src[s][xrow[s nb + b]]  for b < nb (S <= 3):
  * one level of the block cyclic reduction that solves the interface system of the condensed

@@ -44,6 +44,12 @@ class SemVelocityDesc(C.Structure):
                 ("jvv", C.c_void_p), ("dir_mask", C.c_void_p), ("dir_sides", C.c_uint), ("ncomp", C.c_int)]
 
 
+class SemNestedDesc(C.Structure):
+    _fields_ = [("P", C.c_int), ("nex", C.c_int), ("ney", C.c_int), ("nc", C.c_int), ("NY", C.c_int64),
+                ("Xi", C.c_void_p), ("Aei", C.c_void_p), ("Yie", C.c_void_p), ("Se", C.c_void_p),
+                ("pi", C.c_void_p), ("pe", C.c_void_p), ("T", C.c_void_p), ("C", C.c_void_p), ("Ye", C.c_void_p)]
+
+
 class SemNsDesc(C.Structure):
     _fields_ = [("c_mass", C.c_double), ("c_stiff", C.c_double), ("c_gradx", C.c_double), ("c_grady", C.c_double),
                 ("cu", C.c_void_p), ("cv", C.c_void_p), ("juu", C.c_void_p), ("juv", C.c_void_p), ("jvu", C.c_void_p),
@@ -87,6 +93,10 @@ _SIGS = {
     "sem_line_block_sizes": (C.c_int, [C.c_void_p, C.c_int, _i64p]),
     "sem_velocity_blocks": (C.c_int, [C.c_void_p, C.POINTER(SemVelocityDesc)] + [C.c_void_p] * 7),
     "sem_ns_apply": (C.c_int, [C.c_void_p, C.POINTER(SemNsDesc)] + [C.c_void_p] * 7),
+    "sem_nested_solve": (C.c_int, [C.POINTER(SemNestedDesc), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_int64, C.c_void_p]),
+    "sem_interface_rhs": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                    C.c_int64, C.c_void_p, C.c_void_p]),
     "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,
                                  C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p]),
 }

@@ -21,7 +21,8 @@ namespace sem {
 
 constexpr int kGemvWaves = 4;
 constexpr int kGemvRowsPerWave = 4;
-constexpr int kGemvRows = kGemvWaves * kGemvRowsPerWave;  // matrix rows per workgroup
+constexpr int kGemvRows = kGemvWaves * kGemvRowsPerWave;  // matrix rows per workgroup (wide form)
+constexpr int kGemvUnroll = 8;                            // loads in flight per wave (narrow form)
 
 struct GemvArgs {
   const double* M;
@@ -39,15 +40,21 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(64 * kGemvWaves) void block_gemv_kernel(const GemvArgs a) {
-  extern __shared__ double xs[];  // S * m gathered operand values (0 for a skipped operand)
-  const int b = blockIdx.y, m = a.m, S = a.S, K = S * m;
-  for (int s = 0; s < S; ++s) {
+__device__ __forceinline__ void stage_operands(const GemvArgs& a, double* xs, int b) {
+  const int m = a.m;
+  for (int s = 0; s < a.S; ++s) {
     const int64_t r = a.xrow[static_cast<int64_t>(s) * a.nb + b];
     const double* src = r >= 0 ? a.src[s] + r * a.ld_src[s] : nullptr;
     for (int j = threadIdx.x; j < m; j += blockDim.x) xs[s * m + j] = src ? src[j] : 0.0;
   }
   __syncthreads();
+}
+
+// Wide form (many blocks per level): 16 rows per workgroup, four rows in flight per wave.
+__global__ __launch_bounds__(64 * kGemvWaves) void block_gemv_kernel(const GemvArgs a) {
+  extern __shared__ double xs[];  // S * m gathered operand values (0 for a skipped operand)
+  const int b = blockIdx.y, m = a.m, K = a.S * m;
+  stage_operands(a, xs, b);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r0 = blockIdx.x * kGemvRows + wave * kGemvRowsPerWave;
   if (r0 >= m) return;
@@ -69,6 +76,36 @@ __global__ __launch_bounds__(64 * kGemvWaves) void block_gemv_kernel(const GemvA
   for (int i = 0; i < kGemvRowsPerWave; ++i) {
     const double v = wave_sum(acc[i]);
     if (lane == 0 && r0 + i < m) yb[r0 + i] = a.accumulate ? yb[r0 + i] + v : v;
+  }
+}
+
+// Narrow form (the last cyclic-reduction levels, one to a few blocks): one row per wave, four rows
+// per workgroup, so a level's few blocks still spread over ~4x more CUs, and eight independent
+// loads in flight per wave along the row.
+__global__ __launch_bounds__(64 * kGemvWaves) void block_gemv_narrow_kernel(const GemvArgs a) {
+  extern __shared__ double xs[];
+  const int b = blockIdx.y, m = a.m, K = a.S * m;
+  stage_operands(a, xs, b);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.x * kGemvWaves + wave;
+  if (r >= m) return;
+  const double* row = a.M + (static_cast<int64_t>(b) * m + r) * K;
+  double acc[kGemvUnroll];
+#pragma unroll
+  for (int u = 0; u < kGemvUnroll; ++u) acc[u] = 0.0;
+  int j = lane;
+  for (; j + 64 * (kGemvUnroll - 1) < K; j += 64 * kGemvUnroll) {
+#pragma unroll
+    for (int u = 0; u < kGemvUnroll; ++u) acc[u] = fma(row[j + 64 * u], xs[j + 64 * u], acc[u]);
+  }
+  for (int u = 0; j < K; j += 64, ++u) acc[u] = fma(row[j], xs[j], acc[u]);
+  double v = 0.0;
+#pragma unroll
+  for (int u = 0; u < kGemvUnroll; ++u) v += acc[u];
+  v = wave_sum(v);
+  if (lane == 0) {
+    double* yb = a.y + a.yrow[b] * a.ld_y;
+    yb[r] = a.accumulate ? yb[r] + v : v;
   }
 }
 
@@ -99,8 +136,13 @@ int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* s
   a.S = S;
   a.accumulate = accumulate;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((m + sem::kGemvRows - 1) / sem::kGemvRows, nb);
-  hipLaunchKernelGGL(sem::block_gemv_kernel, grid, dim3(64 * sem::kGemvWaves), lds, s, a);
+  const int wide_blocks = (m + sem::kGemvRows - 1) / sem::kGemvRows;
+  if (static_cast<int64_t>(wide_blocks) * nb >= 1024) {
+    hipLaunchKernelGGL(sem::block_gemv_kernel, dim3(wide_blocks, nb), dim3(64 * sem::kGemvWaves), lds, s, a);
+  } else {  // a level too small to fill the chip with 16-row workgroups
+    hipLaunchKernelGGL(sem::block_gemv_narrow_kernel, dim3((m + sem::kGemvWaves - 1) / sem::kGemvWaves, nb),
+                       dim3(64 * sem::kGemvWaves), lds, s, a);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("block_gemv launch: ") + hipGetErrorString(e));
   return SEM_OK;

@@ -1,0 +1,286 @@
+// Nested static condensation of an element column's interior, solved in three fused launches
+// (sem_amd/solvers/velocity_solve.py: VelocityJacobianSolver._nested_solve), in place of the
+// reference's SuperLU triangular solves of the velocity Jacobian (NavierStokes_Solver.py:189-203)
+// and of the ~15 torch gathers, batched GEMMs and scatters that computed the same thing.
+//
+// Inside element column e the interior unknowns (lines l = 1..P-1, components c, nodes gy; column
+// offset o = (l-1) m + c N_y + gy, m = nc N_y) split into element interiors (element n: nodes
+// gy = nP + j, j = 1..P-1; ni = nc (P-1)^2 unknowns, offsets pi[n][.]) and the horizontal edges
+// (gy = kP, k = 0..N_ey; ne1 = nc (P-1) unknowns per edge, offsets pe[k ne1 + .]).  With the factor
+//     Xi  = A_ii^-1 per element        (nex, ney, ni, ni)
+//     Aei = A_ei per element           (nex, ney, 2 ne1, ni)   edges n, n+1 <- interior n
+//     Yie = Xi A_ie per element        (nex, ney, ni, 2 ne1)
+//     Se  = edge Schur complement^-1   (nex, n_e, n_e),  n_e = (N_ey+1) ne1
+// the solve of A_II y = r is
+//   K1 (one workgroup per element):  T = Xi r_i,  C = Aei T
+//   K2 (workgroups over edge rows):  r_e[k] -= C[n=k][0:ne1] + C[n=k-1][ne1:],  y_e = Se r_e
+//   K3 (one workgroup per element):  y_i = T - Yie [y_e[n]; y_e[n+1]]
+// Every matrix is stored column-major (the transpose of the factor's blocks) and read once: a
+// thread owns an output row and walks the columns, so each column is one coalesced vector load
+// across the lanes and no cross-lane reduction is needed (rows here are short: 2 (P-1)^2 = 98
+// at P=8; a row-per-wave GEMV spent most of its time in shuffle reductions).  Threads beyond the
+// row count split the columns; the partial sums meet in LDS in a fixed order, so results are
+// bitwise reproducible.  Operands sit in LDS.  The right-hand side is read straight from the
+// solve's line array (column e's interior lines are contiguous there), optionally corrected by the
+// interface coupling r = b - A_IB x_B (the back substitution, A_IB diagonal per line), and the
+// result is written straight into a line array: no gather, copy or scatter launches.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "sem_internal.h"
+
+namespace sem {
+
+constexpr int kCondThreads = 256;
+constexpr int kEdgeRows = 64;                         // edge-kernel rows per workgroup (4 column splits)
+
+struct CondArgs {
+  const double *Xi, *Aei, *Yie, *Se;
+  const int64_t *pi, *pe;
+  double *T, *C, *Ye;
+  const double* R;     // column e interior at R + e ld_r (offset o)
+  int64_t ld_r;
+  const double* aIB;   // nullable: r -= aIB[e][l-1][0][r'] xB[e][r'] + aIB[e][l-1][1][r'] xB[e+1][r']
+  const double* xB;    // (nex+1, m)
+  double* Y;           // column e interior result at Y + e ld_y (offset o)
+  int64_t ld_y;
+  int P, nex, ney, m, ni, ne1, n_e;
+};
+
+// right-hand side at column offset o of column e (with the optional interface correction)
+__device__ __forceinline__ double rhs(const CondArgs& a, int e, int64_t o) {
+  double v = a.R[e * a.ld_r + o];
+  if (a.aIB) {
+    const int64_t l1 = o / a.m, r = o - l1 * a.m;
+    const double* ab = a.aIB + ((static_cast<int64_t>(e) * (a.P - 1) + l1) * 2) * a.m + r;
+    v -= ab[0] * a.xB[static_cast<int64_t>(e) * a.m + r] + ab[a.m] * a.xB[static_cast<int64_t>(e + 1) * a.m + r];
+  }
+  return v;
+}
+
+// y = M x for a column-major (rows x cols) block M (column j at M + j rows), x in LDS, computed by
+// the whole workgroup.  Up to 128 rows: thread t owns row t % RP (RP = rows rounded up to a
+// wavefront multiple) over the column split t / RP, and the splits' partial sums meet in `part`
+// (LDS) in split order.  More rows: each thread owns rows t, t + 256, ... over all columns.
+// out(row, value) stores.
+template <typename Out>
+__device__ __forceinline__ void colmajor_gemv(const double* __restrict__ M, int rows, int cols, const double* x,
+                                              double* part, Out out) {
+  auto dot = [&](int i, int cb, int ce) {
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+    int j = cb;
+    for (; j + 3 < ce; j += 4) {
+      acc0 = fma(M[static_cast<int64_t>(j) * rows + i], x[j], acc0);
+      acc1 = fma(M[static_cast<int64_t>(j + 1) * rows + i], x[j + 1], acc1);
+      acc2 = fma(M[static_cast<int64_t>(j + 2) * rows + i], x[j + 2], acc2);
+      acc3 = fma(M[static_cast<int64_t>(j + 3) * rows + i], x[j + 3], acc3);
+    }
+    for (; j < ce; ++j) acc0 = fma(M[static_cast<int64_t>(j) * rows + i], x[j], acc0);
+    return (acc0 + acc1) + (acc2 + acc3);
+  };
+  const int t = threadIdx.x;
+  if (rows > kCondThreads / 2) {  // one column range; every thread owns rows t, t + 256, ...
+    for (int i = t; i < rows; i += kCondThreads) out(i, dot(i, 0, cols));
+    return;
+  }
+  // rows <= 128: RP = rows rounded up to a wavefront multiple, 256 / RP column splits (2 or 4)
+  const int RP = (rows + 63) / 64 * 64, splits = kCondThreads / RP;
+  const int i = t % RP, sp = t / RP;
+  double v = 0.0;
+  if (i < rows)
+    v = dot(i, static_cast<int>(static_cast<int64_t>(cols) * sp / splits),
+            static_cast<int>(static_cast<int64_t>(cols) * (sp + 1) / splits));
+  part[sp * RP + i] = v;  // every thread reaches both barriers
+  __syncthreads();
+  if (sp == 0 && i < rows) {
+    double sum = v;
+    for (int q = 1; q < splits; ++q) sum += part[q * RP + i];
+    out(i, sum);
+  }
+  __syncthreads();
+}
+
+// LDS doubles colmajor_gemv needs for its split partial sums
+__host__ __device__ constexpr int part_size() { return kCondThreads; }
+
+// K1: T = Xi r_i, C = Aei T for element (e, n) = (blockIdx.x / ney, blockIdx.x % ney).
+__global__ __launch_bounds__(kCondThreads) void cond_fwd_kernel(const CondArgs a) {
+  extern __shared__ double lds[];
+  double* part = lds;                     // part_size()
+  double* x = lds + part_size();          // ni: r_i
+  double* t = x + a.ni;                   // ni: T
+  const int el = blockIdx.x, e = el / a.ney, n = el - e * a.ney;
+  const int64_t* pin = a.pi + static_cast<int64_t>(n) * a.ni;
+  for (int i = threadIdx.x; i < a.ni; i += blockDim.x) x[i] = rhs(a, e, pin[i]);
+  __syncthreads();
+  const double* Xi = a.Xi + static_cast<int64_t>(el) * a.ni * a.ni;
+  double* T = a.T + static_cast<int64_t>(el) * a.ni;
+  colmajor_gemv(Xi, a.ni, a.ni, x, part, [&](int r, double v) {
+    T[r] = v;
+    t[r] = v;
+  });
+  __syncthreads();
+  const double* Aei = a.Aei + static_cast<int64_t>(el) * 2 * a.ne1 * a.ni;
+  double* C = a.C + static_cast<int64_t>(el) * 2 * a.ne1;
+  colmajor_gemv(Aei, 2 * a.ne1, a.ni, t, part, [&](int r, double v) { C[r] = v; });
+}
+
+// K2: y_e = Se (r_e - edge contributions of C); grid (ceil(n_e / 64), nex).  Every workgroup
+// forms the column's whole reduced edge right-hand side in LDS (n_e values) and computes 64 rows
+// of the column-major Se with four column splits.
+__global__ __launch_bounds__(kCondThreads) void cond_edge_kernel(const CondArgs a) {
+  extern __shared__ double lds[];
+  double* part = lds;
+  double* re = lds + part_size();
+  const int e = blockIdx.y, ne1 = a.ne1;
+  const double* C = a.C + static_cast<int64_t>(e) * a.ney * 2 * ne1;
+  for (int i = threadIdx.x; i < a.n_e; i += blockDim.x) {
+    const int k = i / ne1, q = i - k * ne1;
+    double v = rhs(a, e, a.pe[i]);
+    if (k < a.ney) v -= C[static_cast<int64_t>(k) * 2 * ne1 + q];
+    if (k > 0) v -= C[static_cast<int64_t>(k - 1) * 2 * ne1 + ne1 + q];
+    re[i] = v;
+  }
+  __syncthreads();
+  const int r0 = blockIdx.x * kEdgeRows;
+  const int rows = min(kEdgeRows, a.n_e - r0);
+  constexpr int splits = kCondThreads / kEdgeRows;
+  const int i = threadIdx.x % kEdgeRows, sp = threadIdx.x / kEdgeRows;
+  const int cb = static_cast<int>(static_cast<int64_t>(a.n_e) * sp / splits);
+  const int ce = static_cast<int>(static_cast<int64_t>(a.n_e) * (sp + 1) / splits);
+  const double* Se = a.Se + static_cast<int64_t>(e) * a.n_e * a.n_e + r0;
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+  if (i < rows) {
+    int j = cb;
+    for (; j + 3 < ce; j += 4) {
+      acc0 = fma(Se[static_cast<int64_t>(j) * a.n_e + i], re[j], acc0);
+      acc1 = fma(Se[static_cast<int64_t>(j + 1) * a.n_e + i], re[j + 1], acc1);
+      acc2 = fma(Se[static_cast<int64_t>(j + 2) * a.n_e + i], re[j + 2], acc2);
+      acc3 = fma(Se[static_cast<int64_t>(j + 3) * a.n_e + i], re[j + 3], acc3);
+    }
+    for (; j < ce; ++j) acc0 = fma(Se[static_cast<int64_t>(j) * a.n_e + i], re[j], acc0);
+  }
+  part[sp * kEdgeRows + i] = (acc0 + acc1) + (acc2 + acc3);
+  __syncthreads();
+  if (sp == 0 && i < rows) {
+    double v = part[i];
+    for (int q = 1; q < splits; ++q) v += part[q * kEdgeRows + i];
+    a.Ye[static_cast<int64_t>(e) * a.n_e + r0 + i] = v;
+    a.Y[e * a.ld_y + a.pe[r0 + i]] = v;
+  }
+}
+
+// K3: y_i = T - Yie [y_e[n]; y_e[n+1]] for element (e, n), written to the element's interior nodes.
+__global__ __launch_bounds__(kCondThreads) void cond_back_kernel(const CondArgs a) {
+  extern __shared__ double lds[];
+  double* part = lds;
+  double* ye = lds + part_size();  // 2 ne1: edges n, n+1 (contiguous in Ye)
+  const int el = blockIdx.x, e = el / a.ney, n = el - e * a.ney;
+  const double* src = a.Ye + static_cast<int64_t>(e) * a.n_e + static_cast<int64_t>(n) * a.ne1;
+  for (int i = threadIdx.x; i < 2 * a.ne1; i += blockDim.x) ye[i] = src[i];
+  __syncthreads();
+  const double* Yie = a.Yie + static_cast<int64_t>(el) * a.ni * 2 * a.ne1;
+  const double* T = a.T + static_cast<int64_t>(el) * a.ni;
+  const int64_t* pin = a.pi + static_cast<int64_t>(n) * a.ni;
+  double* Y = a.Y + e * a.ld_y;
+  colmajor_gemv(Yie, a.ni, 2 * a.ne1, ye, part, [&](int r, double v) { Y[pin[r]] = T[r] - v; });
+}
+
+// g[L][r] = B[L P][r] - sum_l aBI[L][0][l][r] yI[L][l][r] - sum_l aBI[L-1][1][l][r] yI[L-1][l][r]
+struct IfaceArgs {
+  const double *B, *aBI, *yI;
+  double* g;
+  int64_t ld_b, ld_yI;
+  int P, nex, m;
+};
+
+__global__ __launch_bounds__(256) void cond_iface_rhs_kernel(const IfaceArgs a) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<int64_t>(a.nex + 1) * a.m) return;
+  const int L = static_cast<int>(t / a.m), r = static_cast<int>(t - static_cast<int64_t>(L) * a.m);
+  double v = a.B[static_cast<int64_t>(L) * a.P * a.ld_b + r];
+  if (L < a.nex) {
+    double s = 0.0;
+    for (int l = 0; l < a.P - 1; ++l)
+      s = fma(a.aBI[((static_cast<int64_t>(L) * 2 + 0) * (a.P - 1) + l) * a.m + r],
+              a.yI[static_cast<int64_t>(L) * a.ld_yI + static_cast<int64_t>(l) * a.m + r], s);
+    v -= s;
+  }
+  if (L > 0) {
+    double s = 0.0;
+    for (int l = 0; l < a.P - 1; ++l)
+      s = fma(a.aBI[((static_cast<int64_t>(L - 1) * 2 + 1) * (a.P - 1) + l) * a.m + r],
+              a.yI[static_cast<int64_t>(L - 1) * a.ld_yI + static_cast<int64_t>(l) * a.m + r], s);
+    v -= s;
+  }
+  a.g[t] = v;
+}
+
+static int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return SEM_OK;
+  return set_error(SEM_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace sem
+
+extern "C" {
+
+int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB, const double* xB,
+                     double* Y, int64_t ld_y, void* stream) {
+  if (!d || !R || !Y) return sem::set_error(SEM_EINVAL, "nested_solve: null argument");
+  if (d->P < 2 || d->nex < 1 || d->ney < 1 || (d->nc != 1 && d->nc != 2) || d->NY != d->ney * d->P + 1)
+    return sem::set_error(SEM_EINVAL, "nested_solve: bad sizes");
+  if (!d->Xi || !d->Aei || !d->Yie || !d->Se || !d->pi || !d->pe || !d->T || !d->C || !d->Ye)
+    return sem::set_error(SEM_EINVAL, "nested_solve: null factor or work array");
+  if ((aIB == nullptr) != (xB == nullptr)) return sem::set_error(SEM_EINVAL, "nested_solve: aIB and xB go together");
+  sem::CondArgs a{};
+  a.Xi = d->Xi;
+  a.Aei = d->Aei;
+  a.Yie = d->Yie;
+  a.Se = d->Se;
+  a.pi = d->pi;
+  a.pe = d->pe;
+  a.T = d->T;
+  a.C = d->C;
+  a.Ye = d->Ye;
+  a.R = R;
+  a.ld_r = ld_r;
+  a.aIB = aIB;
+  a.xB = xB;
+  a.Y = Y;
+  a.ld_y = ld_y;
+  a.P = d->P;
+  a.nex = d->nex;
+  a.ney = d->ney;
+  a.m = d->nc * d->NY;
+  a.ne1 = d->nc * (d->P - 1);
+  a.ni = a.ne1 * (d->P - 1);
+  a.n_e = (d->ney + 1) * a.ne1;
+  if (static_cast<size_t>(a.n_e + sem::part_size()) * sizeof(double) > 64 * 1024)
+    return sem::set_error(SEM_EUNSUPPORTED, "nested_solve: too many edge unknowns per column");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 blk(sem::kCondThreads);
+  const unsigned elems = static_cast<unsigned>(d->nex) * d->ney;
+  const size_t part = sem::part_size() * sizeof(double);
+  hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(elems), blk, part + 2 * a.ni * sizeof(double), s, a);
+  if (int st = sem::launch_check("nested_solve fwd")) return st;
+  hipLaunchKernelGGL(sem::cond_edge_kernel, dim3((a.n_e + sem::kEdgeRows - 1) / sem::kEdgeRows, d->nex), blk,
+                     part + a.n_e * sizeof(double), s, a);
+  if (int st = sem::launch_check("nested_solve edge")) return st;
+  hipLaunchKernelGGL(sem::cond_back_kernel, dim3(elems), blk, part + 2 * a.ne1 * sizeof(double), s, a);
+  return sem::launch_check("nested_solve back");
+}
+
+int sem_interface_rhs(int P, int nex, int m, const double* B, int64_t ld_b, const double* aBI, const double* yI,
+                      int64_t ld_yI, double* g, void* stream) {
+  if (P < 2 || nex < 1 || m < 1 || !B || !aBI || !yI || !g) return sem::set_error(SEM_EINVAL, "interface_rhs");
+  sem::IfaceArgs a{B, aBI, yI, g, ld_b, ld_yI, P, nex, m};
+  const int64_t n = static_cast<int64_t>(nex + 1) * m;
+  hipLaunchKernelGGL(sem::cond_iface_rhs_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return sem::launch_check("interface_rhs");
+}
+
+}  // extern "C"

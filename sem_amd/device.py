@@ -238,7 +238,9 @@ def get_mesh(P, nex, ney, dx, dy, ex_begin=0, ex_end=None, device=None):
 def no_gc():
     """Keep Python's cyclic GC from running inside a stream capture: a collection there can run the
     finaliser of an unrelated object (an old hipGraph, a mesh handle) whose device calls are illegal
-    while the stream captures, which aborts the process.  torch.cuda.graph collects on entry."""
+    while the stream captures, which aborts the process.  torch.cuda.graph collects on entry (an
+    explicit gc.collect runs while the GC is disabled); enter no_gc() first so that the capture has
+    ended before collection is enabled again: `with no_gc(), torch.cuda.graph(g): ...`."""
     enabled = gc.isenabled()
     gc.disable()
     try:

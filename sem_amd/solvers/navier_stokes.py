@@ -359,7 +359,7 @@ class _SchurComplement:
                 self._body(self._x)   # warm-up outside the capture (library workspaces)
             cur.wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g), no_gc():
+            with no_gc(), torch.cuda.graph(g):
                 self._out = self._body(self._x)
             self._graph = g
         except RuntimeError:

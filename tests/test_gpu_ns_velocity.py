@@ -110,3 +110,58 @@ def test_scalar_blocks_and_solve_match_oracle_cd_jacobian(gpu, P, nex, ney, Pe):
     assert np.abs(got - want).max() <= 1e-9 * np.abs(want).max()
     with pytest.raises(ValueError):
         cd._mesh.velocity_blocks(blocks, c_stiff=1.0, juv=cd._dev(b), ncomp=1)
+
+
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 2, 100.0), (8, 4, 4, 1000.0), (5, 3, 6, 250.0), (2, 7, 2, 300.0)])
+def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
+    """sem_nested_solve + sem_interface_rhs (ns_condense.hip) against the torch formulation of the
+    same condensation, for the velocity pair and the one-component CD Jacobian."""
+    ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    ns = _device_solver(P, nex, ney, Re, u, v)
+    vs = ns._velocity_solver()
+    B = torch.as_tensor(np.random.default_rng(4).uniform(-1, 1, (vs.NX, vs.m)), device=ns._mesh.device)
+    x_hip = vs._solve_lines(B.clone())
+    vs.hip_nested = False
+    x_torch = vs._solve_lines(B.clone())
+    vs.hip_nested = True
+    assert (x_hip - x_torch).abs().max().item() <= 1e-12 * x_torch.abs().max().item()
+    from sem_amd.solvers import ConvectionDiffusionSolver
+    cd = ConvectionDiffusionSolver(1.0, 1.0, Re, P, nex, ney, T_W=0.5, T_E=-0.5)
+    cd._get_residuals(np.zeros(cd.N), u, v)
+    vc = cd._jacobian_solver()
+    b = torch.as_tensor(np.random.default_rng(5).uniform(-1, 1, (vc.NX, vc.m)), device=ns._mesh.device)
+    y_hip = vc._solve_lines(b.clone())
+    vc.hip_nested = False
+    y_torch = vc._solve_lines(b.clone())
+    assert (y_hip - y_torch).abs().max().item() <= 1e-12 * y_torch.abs().max().item()
+
+
+@pytest.mark.parametrize("nb,m,S", [(1, 770, 3), (2, 385, 2), (40, 200, 3), (24, 770, 2), (3, 17, 1)])
+def test_block_gemv_wide_and_narrow(gpu, nb, m, S):
+    """sem_block_gemv (both launch forms: wide 16-row workgroups for big levels, narrow one-row-per-wave
+    for the last cyclic-reduction levels) against torch, with absent operands and accumulation."""
+    import ctypes as C
+    from sem_amd import _lib
+    lib = _lib.load()
+    dev = torch.device("cuda")
+    r = np.random.default_rng(nb * 100 + m + S)
+    M = torch.as_tensor(r.uniform(-1, 1, (nb, m, S * m)), device=dev)
+    nrow = nb + 3
+    srcs = [torch.as_tensor(r.uniform(-1, 1, (nrow, m)), device=dev) for _ in range(S)]
+    xrow = torch.as_tensor(r.integers(-1, nrow, (S, nb)), device=dev)
+    y = torch.as_tensor(r.uniform(-1, 1, (nb + 5, m)), device=dev)
+    yrow = torch.as_tensor(r.permutation(nb + 5)[:nb], device=dev)
+    want = y.clone()
+    for b in range(nb):
+        acc = torch.zeros(m, dtype=torch.float64, device=dev)
+        for s in range(S):
+            xr = int(xrow[s, b])
+            if xr >= 0:
+                acc += M[b, :, s * m:(s + 1) * m] @ srcs[s][xr]
+        want[int(yrow[b])] += acc
+    P_ = C.c_void_p
+    src = (P_ * S)(*(P_(t.data_ptr()) for t in srcs))
+    ld = (C.c_int64 * S)(*(t.stride(0) for t in srcs))
+    _lib.check(lib.sem_block_gemv(nb, m, S, P_(M.data_ptr()), src, ld, P_(xrow.data_ptr()), P_(y.data_ptr()),
+                                  y.stride(0), P_(yrow.data_ptr()), 1, P_(torch.cuda.current_stream().cuda_stream)))
+    assert (y - want).abs().max().item() <= 1e-12 * want.abs().max().item()
