@@ -3,5 +3,7 @@ Solvers/ConvectionDiffusion_Solver.py and Solvers/NavierStokes_Solver.py on the 
 from .convection_diffusion import ConvectionDiffusionSolver  # noqa: F401
 from .navier_stokes import NavierStokesSolver  # noqa: F401
 from .boussinesq import BoussinesqCoupler, ParallelBoussinesqCoupler  # noqa: F401
+from .components import ConvectionDiffusion_Component, NavierStokes_Component  # noqa: F401
 
-__all__ = ["ConvectionDiffusionSolver", "NavierStokesSolver", "BoussinesqCoupler", "ParallelBoussinesqCoupler"]
+__all__ = ["ConvectionDiffusionSolver", "NavierStokesSolver", "BoussinesqCoupler", "ParallelBoussinesqCoupler",
+           "ConvectionDiffusion_Component", "NavierStokes_Component"]

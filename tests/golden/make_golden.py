@@ -20,7 +20,7 @@ dependencies of the reference (`requirements.txt:1-4`):
   (`ConvectionDiffusion_Solver.py:146-148`, `NavierStokes_Solver.py:222-224`).
   The shim forwards `tol` as `rtol` (same meaning in SciPy <1.12).
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--only cfg5|components]
 """
 import os
 import sys
@@ -282,6 +282,100 @@ def gen_boussinesq(CDS, NSS):
     np.savez_compressed(os.path.join(OUT, "bous.npz"), **d)
 
 
+def gen_components(CDS, NSS):
+    """The two OpenMDAO components (OpenMDAO/ConvectionDiffusion_Component.py,
+    OpenMDAO/NavierStokes_Component.py) driven method by method, in OpenMDAO's call order, around
+    the reference's own solver classes, on mismatched meshes (CD 4x4 P=4, NS 3x3 P=6) so that
+    change_inputs interpolates.  OpenMDAO is absent offline: `openmdao.api.ImplicitComponent` is
+    the minimal stand-in sem_amd.solvers.components.ImplicitComponent (options.declare,
+    add_input/add_output, initialize at construction) -- all the two components touch."""
+    sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..")))
+    from sem_amd.solvers.components import ImplicitComponent
+    pkg, api = types.ModuleType("openmdao"), types.ModuleType("openmdao.api")
+    api.ImplicitComponent = ImplicitComponent
+    pkg.api = api
+    sys.modules["openmdao"], sys.modules["openmdao.api"] = pkg, api
+    from OpenMDAO.ConvectionDiffusion_Component import ConvectionDiffusion_Component
+    from OpenMDAO.NavierStokes_Component import NavierStokes_Component
+    Re, Ra, Pr = 100.0, 1e3, 0.71
+    cfg = (4, 4, 4, 6, 3, 3)
+    cd = CDS(L_x=1.0, L_y=1.0, Pe=Re * Pr, P=cfg[0], N_ex=cfg[1], N_ey=cfg[2], T_W=0.5, T_E=-0.5, mtol=1e-13)
+    ns = NSS(L_x=1.0, L_y=1.0, Re=Re, Gr=Ra / Pr, P=cfg[3], N_ex=cfg[4], N_ey=cfg[5], mtol=1e-13,
+             mtol_newton=1e-13, iprint=[])
+    d = {"cfg": np.array(cfg), "Re_Ra_Pr": np.array([Re, Ra, Pr])}
+    r = np.random.default_rng(47)
+    U = lambda n, a=0.5: r.uniform(-a, a, n)  # noqa: E731
+    # ---- convection-diffusion component
+    c = ConvectionDiffusion_Component(solver_CD=cd, solver_NS=ns)
+    c.setup()
+    inp = {"u_ns": U(ns.N), "v_ns": U(ns.N)}
+    out = {"T_cd": U(cd.N)}
+    d["cd_u_ns"], d["cd_v_ns"], d["cd_T"] = inp["u_ns"], inp["v_ns"], out["T_cd"]
+    d["cd_change_u"], d["cd_change_v"] = c.change_inputs(inp["u_ns"], inp["v_ns"])
+    res = {}
+    c.apply_nonlinear(inp, out, res)
+    d["cd_res"] = res["T_cd"]
+    c.linearize(inp, out, None)
+    din, dout, dres = {"u_ns": U(ns.N, 1), "v_ns": U(ns.N, 1)}, {"T_cd": U(cd.N, 1)}, {}
+    d["cd_d_u_ns"], d["cd_d_v_ns"], d["cd_dT"] = din["u_ns"], din["v_ns"], dout["T_cd"]
+    c.apply_linear(inp, out, din, dout, dres, "fwd")
+    d["cd_dres"] = dres["T_cd"]
+    c.apply_linear(inp, out, din, {}, dres, "fwd")
+    d["cd_dres_no_dT"] = dres["T_cd"]
+    rhs = {"T_cd": U(cd.N, 1)}
+    dsol = {"T_cd": np.zeros(cd.N)}
+    c.solve_linear(dsol, rhs, "fwd")
+    d["cd_rhs"], d["cd_solve_linear"] = rhs["T_cd"], dsol["T_cd"]
+    out2 = {"T_cd": np.zeros(cd.N)}
+    smooth = {"u_ns": ns._get_vector(lambda x, y: 0.2 * (y - 0.5)), "v_ns": ns._get_vector(lambda x, y: 0.2 * (0.5 - x))}
+    c.solve_nonlinear(smooth, out2)
+    d["cd_smooth_u_ns"], d["cd_smooth_v_ns"] = smooth["u_ns"], smooth["v_ns"]
+    d["cd_solve_nonlinear"], d["cd_iter_count"] = out2["T_cd"], np.array(c.iter_count_solve)
+    # ---- Navier-Stokes component
+    n = NavierStokes_Component(solver_NS=ns, solver_CD=cd)
+    n.setup()
+    inp = {"T_cd": U(cd.N)}
+    out = {k: U(ns.N, 0.2) for k in ("u_ns", "v_ns", "p_ns")}
+    d["ns_T_cd"] = inp["T_cd"]
+    for k in out:
+        d["ns_" + k] = out[k]
+    d["ns_change_T"] = n.change_inputs(inp["T_cd"])
+    res = {}
+    n.apply_nonlinear(inp, out, res)
+    for k in res:
+        d["ns_res_" + k] = res[k]
+    n.linearize(inp, out, None)
+    din, dout = {"T_cd": U(cd.N, 1)}, {k: U(ns.N, 1) for k in ("u_ns", "v_ns", "p_ns")}
+    d["ns_d_T_cd"] = din["T_cd"]
+    for k in dout:
+        d["ns_d_" + k] = dout[k]
+    dres = {}
+    n.apply_linear(inp, out, din, dout, dres, "fwd")
+    for k in dres:
+        d["ns_dres_" + k] = dres[k]
+    dres = {}
+    n.apply_linear(inp, out, din, {"u_ns": dout["u_ns"]}, dres, "fwd")
+    for k in dres:
+        d["ns_dres_partial_" + k] = dres[k]
+    # solve_linear: a consistent right-hand side (the Jacobian applied to a known update, T fixed)
+    # so the singular pressure mode of the equal-order discretisation does not enter
+    dres = {}
+    n.apply_linear(inp, out, {"T_cd": np.zeros(cd.N)}, dout, dres, "fwd")
+    for k in dres:
+        d["ns_rhs_" + k] = dres[k]
+    dsol = {k: np.zeros(ns.N) for k in ("u_ns", "v_ns", "p_ns")}
+    n.solve_linear(dsol, dres, "fwd")
+    for k in dsol:
+        d["ns_solve_linear_" + k] = dsol[k]
+    # solve_nonlinear: the buoyancy-driven flow of the CD component's temperature
+    out2 = {k: np.zeros(ns.N) for k in ("u_ns", "v_ns", "p_ns")}
+    n.solve_nonlinear({"T_cd": d["cd_solve_nonlinear"]}, out2)
+    for k in out2:
+        d["ns_solve_nonlinear_" + k] = out2[k]
+    d["ns_iter_count"] = np.array(n.iter_count_solve)
+    np.savez_compressed(os.path.join(OUT, "components.npz"), **d)
+
+
 def gen_cfg5(SEM):
     """Full-size cfg5 (128x128, P=12, N=2,362,369) operator checksums from the reference's own
     assembled matrices (SEM.global_{stiffness,mass,gradient}_matrices, SEM.py:170-223).  The
@@ -311,7 +405,13 @@ def main():
     install_adapters()
     if "--only" in sys.argv:   # regenerate one fixture: --only cfg5
         from Solvers import SEM
-        {"cfg5": gen_cfg5}[sys.argv[sys.argv.index("--only") + 1]](SEM)
+        from Solvers.ConvectionDiffusion_Solver import ConvectionDiffusionSolver
+        from Solvers.NavierStokes_Solver import NavierStokesSolver
+        which = sys.argv[sys.argv.index("--only") + 1]
+        if which == "components":
+            gen_components(ConvectionDiffusionSolver, NavierStokesSolver)
+        else:
+            {"cfg5": gen_cfg5}[which](SEM)
         return
     from Solvers import GLL, SEM
     from Solvers.ConvectionDiffusion_Solver import ConvectionDiffusionSolver
@@ -324,6 +424,7 @@ def main():
     gen_checksums(SEM)
     gen_cfg5(SEM)
     gen_boussinesq(ConvectionDiffusionSolver, NavierStokesSolver)
+    gen_components(ConvectionDiffusionSolver, NavierStokesSolver)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

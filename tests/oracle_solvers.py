@@ -7,11 +7,28 @@ import scipy.sparse.linalg as spla
 from oracle import sem_oracle as O
 
 
-class OracleCD:
+class _Nodal:
+    """_get_vector / _get_interpol (ConvectionDiffusion_Solver.py:172-190; the NS solver's are the
+    same): what the OpenMDAO components' change_inputs calls."""
+
+    def _nodal(self, L_x, L_y, P, N_ex, N_ey):
+        self._P, self._N_ex, self._N_ey = P, N_ex, N_ey
+        self.points_e = O.element_nodes(P, N_ex, N_ey, L_x / N_ex, L_y / N_ey)
+
+    def _get_vector(self, f_func):
+        return f_func(self.points[0], self.points[1])
+
+    def _get_interpol(self, f, points_plot):
+        f_e = O.scatter(np.asarray(f), self._P, self._N_ex, self._N_ey)
+        return O.eval_interpolation(f_e, self.points_e, points_plot)
+
+
+class OracleCD(_Nodal):
     def __init__(self, L_x, L_y, Pe, P, N_ex, N_ey, T_W=None, T_E=None, mtol=1e-7):
         self.o = O.CDOracle(L_x, L_y, Pe, P, N_ex, N_ey, T_W=T_W, T_E=T_E)
         self.N, self.points = self.o.N, self.o.points
-        self._P, self._N_ex, self._N_ey, self._mtol = P, N_ex, N_ey, mtol
+        self._nodal(L_x, L_y, P, N_ex, N_ey)
+        self._mtol = mtol
 
     def _get_residuals(self, T, u, v):
         return self.o.residuals(np.asarray(T), np.asarray(u), np.asarray(v))
@@ -34,11 +51,11 @@ class OracleCD:
         return T + self._get_update(-self._get_residuals(T, u, v))
 
 
-class OracleNS:
+class OracleNS(_Nodal):
     def __init__(self, L_x, L_y, Re, Gr, P, N_ex, N_ey, mtol=1e-7, mtol_newton=1e-5):
         self.o = O.NSOracle(L_x, L_y, Re, Gr, P, N_ex, N_ey)
         self.N, self.points = self.o.N, self.o.points
-        self._P, self._N_ex, self._N_ey = P, N_ex, N_ey
+        self._nodal(L_x, L_y, P, N_ex, N_ey)
         self._mtol, self._mtol_newton = mtol, mtol_newton
 
     def _get_residuals(self, u, v, p, T):
@@ -54,5 +71,7 @@ class OracleNS:
         return self.o.update(np.asarray(ru), np.asarray(rv), np.asarray(rc), mtol=self._mtol, dp0=dp0)[:3]
 
     def _get_solution(self, T, u0=None, v0=None, p0=None):
-        return self.o.solution(np.asarray(T), mtol=self._mtol, mtol_newton=self._mtol_newton, u0=u0, v0=v0,
-                               p0=p0)[:3]
+        u, v, p, hist = self.o.solution(np.asarray(T), mtol=self._mtol, mtol_newton=self._mtol_newton, u0=u0,
+                                        v0=v0, p0=p0)
+        self._k = len(hist) - 1   # Newton updates taken (NavierStokes_Solver.py:241-270)
+        return u, v, p
