@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 4
+#define SEM_ABI_VERSION 5
 
 enum sem_status {
   SEM_OK = 0,
@@ -311,7 +311,11 @@ int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* s
  * rows when pin_first (the residual's statement order, :116-120) and after them otherwise (:159-160).
  * u, v, p, T, cu, cv, j**, dval_* are nullable (NULL = zeros; cu, cv: ones); a NULL output is not
  * computed.  u, v, ru, rv hold node (gx, gy) at gx * uv_pitch + gy (0 = NY: plain vectors; 2 NY: the
- * line-interleaved [u | v] layout of the velocity solve).  Whole-mesh handles only. */
+ * line-interleaved [u | v] layout of the velocity solve).  `pin` is a global node index.  On an
+ * element-column strip handle (ABI 5) every vector holds the strip's lines; the two interface lines
+ * get partial sums over the strip's elements, and pointwise terms, Dirichlet rows and the pinned row of
+ * the right interface line are written by its right-hand owner only (0 here), so summing the interface
+ * lines across strips (sem_interface_pack/unpack + an all-reduce) gives the whole-mesh rows. */
 typedef struct sem_ns_desc {
   double c_mass, c_stiff, c_gradx, c_grady;
   const double* cu;

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE = range(6)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8

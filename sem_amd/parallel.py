@@ -72,6 +72,19 @@ class InterfaceExchange:
             return y
         return self.finish(y, self.start(y))
 
+    def many(self, ys):
+        """Assemble the interface lines of several vectors with ONE collective (the three Navier-Stokes
+        residuals): each is packed into its own slice of one buffer."""
+        n = self.buf.numel()
+        if getattr(self, "_mbuf", None) is None or self._mbuf.numel() < len(ys) * n:
+            self._mbuf = torch.empty(len(ys) * n, dtype=torch.float64, device=self.mesh.device)
+        for i, y in enumerate(ys):
+            self.mesh.interface_pack(y, self.part.bounds, self._mbuf[i * n:(i + 1) * n])
+        self.dist.all_reduce(self._mbuf[:len(ys) * n], group=self.group)
+        for i, y in enumerate(ys):
+            self.mesh.interface_unpack(self._mbuf[i * n:(i + 1) * n], self.part.bounds, y)
+        return ys
+
 
 class NeighborExchange:
     """Interface assembly by point-to-point exchange with the two neighbouring strips."""
@@ -119,6 +132,12 @@ class NeighborExchange:
         if self.part.world == 1:
             return y
         return self.finish(y, self.start(y))
+
+    def many(self, ys):
+        """Several vectors, one after the other (the receive buffers are shared)."""
+        for y in ys:
+            self(y)
+        return ys
 
 
 class StripApply:
@@ -207,6 +226,39 @@ class Partition:
         """This rank's slice of a global vector (x-major numbering)."""
         m = self.mesh
         return v[m.dof_begin:m.dof_begin + m.n_local]
+
+    def assemble(self, *ys):
+        """Sum the interface lines of strip partial results (one collective for all of them)."""
+        ex = self.step.exch
+        if ex is not None:
+            ex.many(list(ys))
+        return ys
+
+    def backend_device(self):
+        """Where collective buffers live: the GPU under RCCL ("nccl"), the host under gloo."""
+        if self.dist.get_backend(self.group) == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def norm(self, *ys):
+        """2-norm of the stacked global vectors from strips (a shared line counted once)."""
+        own = self.inner.own
+        s = sum((y.square() * own).sum() for y in ys).reshape(1).to(self.backend_device())
+        self.dist.all_reduce(s, group=self.group)
+        return float(torch.sqrt(s).item())
+
+    def amax(self, *ys):
+        m = torch.stack([y.abs().max() for y in ys]).max().reshape(1).to(self.backend_device())
+        self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX, group=self.group)
+        return float(m.item())
+
+    def broadcast(self, t, src=0):
+        """t (a host or device tensor, same shape on every rank) from rank src, on this rank's device."""
+        dev = t.device
+        b = t.to(self.backend_device())
+        self.dist.broadcast(b, src=src if self.group is None else self.dist.get_global_rank(self.group, src),
+                            group=self.group)
+        return b.to(dev)
 
     def gather(self, y):
         """Global vector (every rank) from the local strips; shared lines agree after an exchange."""

@@ -24,6 +24,7 @@ import torch
 from .. import SEM, _lib
 from ..device import get_mesh, no_gc
 from ..krylov import Recycle, gcro
+from ..operators import ConvectionTensor, SEMOperator
 from .convection_diffusion import DirichletRows
 from .velocity_solve import VelocityJacobianSolver
 
@@ -33,8 +34,16 @@ class NavierStokesSolver:
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
                  max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
-                 recycle_bytes: float = 0.0, velocity_sweep: str = "cr", schur_precond: str = "mass"):
-        """recycle_bytes: device memory for a recycled Krylov subspace of the Schur-complement solves
+                 recycle_bytes: float = 0.0, velocity_sweep: str = "cr", schur_precond: str = "mass",
+                 partition=None):
+        """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip per
+        rank: _get_residuals / _calc_jacobians / _get_dresiduals run the fused strip launch and sum the
+        interface lines of all three outputs with one collective; _get_update is the whole-mesh direct
+        velocity solve inside the Schur Krylov solve, run by rank 0 on a whole-mesh counterpart
+        (_central_solver) and broadcast -- its condensation couples every interface line, so it is not
+        split.  The reference methods take and return global NumPy vectors (local strips when given
+        device tensors).
+        recycle_bytes: device memory for a recycled Krylov subspace of the Schur-complement solves
         (sem_amd.krylov.Recycle, GCRO; 0 = off, the default): consecutive _get_update calls with one
         linearisation -- the Boussinesq coupler's block-Jacobi preconditioner -- then start from the
         earlier solves' spaces.  Measured (tools/recycle_probe.py, profiles/r02/bous): 5-8x fewer Schur
@@ -72,12 +81,20 @@ class NavierStokesSolver:
         self.points = SEM.global_nodes(P, N_ex, N_ey, L_x / N_ex, L_y / N_ey)
         self.points_e = SEM.element_nodes(P, N_ex, N_ey, dx, dy)
         self.N = (N_ex * P + 1) * (N_ey * P + 1)
-        self._mesh = m = get_mesh(P, N_ex, N_ey, dx, dy)
-
-        self._M = SEM.global_mass_matrix(P, N_ex, N_ey, dx, dy)
-        self._K = SEM.global_stiffness_matrix(P, N_ex, N_ey, dx, dy)
-        self._G_x, self._G_y = SEM.global_gradient_matrices(P, N_ex, N_ey, dx, dy)
-        self._C_x, self._C_y = SEM.global_convection_matrices(P, N_ex, N_ey, dx, dy)
+        self._args = dict(L_x=L_x, L_y=L_y, Re=Re, Gr=Gr, P=P, N_ex=N_ex, N_ey=N_ey, v_W=v_W, v_E=v_E, u_S=u_S,
+                          u_N=u_N, mtol=mtol, mtol_newton=mtol_newton, iprint=iprint, max_basis=max_basis,
+                          velocity_interior=velocity_interior, velocity_graph=velocity_graph,
+                          recycle_bytes=recycle_bytes, velocity_sweep=velocity_sweep, schur_precond=schur_precond)
+        self._part, self._twin, self._lin, self._lin_sys = partition, None, None, None
+        if partition is None:
+            self._mesh = m = get_mesh(P, N_ex, N_ey, dx, dy)
+            self._M = SEM.global_mass_matrix(P, N_ex, N_ey, dx, dy)
+            self._K = SEM.global_stiffness_matrix(P, N_ex, N_ey, dx, dy)
+            self._C_x, self._C_y = SEM.global_convection_matrices(P, N_ex, N_ey, dx, dy)
+        else:   # matrix-free operators on this rank's strip
+            self._mesh = m = partition.setup(P, N_ex, N_ey, dx, dy)
+            self._M, self._K = SEMOperator(m, cM=1.0), SEMOperator(m, cK=1.0)
+            self._C_x, self._C_y = ConvectionTensor(m, "x"), ConvectionTensor(m, "y")
         self._Sys = None
         self._Jac_u_u = self._Jac_u_v = self._Jac_v_u = self._Jac_v_v = None
         self._jac_kw, self._schur = None, None
@@ -99,13 +116,15 @@ class NavierStokesSolver:
         self._mask_dir_p = ~np.isnan(dpp)
         all_sides = _lib.SIDE_W | _lib.SIDE_E | _lib.SIDE_S | _lib.SIDE_N
         self._dir = DirichletRows(m, self._mask_bound, all_sides)
-        self._dval_u = m.to_device(np.where(self._mask_bound, du, 0.0))
-        self._dval_v = m.to_device(np.where(self._mask_bound, dv, 0.0))
+        self._dval_u = self._dev(np.where(self._mask_bound, du, 0.0))
+        self._dval_v = self._dev(np.where(self._mask_bound, dv, 0.0))
         pins = np.nonzero(self._mask_dir_p)[0]
         if len(pins) > 1:
             raise ValueError("one pinned pressure node is supported")
         self._pin = int(pins[0]) if len(pins) else -1
         self._pin_val = float(dpp[self._pin]) if len(pins) else 0.0
+        if partition is not None:   # the update runs on the whole-mesh counterpart
+            return
         self._Mdiag = m.to_device(self._M.diagonal())
         # PCD row weights: 1/M on the continuity rows, 0 on the replaced rows (and the reverse)
         repl = self._mask_bound.copy()
@@ -116,11 +135,41 @@ class NavierStokesSolver:
 
     # ------------------------------------------------------------------ helpers
     def _dev(self, a):
-        return None if a is None else self._mesh.to_device(a)
+        """Device vector of this solver's (local) DOFs; a global NumPy vector is sliced to the strip."""
+        if a is None:
+            return None
+        if self._part is not None and not isinstance(a, torch.Tensor):
+            a = self._part.local(np.asarray(a))
+        return self._mesh.to_device(a)
 
-    @staticmethod
-    def _out(t, like):
-        return t if isinstance(like, torch.Tensor) else t.cpu().numpy()
+    def _out(self, t, like):
+        if isinstance(like, torch.Tensor):
+            return t
+        if self._part is not None:
+            t = self._part.gather(t)
+        return t.cpu().numpy()
+
+    def _global(self, a):
+        """Global NumPy vector from a global NumPy vector or this rank's strip tensor."""
+        if isinstance(a, torch.Tensor) and self._part is not None:
+            return self._part.gather(a).cpu().numpy()
+        return np.asarray(a.cpu() if isinstance(a, torch.Tensor) else a, dtype=np.float64)
+
+    def _norm(self, *ys):
+        if self._part is not None:
+            return self._part.norm(*ys)
+        return torch.sqrt(sum(y.square().sum() for y in ys)).item()
+
+    def _amax(self, *ys):
+        if self._part is not None:
+            return self._part.amax(*ys)
+        return max(y.abs().max().item() for y in ys)
+
+    def _grad(self, x, which):
+        """G_x x or G_y x, assembled across strips on a partitioned solver."""
+        if self._part is None:
+            return self._mesh.apply(x, **{which: 1.0})
+        return self._part.step(x, **{which: 1.0})
 
     def _sys_kw(self, Sys):
         cX, cu, cY, cv, d = Sys._coeffs()
@@ -143,6 +192,9 @@ class NavierStokesSolver:
         ru, rv, rc = (torch.empty_like(U) for _ in range(3))
         m.ns_apply(U, V, Pp, ru, rv, rc, **self._sys_kw(self._Sys), c_T=-self._Gr_over_Re, T=Tt,
                    dval_u=self._dval_u, dval_v=self._dval_v, **self._ns_kw(pin_first=True))
+        if self._part is not None:
+            self._part.assemble(ru, rv, rc)
+            self._lin_sys = (U, V)   # Sys's velocity: part of the next linearisation
         return self._out(ru, u), self._out(rv, u), self._out(rc, u)
 
     def _calc_jacobians(self, u, v):
@@ -150,10 +202,18 @@ class NavierStokesSolver:
         reference's J_uu = Sys + ... does, even if _get_residuals runs again before they are used."""
         U, V = self._dev(u), self._dev(v)
         Re = self._Re
-        self._Jac_u_u = self._Sys + Re * SEM.tensordot(self._C_x, U, (2, 0))
-        self._Jac_v_v = self._Sys + Re * SEM.tensordot(self._C_y, V, (2, 0))
-        self._Jac_u_v = Re * SEM.tensordot(self._C_y, U, (2, 0))
-        self._Jac_v_u = Re * SEM.tensordot(self._C_x, V, (2, 0))
+        if self._part is None:
+            self._Jac_u_u = self._Sys + Re * SEM.tensordot(self._C_x, U, (2, 0))
+            self._Jac_v_v = self._Sys + Re * SEM.tensordot(self._C_y, V, (2, 0))
+            self._Jac_u_v = Re * SEM.tensordot(self._C_y, U, (2, 0))
+            self._Jac_v_u = Re * SEM.tensordot(self._C_x, V, (2, 0))
+        else:   # G u on a strip needs the interface exchange before it becomes a diagonal
+            m = self._mesh
+            self._Jac_u_u = self._Sys + SEMOperator(m, dg=[(Re, self._grad(U, "c_gradx"))])
+            self._Jac_v_v = self._Sys + SEMOperator(m, dg=[(Re, self._grad(V, "c_grady"))])
+            self._Jac_u_v = SEMOperator(m, dg=[(Re, self._grad(U, "c_grady"))])
+            self._Jac_v_u = SEMOperator(m, dg=[(Re, self._grad(V, "c_gradx"))])
+            self._lin = {"sys": self._lin_sys, "jac": (U, V), "stale": True}
         self._jac_kw = dict(self._sys_kw(self._Sys), juu=self._Jac_u_u._coeffs()[4], jvv=self._Jac_v_v._coeffs()[4],
                             juv=self._Jac_u_v._coeffs()[4], jvu=self._Jac_v_u._coeffs()[4])
         self._velo = None  # factorised on first use, reused until the next linearisation
@@ -168,7 +228,47 @@ class NavierStokesSolver:
         ru, rv, rc = (torch.empty_like(DU) for _ in range(3))
         m.ns_apply(DU, DV, DP, ru, rv, rc, **self._jac_kw, c_T=-self._Gr_over_Re if dT is not None else 0.0,
                    T=self._dev(dT), **self._ns_kw(pin_first=False))
+        if self._part is not None:
+            self._part.assemble(ru, rv, rc)
         return self._out(ru, du), self._out(rv, du), self._out(rc, du)
+
+    def _central_solver(self):
+        """Rank 0's whole-mesh counterpart that runs the partitioned solver's updates (same arguments,
+        no partition)."""
+        return NavierStokesSolver(**self._args)
+
+    def _get_update_partitioned(self, dres_u, dres_v, dres_cont, du0, dv0, dp0):
+        """Whole-mesh update for a strip-partitioned solver: the linearisation (the residual's u, v for
+        Sys, the Jacobian's u, v) and the right-hand sides are gathered; rank 0 hands them to its
+        whole-mesh counterpart through the reference interface (_get_residuals sets Sys,
+        _calc_jacobians the Jacobians, _get_update solves) and broadcasts the update."""
+        part = self._part
+        lin = self._lin
+        if lin is None:
+            raise RuntimeError("NavierStokes: _calc_jacobians must run before _get_update")
+        if lin.get("stale"):
+            us, vs = (self._global(a) for a in lin["sys"])
+            uj, vj = (self._global(a) for a in lin["jac"])
+            if part.rank == 0:
+                if self._twin is None:
+                    self._twin = self._central_solver()
+                z = np.zeros(self.N)
+                self._twin._get_residuals(us, vs, z, z)
+                self._twin._calc_jacobians(uj, vj)
+            lin["stale"] = False
+        rhs = [self._global(a) for a in (dres_u, dres_v, dres_cont)]
+        x0 = [None if a is None else self._global(a) for a in (du0, dv0, dp0)]
+        out = torch.zeros(3 * self.N + 1, dtype=torch.float64)
+        if part.rank == 0:
+            d = self._twin._get_update(*rhs, du0=x0[0], dv0=x0[1], dp0=x0[2])
+            out[:3 * self.N] = torch.from_numpy(np.concatenate([np.asarray(a) for a in d]))
+            out[-1] = float(getattr(self._twin, "schur_matvecs", -1))
+        out = part.broadcast(out)
+        self.schur_matvecs = int(out[-1].item())
+        d = [out[i * self.N:(i + 1) * self.N].cpu().numpy() for i in range(3)]
+        if isinstance(dres_u, torch.Tensor):
+            return tuple(self._dev(a) for a in d)
+        return tuple(d)
 
     def _velocity_solver(self):
         """Device factorisation of the Dirichlet-row-replaced velocity Jacobian -- the reference's
@@ -226,6 +326,8 @@ class NavierStokesSolver:
         unrestarted GMRES with outer augmentation.  A plain GMRES restarted at 0.3 N stagnates on small
         meshes (the Schur complement carries the spurious pressure modes of the equal-order
         discretisation), so the device GMRES runs unrestarted up to max_basis vectors."""
+        if self._part is not None:
+            return self._get_update_partitioned(dres_u, dres_v, dres_cont, du0, dv0, dp0)
         vs = self._velocity_solver()
         m = self._mesh
         ru, rv, rc = self._dev(dres_u), self._dev(dres_v), self._dev(dres_cont)
@@ -283,7 +385,7 @@ class NavierStokesSolver:
         """Newton iteration (NavierStokes_Solver.py:238-270), iterates kept on the device; NumPy in,
         NumPy out (device tensors in, device tensors out)."""
         like = T
-        Z = torch.zeros(self.N, dtype=torch.float64, device=self._mesh.device)
+        Z = torch.zeros(self._mesh.n_local, dtype=torch.float64, device=self._mesh.device)
         u = self._dev(u0) if u0 is not None else Z.clone()
         v = self._dev(v0) if v0 is not None else Z.clone()
         p = self._dev(p0) if p0 is not None else Z.clone()
@@ -292,13 +394,13 @@ class NavierStokesSolver:
         self.newton_history = []
         while True:
             res_u, res_v, res_cont = self._get_residuals(u, v, p, T)
-            norm = torch.sqrt(res_u.square().sum() + res_v.square().sum() + res_cont.square().sum()).item()
+            norm = self._norm(res_u, res_v, res_cont)
             if 'NEWTON_iter' in self._iprint:
                 print(f'NavierStokes NEWTON: {self._k}\t{norm}')
             if norm <= self._mtol_newton * np.sqrt(self.N * 3):
                 self.newton_history.append((norm, 0))
                 if 'NEWTON_suc' in self._iprint:
-                    mx = max(res_u.abs().max().item(), res_v.abs().max().item(), res_cont.abs().max().item())
+                    mx = self._amax(res_u, res_v, res_cont)
                     print(f'NavierStokes NEWTON: Converged in {self._k} iterations with max-norm {mx}')
                 break
             self._calc_jacobians(u, v)

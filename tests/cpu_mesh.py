@@ -79,6 +79,56 @@ class CPUStripMesh:
         yn[write] = z[write]
         return y
 
+    def _own_dir(self, dir_mask, dir_sides):
+        idx = np.arange(self.n_local)
+        gx, gy = self.line_begin + idx // self.NY, idx % self.NY
+        own = ~((gx == self.line_end) & (self.ex_end < self.nex))
+        if dir_mask is not None:
+            dm = dir_mask.numpy() != 0
+        else:
+            dm = (((dir_sides & 1) != 0) & (gx == 0)) | (((dir_sides & 2) != 0) & (gx == self.NX - 1)) | \
+                 (((dir_sides & 4) != 0) & (gy == 0)) | (((dir_sides & 8) != 0) & (gy == self.NY - 1))
+        return own, dm, gx * self.NY + gy
+
+    def ns_apply(self, u=None, v=None, p=None, ru=None, rv=None, rc=None, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0,
+                 c_grady=0.0, cu=None, cv=None, juu=None, juv=None, jvu=None, jvv=None, c_T=0.0, T=None, c_div=1.0,
+                 dval_u=None, dval_v=None, dir_mask=None, dir_sides=0, pin=-1, pin_val=0.0, pin_first=False,
+                 stream=None):
+        """sem_ns_apply (include/sem_ops.h) on the strip, composed from strip applies: partial sums over
+        the strip's elements; pointwise terms, Dirichlet rows and the pin of the right interface line
+        left to its right-hand owner."""
+        n = self.n_local
+        zero = torch.zeros(n, dtype=torch.float64)
+        u = zero if u is None else u
+        v = zero if v is None else v
+        p = zero if p is None else p
+        own, dm, gq = self._own_dir(dir_mask, dir_sides)
+        sysk = dict(c_mass=c_mass, c_stiff=c_stiff, c_gradx=c_gradx, c_grady=c_grady, cu=cu, cv=cv)
+        A = lambda x, **kw: self.apply(x, **kw).numpy()   # noqa: E731
+        pt = lambda c, x: own * (c.numpy() * x.numpy()) if c is not None else 0.0   # noqa: E731
+        un, vn, pn = u.numpy(), v.numpy(), p.numpy()
+        if ru is not None:
+            z = A(u, **sysk) + pt(juu, u) + pt(juv, v) + A(p, c_gradx=1.0)
+            z[dm] = own[dm] * (un[dm] - (dval_u.numpy()[dm] if dval_u is not None else 0.0))
+            ru.copy_(torch.from_numpy(z))
+        if rv is not None:
+            z = A(v, **sysk) + pt(jvu, u) + pt(jvv, v) + A(p, c_grady=1.0)
+            if T is not None:
+                z = z + c_T * A(T, c_mass=1.0)
+            z[dm] = own[dm] * (vn[dm] - (dval_v.numpy()[dm] if dval_v is not None else 0.0))
+            rv.copy_(torch.from_numpy(z))
+        if rc is not None:
+            z = c_div * (A(u, c_gradx=1.0) + A(v, c_grady=1.0))
+            pinned = gq == pin
+            pinrow = own * (pn - pin_val)
+            if pin_first:
+                z[pinned] = pinrow[pinned]
+            z[dm] = A(p, c_stiff=1.0)[dm]
+            if not pin_first:
+                z[pinned] = pinrow[pinned]
+            rc.copy_(torch.from_numpy(z))
+        return ru, rv, rc
+
     def interface_pack(self, y, bounds, buf, stream=None):
         r = bounds.index(self.ex_begin)
         left, right = (r - 1 if r > 0 else -1), (r if r < len(bounds) - 2 else -1)

@@ -1,0 +1,105 @@
+"""World-size 2/3 gloo tests (CPU) of the strip-partitioned Navier-Stokes solver
+(NavierStokesSolver(partition=...)), the NS half of the element-partitioned Boussinesq (cfg5):
+
+* _get_residuals / _calc_jacobians / _get_dresiduals (global NumPy in, global NumPy out) on element
+  strips, the three outputs' interface lines summed with one collective, against the oracle's
+  (NavierStokes_Solver.py:93-160), for both exchange protocols and a pin on a strip interface;
+* _get_update: rank 0's whole-mesh counterpart fed the gathered linearisation, the update broadcast;
+* _get_solution: the lid-driven Newton iteration on strips (distributed residual norms) takes the
+  oracle's Newton steps and lands on its solution.
+
+Each rank's strip mesh is tests/cpu_mesh.CPUStripMesh (the strip semantics of sem_ns_apply computed by
+the oracle); rank 0's whole-mesh counterpart is the oracle solver double (tests/oracle_solvers.py)."""
+import os
+import queue
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, case, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    sys.path.insert(0, here)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cpu_mesh import CPUStripMesh
+        from oracle import sem_oracle as O
+        from oracle_solvers import OracleNS
+        from sem_amd.parallel import Partition
+        from sem_amd.solvers import NavierStokesSolver
+        P, nex, ney, kind, Re, Gr = case
+        part = Partition(dist, exchange=kind, mesh_factory=CPUStripMesh)
+        ns = NavierStokesSolver(1.0, 1.0, Re, Gr, P, nex, ney, u_N=1.0, mtol=1e-11, mtol_newton=1e-9, iprint=[],
+                                partition=part)
+        ns._central_solver = lambda: OracleNS(1.0, 1.0, Re, Gr, P, nex, ney, mtol=1e-11, mtol_newton=1e-9)
+        ref = O.NSOracle(1.0, 1.0, Re, Gr, P, nex, ney, u_N=1.0)
+        r = np.random.default_rng(29)
+        u, v, p, T, du, dv, dp, dT = (r.uniform(-1, 1, ns.N) for _ in range(8))
+        errs = {}
+        rel = lambda a, b: max(np.abs(x - y).max() / np.abs(y).max() for x, y in zip(a, b))  # noqa: E731
+        errs["res"] = rel(ns._get_residuals(u, v, p, T), ref.residuals(u, v, p, T))
+        ns._calc_jacobians(u, v)
+        ref.calc_jacobians(u, v)
+        errs["dres"] = rel(ns._get_dresiduals(du, dv, dp, dT), ref.dresiduals(du, dv, dp, dT))
+        errs["dres_noT"] = rel(ns._get_dresiduals(du, dv, dp), ref.dresiduals(du, dv, dp))
+        # lid-driven Newton solve (NavierStokes_Solver.py:238-270) from rest, T = 0
+        z = np.zeros(ns.N)
+        us, vs, ps = ns._get_solution(z)
+        uo, vo, po, hist = ref.solution(z, mtol=1e-11, mtol_newton=1e-9)
+        errs["newton"] = (ns._k, len(hist) - 1)
+        errs["solve"] = max(np.abs(us - uo).max(), np.abs(vs - vo).max())
+        # one update at that state on a consistent right-hand side (the Jacobian of a known step)
+        ns._get_residuals(uo, vo, po, z)
+        ns._calc_jacobians(uo, vo)
+        ref.residuals(uo, vo, po, z)
+        ref.calc_jacobians(uo, vo)
+        rhs = ref.dresiduals(0.1 * du, 0.1 * dv, 0.1 * dp)
+        d = ns._get_update(*rhs)
+        want = ref.update(*rhs, mtol=1e-11)[:2]
+        errs["update"] = max(np.abs(a - b).max() for a, b in zip(d[:2], want))
+        q.put((rank, errs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,case", [
+    (2, (4, 4, 3, "allreduce", 100.0, 50.0)),   # pinned node N//2 on the strip interface line
+    (2, (4, 4, 3, "p2p", 200.0, 100.0)),
+    (3, (4, 6, 3, "allreduce", 50.0, 20.0)),
+])
+def test_partitioned_ns_solver_gloo(world, case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, t0 = {}, time.time()
+    while len(res) < world:     # fail fast when a rank dies instead of waiting out the queue
+        try:
+            k, v = q.get(timeout=2)
+            res[k] = v
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead and time.time() - t0 < 300, f"rank failed (exit codes {dead})"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, e in res.items():
+        assert e["res"] < 1e-13 and e["dres"] < 1e-13 and e["dres_noT"] < 1e-13, (rank, e)
+        assert e["update"] < 1e-9, (rank, e)
+        assert e["newton"][0] == e["newton"][1], (rank, e)
+        assert e["solve"] < 1e-8, (rank, e)

@@ -136,3 +136,67 @@ def test_partitioned_cd_solver(gpu, world, kind, overlap):
         assert np.abs(pdres - dres).max() <= 1e-13 * np.abs(dres).max(), rank
         assert np.abs(psol - sol).max() < 1e-8, rank
         assert abs(mv - cd.matvecs) <= 2, (rank, mv, cd.matvecs)
+
+
+NS_CASE = dict(P=4, nex=6, ney=4, Re=100.0, Gr=50.0)
+
+
+def _ns_fields(N):
+    r = np.random.default_rng(41)
+    return [r.uniform(-1, 1, N) for _ in range(7)]
+
+
+def _ns_run(ns):
+    """The NS solver methods the Boussinesq coupler calls, at a seeded state, then a lid-driven solve."""
+    u, v, p, T, du, dv, dp = _ns_fields(ns.N)
+    out = {"res": ns._get_residuals(u, v, p, T)}
+    ns._calc_jacobians(u, v)
+    out["dres"] = ns._get_dresiduals(du, dv, dp, T)
+    z = np.zeros(ns.N)
+    out["sol"] = ns._get_solution(z)
+    out["newton"] = ns._k
+    return out
+
+
+def _worker_ns(rank, world, port, q, kind):
+    """NavierStokesSolver(partition=...) on real strip meshes (the fused strip sem_ns_apply, interface
+    assembly of the three outputs in one collective); updates by rank 0's whole-mesh counterpart."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sem_amd.parallel import Partition
+        from sem_amd.solvers import NavierStokesSolver
+        c = NS_CASE
+        ns = NavierStokesSolver(1.0, 1.0, c["Re"], c["Gr"], c["P"], c["nex"], c["ney"], u_N=1.0, mtol=1e-10,
+                                mtol_newton=1e-9, iprint=[], partition=Partition(dist, exchange=kind))
+        q.put((rank, _ns_run(ns)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind", [(2, "allreduce"), (3, "p2p")])
+def test_partitioned_ns_solver(gpu, world, kind):
+    from sem_amd.solvers import NavierStokesSolver
+    c = NS_CASE
+    ns = NavierStokesSolver(1.0, 1.0, c["Re"], c["Gr"], c["P"], c["nex"], c["ney"], u_N=1.0, mtol=1e-10,
+                            mtol_newton=1e-9, iprint=[])
+    want = _ns_run(ns)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_ns, args=(r, world, port, q, kind)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got in out:
+        for key in ("res", "dres"):
+            for a, b in zip(got[key], want[key]):
+                assert np.abs(a - b).max() <= 1e-13 * np.abs(b).max(), (rank, key)
+        assert got["newton"] == want["newton"], rank
+        for a, b in zip(got["sol"][:2], want["sol"][:2]):
+            assert np.abs(a - b).max() < 1e-8, rank
