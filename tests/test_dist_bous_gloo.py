@@ -75,3 +75,59 @@ def test_parallel_coupler_matches_sequential(mode):
     # each rank ran only its own block solves
     assert calls0["ns_update"] == 0 and calls1["cd_update"] == 0
     assert calls0["cd_update"] == calls1["ns_update"] > 0 or mode == "JNK" and it0 == 0
+
+
+def _worker_partitioned(rank, world, port, key, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.dirname(here), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import golden
+        from cpu_mesh import CPUStripMesh
+        from oracle_solvers import OracleNS
+        from sem_amd.solvers.boussinesq import partitioned_coupler
+        g = golden("bous.npz")
+        Pc, nxc, nyc, Pn, nxn, nyn = (int(a) for a in g[key + "_cfg"])
+        Re, Ra, Pr = 1e3, 1e3, 0.71
+        c = partitioned_coupler(dist, 1.0, 1.0, Re, Ra, Pr, Pc, nxc, nyc, Pn, nxn, nyn, mesh_factory=CPUStripMesh,
+                                mode=str(g[key + "_mode"]))
+        c.ns._central_solver = lambda: OracleNS(1.0, 1.0, Re, Ra / Pr, Pn, nxn, nyn, mtol=1e-13, mtol_newton=1e-13)
+        R = c.residuals(g[key + "_x"])
+        c.linearize(g[key + "_x"])
+        JR = c.jacobian_apply(g[key + "_dx"])
+        T, u, v, p = c.solve()
+        q.put((rank, R, JR, T, u, v, c.iterations))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,key", [(2, "a"), (2, "c")])
+def test_element_partitioned_coupler(world, key):
+    """cfg5's structure at the golden's size: both solvers strip-partitioned over `world` ranks
+    (partitioned_coupler), against the reference solver classes driven through the same coupling
+    (tests/golden/bous.npz): coupled residual / Jacobian apply to 1e-12, the same Newton count, the
+    fields to the nonlinear tolerance."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from conftest import golden
+    g = golden("bous.npz")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_partitioned, args=(r, world, port, key, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=600) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, R, JR, T, u, v, iters in out:
+        assert np.abs(R - g[key + "_R"]).max() <= 1e-12 * np.abs(g[key + "_R"]).max(), rank
+        assert np.abs(JR - g[key + "_JR"]).max() <= 1e-12 * np.abs(g[key + "_JR"]).max(), rank
+        assert iters == int(g[key + "_iters"]), (rank, iters)
+        for name, a in zip("Tuv", (T, u, v)):
+            ref = g[key + "_" + name]
+            assert np.abs(a - ref).max() <= 1e-6 * max(np.abs(ref).max(), 1e-3), (rank, name)

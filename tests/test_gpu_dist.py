@@ -200,3 +200,60 @@ def test_partitioned_ns_solver(gpu, world, kind):
         assert got["newton"] == want["newton"], rank
         for a, b in zip(got["sol"][:2], want["sol"][:2]):
             assert np.abs(a - b).max() < 1e-8, rank
+
+
+CFG5 = dict(P=12, ne=128, Re=1e3, Ra=1e6, Pr=0.71)
+
+
+def _cfg5_state(DOF):
+    r = np.random.default_rng(55)
+    return r.uniform(-0.5, 0.5, DOF), r.uniform(-1, 1, DOF)
+
+
+def _worker_cfg5(rank, world, port, q):
+    """BASELINE cfg5's element-partitioned coupler (128^2, P=12, both solvers strip-partitioned): one
+    coupled residual and Jacobian apply (every apply a strip launch + interface exchange)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sem_amd.solvers.boussinesq import partitioned_coupler
+        c5 = CFG5
+        c = partitioned_coupler(dist, 1.0, 1.0, c5["Re"], c5["Ra"], c5["Pr"], c5["P"], c5["ne"], c5["ne"], c5["P"],
+                                c5["ne"], c5["ne"])
+        x, dx = _cfg5_state(c.DOF)
+        R = c.residuals(x)
+        c.linearize(x)
+        JR = c.jacobian_apply(dx)
+        if rank == 0:
+            q.put((R, JR))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cfg5_element_partitioned_coupled_maps(gpu):
+    """cfg5 (128^2, P=12, 9.45 M coupled DOFs) split over 4 ranks on one GPU: the partitioned coupled
+    residual and Jacobian apply equal the whole-mesh device coupler's to 1e-13 (the whole-mesh maps are
+    pinned to the reference at small sizes and by cfg5_checksums.npz at this size)."""
+    from sem_amd.solvers.boussinesq import BoussinesqCoupler
+    c5 = CFG5
+    c = BoussinesqCoupler(1.0, 1.0, c5["Re"], c5["Ra"], c5["Pr"], c5["P"], c5["ne"], c5["ne"], c5["P"], c5["ne"],
+                          c5["ne"])
+    x, dx = _cfg5_state(c.DOF)
+    R = c.residuals(x)
+    c.linearize(x)
+    JR = c.jacobian_apply(dx)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_worker_cfg5, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    PR, PJR = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.abs(PR - R).max() <= 1e-13 * np.abs(R).max()
+    assert np.abs(PJR - JR).max() <= 1e-13 * np.abs(JR).max()
