@@ -52,3 +52,22 @@ def test_de_vahl_davis_ra1e3(gpu):
     assert abs(u.max() * 710 - 3.649) < 0.01 * 3.649
     assert abs(v.max() * 710 - 3.697) < 0.01 * 3.697
     assert np.abs(T).max() <= 0.5 + 1e-9
+
+
+def test_de_vahl_davis_ra1e4_midlines(gpu):
+    """cfg4's physics on a 16^2, P=8 mesh: the JNK coupler from rest through Ra = 1e3 to Ra = 1e4
+    (continuation through the coupler's initial guess, as tools/bous_solve.py runs cfg4), then the
+    de Vahl Davis (1983) midline maxima: u_max*RePr = 16.178 at y = 0.823 on x = 1/2 and
+    v_max*RePr = 19.617 at x = 0.119 on y = 1/2."""
+    from sem_amd.solvers.boussinesq import BoussinesqCoupler
+    x = None
+    for Ra in (1e3, 1e4):
+        c = BoussinesqCoupler(1.0, 1.0, 1e3, Ra, 0.71, 8, 16, 16, 8, 16, 16, mode="JNK")
+        x = np.concatenate(c.solve(x))
+    N = c.Nns
+    u, v = x[c.Ncd:c.Ncd + N], x[c.Ncd + N:c.Ncd + 2 * N]
+    s = np.linspace(0.0, 1.0, 1001)
+    um = np.asarray(c.ns._get_interpol(u, np.meshgrid([0.5], s, indexing="ij")))[0] * 710.0
+    vm = np.asarray(c.ns._get_interpol(v, np.meshgrid(s, [0.5], indexing="ij")))[:, 0] * 710.0
+    assert abs(um.max() - 16.178) < 0.005 * 16.178 and abs(s[um.argmax()] - 0.823) <= 0.004
+    assert abs(vm.max() - 19.617) < 0.005 * 19.617 and abs(s[vm.argmax()] - 0.119) <= 0.004
