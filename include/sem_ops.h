@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 5
+#define SEM_ABI_VERSION 6
 
 enum sem_status {
   SEM_OK = 0,
@@ -247,6 +247,8 @@ typedef struct sem_velocity_desc {
   unsigned dir_sides;
   int ncomp;          /* 0 or 2: the velocity pair; 1: the scalar operator A + diag(juu) alone (the
                        * convection-diffusion Jacobian, ConvectionDiffusion_Solver.py:104-121) */
+  int col_begin;      /* ABI 6: A_II holds element columns [col_begin, col_end) only (col_end 0 = all), */
+  int col_end;        /* so a large mesh's dense interiors are assembled a chunk of columns at a time */
 } sem_velocity_desc;
 /* Sizes for ncomp components per node (m = ncomp N_y unknowns per line); the velocity form is
  * sem_line_block_sizes(h, 2, sizes). */

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE = range(6)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
@@ -41,7 +41,8 @@ class SemApplyDesc(C.Structure):
 class SemVelocityDesc(C.Structure):
     _fields_ = [("c_mass", C.c_double), ("c_stiff", C.c_double), ("c_gradx", C.c_double), ("c_grady", C.c_double),
                 ("cu", C.c_void_p), ("cv", C.c_void_p), ("juu", C.c_void_p), ("juv", C.c_void_p), ("jvu", C.c_void_p),
-                ("jvv", C.c_void_p), ("dir_mask", C.c_void_p), ("dir_sides", C.c_uint), ("ncomp", C.c_int)]
+                ("jvv", C.c_void_p), ("dir_mask", C.c_void_p), ("dir_sides", C.c_uint), ("ncomp", C.c_int),
+                ("col_begin", C.c_int), ("col_end", C.c_int)]
 
 
 class SemNestedDesc(C.Structure):

@@ -24,7 +24,10 @@
 //   F    [L][c NY + gy]           row on line L+1, column on line L
 // Dirichlet rows (the reference's mask_bound) are identity rows: 1 on the diagonal, 0 elsewhere,
 // in every piece.  The dense blocks are zero-filled by the caller (hipMemsetAsync); each row is
-// written by exactly one thread, so nothing races.
+// written by exactly one thread, so nothing races.  A column range [c0, c1) restricts the A_II
+// writes to those element columns (A_II then holds c1 - c0 blocks): the factorisation assembles and
+// condenses a large mesh's dense interiors a chunk of columns at a time; every other piece is
+// written in full by every call.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -40,6 +43,7 @@ struct VelocityArgs {
   double fKx, fKy, fM, fX, fY;  // cK dy/dx, cK dx/dy, cM dx dy/4, cX dy/2, cY dx/2
   int P, nex, ney, NY, NX;
   int nc;  // components per node: 2 (NS velocity [u | v]) or 1 (a scalar operator, e.g. the CD Jacobian)
+  int c0, c1;  // element columns whose A_II blocks are written (A_II indexed from c0)
   unsigned sides;
   double *AII, *D, *aIB, *aBI, *E, *F;
 };
@@ -67,11 +71,26 @@ __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs
   // row pointer into the dense block holding this row, and the column offset of line-local node 0
   double* row;
   int64_t col0;  // column index of (this line, c = 0, gy = 0) within the block
+  if (l != 0 && (L < a.c0 || L >= a.c1)) {  // interior row of a column outside the A_II range: aIB only
+    double* ib = a.aIB + (static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 * m + r;
+    if (dir) {
+      ib[0] = 0.0;
+      ib[m] = 0.0;
+      return;
+    }
+    const int ey = gy / P, j = gy - ey * P;
+    const double my = j != 0 ? w[j] : (ey > 0 ? w[P] : 0.0) + (ey < a.ney ? w[0] : 0.0);
+    const double cu = a.cu ? a.cu[node] : 1.0;
+    const double fx = a.fKx * my, gxc = a.fX * cu * my;
+    ib[0] = fx * Ks[l * n] + gxc * Gs[l * n];
+    ib[m] = fx * Ks[l * n + P] + gxc * Gs[l * n + P];
+    return;
+  }
   if (l == 0) {
     row = a.D + (static_cast<int64_t>(L) * m + r) * m;
     col0 = 0;
   } else {
-    row = a.AII + (static_cast<int64_t>(L) * nI + (l - 1) * m + r) * nI;
+    row = a.AII + (static_cast<int64_t>(L - a.c0) * nI + (l - 1) * m + r) * nI;
     col0 = static_cast<int64_t>(l - 1) * m;
   }
   const int64_t self = col0 + r;
@@ -192,11 +211,14 @@ int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, 
   if (nc != 1 && nc != 2) return sem::set_error(SEM_EINVAL, "ncomp must be 0, 1 or 2");
   if (nc == 1 && (d->juv || d->jvu || d->jvv))
     return sem::set_error(SEM_EINVAL, "a one-component operator has no juv / jvu / jvv term");
+  const int c0 = d->col_begin, c1 = d->col_end == 0 ? h->nex : d->col_end;
+  if (c0 < 0 || c1 > h->nex || c0 >= c1) return sem::set_error(SEM_EINVAL, "bad A_II column range");
   int64_t sz[6];
   sem_line_block_sizes(h, nc, sz);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int st;
-  if (h->P > 1 && (st = sem::hip_check_v(hipMemsetAsync(AII, 0, sz[0] * sizeof(double), s), "memset A_II")))
+  const int64_t szA = sz[0] / h->nex * (c1 - c0);
+  if (h->P > 1 && (st = sem::hip_check_v(hipMemsetAsync(AII, 0, szA * sizeof(double), s), "memset A_II")))
     return st;
   if ((st = sem::hip_check_v(hipMemsetAsync(D, 0, sz[1] * sizeof(double), s), "memset D"))) return st;
   sem::VelocityArgs a{};
@@ -220,6 +242,8 @@ int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, 
   a.NY = static_cast<int>(h->NY);
   a.NX = static_cast<int>(h->NX);
   a.nc = nc;
+  a.c0 = c0;
+  a.c1 = c1;
   a.AII = AII;
   a.D = D;
   a.aIB = aIB;

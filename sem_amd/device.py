@@ -139,10 +139,12 @@ class Mesh:
                                                   self.stream_ptr(stream)))
 
     def velocity_blocks(self, blocks, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None, cv=None,
-                        juu=None, juv=None, jvu=None, jvv=None, dir_mask=None, dir_sides=0, ncomp=2, stream=None):
+                        juu=None, juv=None, jvu=None, jvv=None, dir_mask=None, dir_sides=0, ncomp=2, cols=None,
+                        stream=None):
         """Static-condensation pieces of the NS velocity Jacobian (include/sem_ops.h,
         sem_velocity_blocks) into `blocks` (VelocityJacobianSolver.empty_blocks layout); ncomp=1:
-        the scalar operator A + diag(juu) alone."""
+        the scalar operator A + diag(juu) alone.  cols=(c0, c1): blocks["AII"] holds the dense
+        interiors of element columns [c0, c1) only."""
         for nm, t in (("cu", cu), ("cv", cv), ("juu", juu), ("juv", juv), ("jvu", jvu), ("jvv", jvv)):
             self._vec(t, nm)
         if dir_mask is not None and (dir_mask.dtype != torch.uint8 or dir_mask.numel() != self.n_local):
@@ -150,6 +152,10 @@ class Mesh:
         sizes = (C.c_int64 * 6)()
         _lib.check(self._lib.sem_line_block_sizes(self._h, int(ncomp), sizes))
         names = ("AII", "D", "aIB", "aBI", "E", "F")
+        c0, c1 = (0, self.nex) if cols is None else (int(cols[0]), int(cols[1]))
+        if not 0 <= c0 < c1 <= self.nex:
+            raise ValueError("cols must be a non-empty element-column range")
+        sizes[0] = sizes[0] // self.nex * (c1 - c0)
         for nm, sz in zip(names, sizes):
             t = blocks.get(nm)
             if sz and (t is None or t.numel() != sz or t.dtype != torch.float64 or t.device != self.device
@@ -157,7 +163,7 @@ class Mesh:
                 raise ValueError(f"block {nm} must be a contiguous float64 tensor of {sz} entries on {self.device}")
         d = _lib.SemVelocityDesc(float(c_mass), float(c_stiff), float(c_gradx), float(c_grady), _ptr(cu), _ptr(cv),
                                  _ptr(juu), _ptr(juv), _ptr(jvu), _ptr(jvv), _ptr(dir_mask), int(dir_sides),
-                                 int(ncomp))
+                                 int(ncomp), c0, c1)
         _lib.check(self._lib.sem_velocity_blocks(self._h, C.byref(d), *(_ptr(blocks.get(nm)) for nm in names),
                                                  self.stream_ptr(stream)))
         return blocks

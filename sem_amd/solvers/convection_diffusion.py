@@ -212,11 +212,10 @@ class ConvectionDiffusionSolver:
                 raise RuntimeError("ConvectionDiffusion: _get_residuals must run before _get_update")
             m = self._mesh
             vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
-            blocks = vs.empty_blocks()
             cX, cu, cY, cv, d = self._Sys._coeffs()
-            m.velocity_blocks(blocks, c_mass=self._Sys.cM, c_stiff=self._Sys.cK, c_gradx=cX, cu=cu, c_grady=cY,
-                              cv=cv, juu=d, ncomp=1, **self._dir.kw())
-            vs.factor(blocks.pop("AII"), **blocks)
+            vs.factor_from(lambda b, cols: m.velocity_blocks(b, cols=cols, c_mass=self._Sys.cM, c_stiff=self._Sys.cK,
+                                                             c_gradx=cX, cu=cu, c_grady=cY, cv=cv, juu=d, ncomp=1,
+                                                             **self._dir.kw()))
             if m.device.type == "cuda":
                 vs.capture()
             self._factor = vs

@@ -282,9 +282,8 @@ class NavierStokesSolver:
         m = self._mesh
         vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior,
                                     sweep=self._velocity_sweep)
-        blocks = vs.empty_blocks()
-        m.velocity_blocks(blocks, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
-        vs.factor(blocks.pop("AII"), **blocks)
+        vs.factor_from(lambda b, cols: m.velocity_blocks(b, cols=cols, dir_mask=self._dir.mask,
+                                                         dir_sides=self._dir.sides, **self._jac_kw))
         if self._velocity_graph:
             vs.capture()
         self._velo = vs
@@ -299,11 +298,9 @@ class NavierStokesSolver:
         if self._Ap is None:
             m = self._mesh
             vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
-            blocks = vs.empty_blocks()
             mask = torch.zeros(m.n_local, dtype=torch.uint8, device=m.device)
             mask[self._pin if self._pin >= 0 else self.N // 2] = 1
-            m.velocity_blocks(blocks, c_stiff=1.0, ncomp=1, dir_mask=mask)
-            vs.factor(blocks.pop("AII"), **blocks)
+            vs.factor_from(lambda b, cols: m.velocity_blocks(b, cols=cols, c_stiff=1.0, ncomp=1, dir_mask=mask))
             if self._velocity_graph and m.device.type == "cuda":
                 vs.capture()
             self._Ap = vs

@@ -72,17 +72,79 @@ class VelocityJacobianSolver:
         self.factored = False
 
     # ------------------------------------------------------------------ assembly
-    def empty_blocks(self):
+    def empty_blocks(self, with_interior=True):
         """Zeroed storage for the pieces, in sem_velocity_blocks' layout."""
         P, nex, m, nI = self.P, self.nex, self.m, self.nI
         z = dict(dtype=torch.float64, device=self.device)
-        return dict(AII=torch.zeros((nex, nI, nI), **z) if P > 1 else None,
+        return dict(AII=torch.zeros((nex, nI, nI), **z) if P > 1 and with_interior else None,
                     D=torch.zeros((nex + 1, m, m), **z),
                     aIB=torch.zeros((nex, P - 1, 2, m), **z) if P > 1 else None,
                     aBI=torch.zeros((nex, 2, P - 1, m), **z) if P > 1 else None,
                     E=torch.zeros((nex, m), **z), F=torch.zeros((nex, m), **z))
 
     # ------------------------------------------------------------------ factorisation
+    def interior_bytes(self):
+        """Bytes of the dense A_II blocks of the whole mesh."""
+        return self.nex * self.nI * self.nI * 8
+
+    def factor_from(self, fill, budget_bytes=48 << 30):
+        """Assemble and factor.  fill(blocks, cols) writes the pieces (sem_velocity_blocks) with
+        blocks["AII"] holding the dense interiors of element columns cols = (c0, c1).  When the whole
+        mesh's A_II fits in budget_bytes this is one fill + factor(); otherwise (cfg5: 1.17 TB of
+        dense interiors at 128^2, P = 12) the nested condensation runs a chunk of columns at a time,
+        each chunk's A_II assembled, condensed and freed before the next."""
+        per_col = self.nI * self.nI * 8 + 3 * self.nI * 2 * self.m * 8   # A_II + A_IB, W, work per column
+        if self.P == 1 or self.nex * per_col <= budget_bytes:
+            blocks = self.empty_blocks()
+            fill(blocks, (0, self.nex))
+            return self.factor(blocks.pop("AII"), **blocks)
+        if self.interior != "nested":
+            raise ValueError("column-chunked factorisation needs interior='nested'")
+        chunk = max(1, int(budget_bytes // per_col))
+        blocks = self.empty_blocks(with_interior=False)
+        self._nested_index()
+        P, nex, ney, m = self.P, self.nex, self.ney, self.m
+        ni, ne1, n_e = self._pi.shape[1], self._ne1, self._pe.numel()
+        z = dict(dtype=torch.float64, device=self.device)
+        Xi, Yie = torch.empty((nex, ney, ni, ni), **z), torch.empty((nex, ney, ni, 2 * ne1), **z)
+        Aei, Sinv = torch.empty((nex, ney, 2 * ne1, ni), **z), torch.empty((nex, n_e, n_e), **z)
+        S_diag = S_up = S_lo = None
+        for c0 in range(0, nex, chunk):
+            c1 = min(nex, c0 + chunk)
+            blocks["AII"] = torch.zeros((c1 - c0, self.nI, self.nI), **z)
+            fill(blocks, (c0, c1))
+            AII = blocks.pop("AII")
+            Xi[c0:c1], Yie[c0:c1], Aei[c0:c1], Sinv[c0:c1] = self._nested_pieces(AII)
+            del AII
+            if S_diag is None:   # every fill writes the line pieces in full: take them from the first
+                aIB, aBI = blocks["aIB"], blocks["aBI"]
+                S_diag = blocks["D"].clone()
+                S_up, S_lo = torch.diag_embed(blocks["E"]), torch.diag_embed(blocks["F"])
+            self._Xi, self._Yie, self._Aei, self._Se_inv = Xi, Yie, Aei, Sinv
+            AIB = torch.diag_embed(aIB[c0:c1]).permute(0, 1, 3, 2, 4).reshape(c1 - c0, self.nI, 2 * m)
+            W = self._nested_solve(AIB, slice(c0, c1))
+            del AIB
+            C = self._interface_coupling(aBI[c0:c1], W)
+            del W
+            S_diag[c0:c1] -= C[:, 0, :, 0, :]
+            S_diag[c0 + 1:c1 + 1] -= C[:, 1, :, 1, :]
+            S_up[c0:c1] -= C[:, 0, :, 1, :]
+            S_lo[c0:c1] -= C[:, 1, :, 0, :]
+            del C
+        self._nested_finish()
+        self.W = None
+        self.aBI, self.aIB = aBI, aIB
+        self._sweep_factor(S_diag, S_up, S_lo)
+
+    def _interface_coupling(self, aBI, W):
+        """C[e, s, r, t, k] = sum_l aBI[e, s, l, r] W[e, l, r, t, k]: A_BI A_II^-1 A_IB per column."""
+        nc, P, m = W.shape[0], self.P, self.m
+        Wr = W.view(nc, P - 1, m, 2, m)
+        C = torch.zeros((nc, 2, m, 2, m), dtype=torch.float64, device=self.device)
+        for li in range(P - 1):
+            C += aBI[:, :, li, :, None, None] * Wr[:, None, li]
+        return C
+
     def factor(self, AII, D, aIB, aBI, E, F):
         """Condense and factor.  AII is consumed (its storage is reused for the LU factors)."""
         P, nex, m = self.P, self.nex, self.m
@@ -100,11 +162,7 @@ class VelocityJacobianSolver:
                     raise RuntimeError("velocity Jacobian: singular interior block")
                 W = torch.linalg.lu_solve(LU, piv, AIB)
             del AIB
-            Wr = W.view(nex, P - 1, m, 2, m)
-            # C[e, s, r, t, k] = sum_l aBI[e, s, l, r] W[e, l, r, t, k]: A_BI W for both interface lines
-            C = torch.zeros((nex, 2, m, 2, m), dtype=torch.float64, device=self.device)
-            for li in range(P - 1):
-                C += aBI[:, :, li, :, None, None] * Wr[:, None, li]
+            C = self._interface_coupling(aBI, W)   # A_BI W for both interface lines
             S_diag = D.clone()
             S_diag[:-1] -= C[:, 0, :, 0, :]
             S_diag[1:] -= C[:, 1, :, 1, :]
@@ -122,6 +180,10 @@ class VelocityJacobianSolver:
             self.aBI, self.aIB = aBI, aIB
         else:
             S_diag, S_up, S_lo = D, torch.diag_embed(E), torch.diag_embed(F)
+        self._sweep_factor(S_diag, S_up, S_lo)
+
+    def _sweep_factor(self, S_diag, S_up, S_lo):
+        nex, m = self.nex, self.m
         if self.sweep == "cr":
             self._cr_factor(S_diag, S_up, S_lo)
             self.factored = True
@@ -263,44 +325,51 @@ class VelocityJacobianSolver:
         self._pe = pe.reshape(-1)                                       # (n_e,)
         self._pe_el = torch.cat((pe[:-1].reshape(ney, -1), pe[1:].reshape(ney, -1)), dim=1)  # edges k=n, n+1
 
-    def _nested_factor(self, AII):
-        self._nested_index()
-        nex, ney = self.nex, self.ney
+    def _nested_pieces(self, AII):
+        """Element-interior inverses Xi, Xi A_ie, A_ei and the inverse edge Schur blocks of the
+        columns whose dense interiors AII holds."""
+        nex, ney = AII.shape[0], self.ney
         pi, pe, pel = self._pi, self._pe, self._pe_el
         e = torch.arange(nex, device=self.device)[:, None, None, None]
         A_ii = AII[e, pi[None, :, :, None], pi[None, :, None, :]]     # (nex, ney, ni, ni)
         A_ie = AII[e, pi[None, :, :, None], pel[None, :, None, :]]    # (nex, ney, ni, 2 ne1)
         A_ei = AII[e, pel[None, :, :, None], pi[None, :, None, :]]    # (nex, ney, 2 ne1, ni)
         S_e = AII[e[:, :, 0], pe[None, :, None], pe[None, None, :]]   # (nex, n_e, n_e)
-        self._Xi = batched_inverse(A_ii.reshape(-1, *A_ii.shape[-2:])).view(A_ii.shape)
-        self._Yie = self._Xi @ A_ie
-        self._Aei = A_ei
-        C = (A_ei @ self._Yie).view(nex, ney, 2, self._ne1, 2, self._ne1)
+        Xi = batched_inverse(A_ii.reshape(-1, *A_ii.shape[-2:])).view(A_ii.shape)
+        Yie = Xi @ A_ie
+        C = (A_ei @ Yie).view(nex, ney, 2, self._ne1, 2, self._ne1)
         S = S_e.view(nex, ney + 1, self._ne1, ney + 1, self._ne1)
         n = torch.arange(ney, device=self.device)
         for a in range(2):          # element n touches edge rows k = n + a, columns k = n + b
             for b in range(2):
                 S[:, n + a, :, n + b, :] -= C[:, :, a, :, b, :].permute(1, 0, 2, 3)  # index dims lead
-        self._Se_inv = batched_inverse(S_e)
+        return Xi, Yie, A_ei, batched_inverse(S_e)
+
+    def _nested_factor(self, AII):
+        self._nested_index()
+        self._Xi, self._Yie, self._Aei, self._Se_inv = self._nested_pieces(AII)
+        self._nested_finish()
+
+    def _nested_finish(self):
         if self.device.type == "cuda":   # column-major blocks for sem_nested_solve (ns_condense.hip)
             self._hipT = tuple(t.transpose(-1, -2).contiguous() for t in
                                (self._Xi, self._Aei, self._Yie, self._Se_inv))
             self._pi, self._pe = self._pi.contiguous(), self._pe.contiguous()
 
-    def _nested_solve(self, R):
-        """A_II^-1 R for every column at once; R (nex, nI, k)."""
-        nex, ney, ne1 = self.nex, self.ney, self._ne1
+    def _nested_solve(self, R, cols=slice(None)):
+        """A_II^-1 R for every column (or the columns `cols`) at once; R (columns, nI, k)."""
+        nex, ney, ne1 = R.shape[0], self.ney, self._ne1
         k = R.shape[-1]
         Ri = R[:, self._pi]                                             # (nex, ney, ni, k)
         Re = R[:, self._pe].clone()                                     # (nex, n_e, k)
-        Ti = self._Xi @ Ri
-        Cn = self._Aei @ Ti                                             # (nex, ney, 2 ne1, k)
+        Ti = self._Xi[cols] @ Ri
+        Cn = self._Aei[cols] @ Ti                                       # (nex, ney, 2 ne1, k)
         Rv = Re.view(nex, ney + 1, ne1, k)
         Rv[:, :-1] -= Cn[:, :, :ne1]
         Rv[:, 1:] -= Cn[:, :, ne1:]
-        Ye = self._Se_inv @ Re                                          # (nex, n_e, k)
+        Ye = self._Se_inv[cols] @ Re                                    # (nex, n_e, k)
         Yv = Ye.view(nex, ney + 1, ne1, k)
-        Yi = Ti - self._Yie @ torch.cat((Yv[:, :-1], Yv[:, 1:]), dim=2)
+        Yi = Ti - self._Yie[cols] @ torch.cat((Yv[:, :-1], Yv[:, 1:]), dim=2)
         Y = torch.empty_like(R)
         Y[:, self._pi] = Yi
         Y[:, self._pe] = Ye

@@ -165,3 +165,38 @@ def test_block_gemv_wide_and_narrow(gpu, nb, m, S):
     _lib.check(lib.sem_block_gemv(nb, m, S, P_(M.data_ptr()), src, ld, P_(xrow.data_ptr()), P_(y.data_ptr()),
                                   y.stride(0), P_(yrow.data_ptr()), 1, P_(torch.cuda.current_stream().cuda_stream)))
     assert (y - want).abs().max().item() <= 1e-12 * want.abs().max().item()
+
+
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 8, 3, 700.0), (6, 5, 2, 1000.0)])
+def test_column_ranged_blocks_and_chunked_factor(gpu, P, nex, ney, Re):
+    """sem_velocity_blocks with an A_II column range (ABI 6) writes exactly those columns' dense
+    interiors and every other piece in full; the column-chunked factorisation it feeds (the cfg5 path,
+    VelocityJacobianSolver.factor_from below its memory budget) solves the Jacobian like the one-shot
+    factorisation."""
+    from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
+    ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    ns = _device_solver(P, nex, ney, Re, u, v)
+    kw = dict(juu=ns._Jac_u_u._coeffs()[4], juv=ns._Jac_u_v._coeffs()[4], jvu=ns._Jac_v_u._coeffs()[4],
+              jvv=ns._Jac_v_v._coeffs()[4], dir_mask=ns._dir.mask, dir_sides=ns._dir.sides, **ns._sys_kw(ns._Sys))
+    vs = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
+    full = vs.empty_blocks()
+    ns._mesh.velocity_blocks(full, **kw)
+    for c0, c1 in ((0, 1), (2, 5), (nex - 1, nex)):
+        part = vs.empty_blocks(with_interior=False)
+        part["AII"] = torch.zeros((c1 - c0, vs.nI, vs.nI), dtype=torch.float64, device=ns._mesh.device)
+        part["aIB"].fill_(7.0)   # every piece is rewritten
+        ns._mesh.velocity_blocks(part, cols=(c0, c1), **kw)
+        assert torch.equal(part["AII"], full["AII"][c0:c1])
+        for k in ("D", "aIB", "aBI", "E", "F"):
+            assert torch.equal(part[k], full[k]), k
+    with pytest.raises(ValueError):
+        ns._mesh.velocity_blocks(full, cols=(3, 3), **kw)
+    ch = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
+    per_col = ch.nI * ch.nI * 8 + 3 * ch.nI * 2 * ch.m * 8
+    ch.factor_from(lambda b, cols: ns._mesh.velocity_blocks(b, cols=cols, **kw), budget_bytes=2 * per_col)
+    r = np.random.default_rng(3)
+    bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
+    xu, xv = ch.solve(ns._dev(bu), ns._dev(bv))
+    got = np.hstack((xu.cpu().numpy(), xv.cpu().numpy()))
+    want = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
+    assert np.abs(got - want).max() <= 1e-9 * np.abs(want).max()

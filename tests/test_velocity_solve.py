@@ -58,3 +58,31 @@ def test_scalar_condensation_solves_the_cd_jacobian(P, nex, ney, Pe, sweep):
     assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
     with pytest.raises(ValueError):
         vs.solve(torch.as_tensor(b), torch.as_tensor(b))
+
+
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 5, 2, 100.0), (3, 6, 2, 50.0), (6, 3, 2, 1000.0)])
+@pytest.mark.parametrize("chunk_cols", [1, 2])
+def test_column_chunked_factor_matches_one_shot(P, nex, ney, Re, chunk_cols):
+    """factor_from with a budget of chunk_cols columns (the cfg5 path: dense interiors assembled,
+    condensed and freed a chunk at a time, sem_velocity_blocks' col_begin/col_end) gives the solve of
+    the one-shot factorisation."""
+    ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
+
+    def fill(blocks, cols):   # the kernel's contract: A_II of columns cols, every other piece in full
+        c0, c1 = cols
+        for k in ("D", "aIB", "aBI", "E", "F"):
+            blocks[k].copy_(pcs[k])
+        blocks["AII"].copy_(pcs["AII"][c0:c1])
+
+    one = VelocityJacobianSolver(P, nex, ney, "cpu")
+    one.factor(pcs["AII"].clone(), pcs["D"], pcs["aIB"], pcs["aBI"], pcs["E"], pcs["F"])
+    ch = VelocityJacobianSolver(P, nex, ney, "cpu")
+    nI, m = ch.nI, ch.m
+    ch.factor_from(fill, budget_bytes=chunk_cols * (nI * nI * 8 + 3 * nI * 2 * m * 8))
+    r = np.random.default_rng(9)
+    bu, bv = (torch.as_tensor(r.uniform(-1, 1, ns.N)) for _ in range(2))
+    want = spla.spsolve(ns.Jvelo.tocsc(), np.hstack((bu.numpy(), bv.numpy())))
+    for s in (ch, one):   # the same factor up to the summation order of the interface blocks
+        got = np.hstack([t.numpy() for t in s.solve(bu, bv)])
+        assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
