@@ -89,11 +89,17 @@ class ConvectionDiffusionSolver:
     def __init__(self, L_x: float, L_y: float, Pe: float, P: int, N_ex: int, N_ey: int,
                  T_W: float = None, T_E: float = None, T_S: float = None, T_N: float = None,
                  mtol=1e-7, iprint: list = [], krylov: str = "device", max_basis: int = 2000,  # noqa: B006
-                 partition=None, recycle_bytes: float = 0.0, precond: str = "condensed"):
+                 partition=None, recycle_bytes: float = 0.0, precond: str = "condensed",
+                 partition_update: str = "distributed"):
         """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip
         per rank, every apply ends with the interface exchange (overlapped with the interior) and
         the Krylov inner products are all-reduced; the reference methods still take and return
-        global NumPy vectors (local strips when given device tensors)."""
+        global NumPy vectors (local strips when given device tensors).
+        partition_update: how a partitioned solver solves its Newton update -- "distributed": the
+        device GMRES over the strips (every matvec a strip apply + exchange, inner products
+        all-reduced; unpreconditioned, as there is no whole-mesh factor); "central": the Sys velocity
+        field and the right-hand side are gathered, rank 0's whole-mesh counterpart
+        (_central_solver) solves with the condensed direct preconditioner, the update is broadcast."""
         if krylov not in ("device", "scipy"):
             raise ValueError("krylov must be 'device' or 'scipy'")
         if partition is not None and krylov != "device":
@@ -102,6 +108,12 @@ class ConvectionDiffusionSolver:
             raise ValueError("precond must be 'condensed' or None")
         # the condensation needs the whole mesh on one device; a partitioned solver runs plain GMRES
         self._precond = precond if partition is None else None
+        if partition_update not in ("distributed", "central"):
+            raise ValueError("partition_update must be 'distributed' or 'central'")
+        self._partition_update = partition_update
+        self._args = dict(L_x=L_x, L_y=L_y, Pe=Pe, P=P, N_ex=N_ex, N_ey=N_ey, T_W=T_W, T_E=T_E, T_S=T_S, T_N=T_N,
+                          mtol=mtol, iprint=iprint, max_basis=max_basis, precond=precond)
+        self._twin, self._sys_uv, self._twin_stale = None, None, True
         self._factor = None     # condensed Jacobian of the current Sys (rebuilt after _get_residuals)
         self._krylov, self._max_basis = krylov, max_basis
         self._part = partition
@@ -167,6 +179,8 @@ class ConvectionDiffusionSolver:
         Conv = self._Pe * (SEM.tensordot(self._C_x, self._dev(u), (1, 0)) + SEM.tensordot(self._C_y, self._dev(v), (1, 0)))
         self._Sys = Conv + self._K
         self._factor = None
+        if self._part is not None:
+            self._sys_uv, self._twin_stale = (self._dev(u), self._dev(v)), True
         if self._recycle is not None:   # the update operator depends on Sys
             self._recycle.reset()
         y = self._apply(self._dev(T), dir_mode=_lib.DIR_IDENTITY, dir_val=self._dir_val, **self._sys_kw(),
@@ -199,6 +213,8 @@ class ConvectionDiffusionSolver:
 
     def _get_update(self, dres, dT0=None):
         """Newton update: solve dres_op(dT) = dres (ConvectionDiffusion_Solver.py:123-156)."""
+        if self._part is not None and self._partition_update == "central":
+            return self._get_update_central(dres, dT0)
         if self._krylov == "device":
             return self._get_update_device(dres, dT0)
         return self._get_update_scipy(dres, dT0)
@@ -259,6 +275,41 @@ class ConvectionDiffusionSolver:
             res = (self._get_dresiduals(r.x) - b).abs().max().item()
             print(f"ConvectionDiffusion GMRES: Converged in {r.matvecs} evaluations with max-norm {res}")
         return self._out(r.x, dres)
+
+    def _central_solver(self):
+        """Rank 0's whole-mesh counterpart for partition_update="central" (same arguments, no
+        partition)."""
+        return ConvectionDiffusionSolver(**self._args)
+
+    def _global(self, a):
+        if isinstance(a, torch.Tensor):
+            return self._part.gather(a).cpu().numpy()
+        return np.asarray(a, dtype=np.float64)
+
+    def _get_update_central(self, dres, dT0=None):
+        """The partitioned solver's update on rank 0's whole-mesh counterpart: its Sys is set from
+        the gathered velocity field of the last _get_residuals (the reference interface), it solves
+        with the condensed direct preconditioner, and the update is broadcast to every rank."""
+        part = self._part
+        if self._sys_uv is None:
+            raise RuntimeError("ConvectionDiffusion: _get_residuals must run before _get_update")
+        if self._twin_stale:
+            u, v = (self._global(a) for a in self._sys_uv)
+            if part.rank == 0:
+                if self._twin is None:
+                    self._twin = self._central_solver()
+                self._twin._get_residuals(np.zeros(self.N), u, v)
+            self._twin_stale = False
+        b = self._global(dres)
+        x0 = None if dT0 is None else self._global(dT0)
+        out = torch.zeros(self.N + 1, dtype=torch.float64)
+        if part.rank == 0:
+            out[:self.N] = torch.from_numpy(np.asarray(self._twin._get_update(b, dT0=x0)))
+            out[-1] = float(getattr(self._twin, "matvecs", -1))
+        out = part.broadcast(out)
+        self.matvecs = int(out[-1].item())
+        dT = out[:self.N].cpu().numpy()
+        return self._dev(dT) if isinstance(dres, torch.Tensor) else dT
 
     def _get_update_scipy(self, dres, dT0=None):
         """The reference's LGMRES on the host around device matvecs."""

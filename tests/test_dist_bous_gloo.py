@@ -77,7 +77,7 @@ def test_parallel_coupler_matches_sequential(mode):
     assert calls0["cd_update"] == calls1["ns_update"] > 0 or mode == "JNK" and it0 == 0
 
 
-def _worker_partitioned(rank, world, port, key, q):
+def _worker_partitioned(rank, world, port, key, q, cd_update="central"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.dirname(here), here]
@@ -86,14 +86,15 @@ def _worker_partitioned(rank, world, port, key, q):
     try:
         from conftest import golden
         from cpu_mesh import CPUStripMesh
-        from oracle_solvers import OracleNS
+        from oracle_solvers import OracleCD, OracleNS
         from sem_amd.solvers.boussinesq import partitioned_coupler
         g = golden("bous.npz")
         Pc, nxc, nyc, Pn, nxn, nyn = (int(a) for a in g[key + "_cfg"])
         Re, Ra, Pr = 1e3, 1e3, 0.71
         c = partitioned_coupler(dist, 1.0, 1.0, Re, Ra, Pr, Pc, nxc, nyc, Pn, nxn, nyn, mesh_factory=CPUStripMesh,
-                                mode=str(g[key + "_mode"]))
+                                mode=str(g[key + "_mode"]), cd_update=cd_update)
         c.ns._central_solver = lambda: OracleNS(1.0, 1.0, Re, Ra / Pr, Pn, nxn, nyn, mtol=1e-13, mtol_newton=1e-13)
+        c.cd._central_solver = lambda: OracleCD(1.0, 1.0, Re * Pr, Pc, nxc, nyc, T_W=0.5, T_E=-0.5, mtol=1e-13)
         R = c.residuals(g[key + "_x"])
         c.linearize(g[key + "_x"])
         JR = c.jacobian_apply(g[key + "_dx"])
@@ -103,8 +104,8 @@ def _worker_partitioned(rank, world, port, key, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,key", [(2, "a"), (2, "c")])
-def test_element_partitioned_coupler(world, key):
+@pytest.mark.parametrize("world,key,cd_update", [(2, "a", "central"), (2, "c", "central"), (2, "a", "distributed")])
+def test_element_partitioned_coupler(world, key, cd_update):
     """cfg5's structure at the golden's size: both solvers strip-partitioned over `world` ranks
     (partitioned_coupler), against the reference solver classes driven through the same coupling
     (tests/golden/bous.npz): coupled residual / Jacobian apply to 1e-12, the same Newton count, the
@@ -117,7 +118,7 @@ def test_element_partitioned_coupler(world, key):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_partitioned, args=(r, world, port, key, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_partitioned, args=(r, world, port, key, q, cd_update)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=600) for _ in range(world)]

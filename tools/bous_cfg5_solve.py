@@ -1,0 +1,79 @@
+"""BASELINE cfg5 end to end: the element-partitioned Boussinesq coupler (both solvers strip-partitioned
+over the ranks, sem_amd.solvers.boussinesq.partitioned_coupler), 128 x 128 elements, P = 12, JNK from
+rest at the given Ra.  Rank 0 also holds the whole-mesh counterparts that solve the Newton updates.
+
+  torchrun --nproc-per-node N tools/bous_cfg5_solve.py [--Ra 1e3]                  # RCCL, one GPU per rank
+  torchrun --nproc-per-node N tools/bous_cfg5_solve.py --backend gloo              # N ranks on one GPU
+Prints the Newton history and one JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ne", type=int, default=128)
+    ap.add_argument("--P", type=int, default=12)
+    ap.add_argument("--Ra", type=float, default=1e3)
+    ap.add_argument("--mode", default="JNK")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    if "RANK" not in os.environ:
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29534")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local % torch.cuda.device_count() if args.backend == "nccl" else 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group(args.backend)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    from sem_amd.solvers.boussinesq import partitioned_coupler
+    Re, Pr = 1e3, 0.71
+    c = partitioned_coupler(dist, 1.0, 1.0, Re, args.Ra, Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
+                            mode=args.mode, iprint=2 if rank == 0 else 0)
+    make_ns, make_cd = c.ns._central_solver, c.cd._central_solver
+
+    def central_ns():   # progress lines from rank 0's whole-mesh solves (long Krylov solves at this size)
+        t = make_ns()
+        t._progress, t._iprint = 250, ["LU_suc"]
+        return t
+
+    def central_cd():
+        t = make_cd()
+        t._progress = 250
+        return t
+
+    c.ns._central_solver, c.cd._central_solver = central_ns, central_cd
+    t0 = time.perf_counter()
+    T, u, v, p = c.solve()
+    dt = time.perf_counter() - t0
+    if rank == 0:
+        s = np.linspace(0.0, 1.0, 1001)
+        um = np.asarray(c.ns._get_interpol(u, np.meshgrid([0.5], s, indexing="ij")))[0] * Re * Pr
+        vm = np.asarray(c.ns._get_interpol(v, np.meshgrid(s, [0.5], indexing="ij")))[:, 0] * Re * Pr
+        out = {"config": f"cfg5 element-partitioned Boussinesq {args.mode} Ra={args.Ra:g}, {args.ne}x{args.ne} P={args.P}",
+               "ranks": world, "backend": args.backend, "DOF": int(c.DOF), "newton_iters": c.iterations,
+               "seconds": dt, "timing": c.timing, "calls": c.calls,
+               "u_max_midline": float(um.max()), "u_max_y": float(s[um.argmax()]),
+               "v_max_midline": float(vm.max()), "v_max_x": float(s[vm.argmax()]),
+               "residual_2norm": float(np.linalg.norm(c.residuals(np.concatenate([T, u, v, p])))),
+               "tolerance": float(c.atol_nonlin), "device": torch.cuda.get_device_name(dev)}
+        print(json.dumps(out), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(out, f)
+    else:
+        c.residuals(np.concatenate([T, u, v, p]))   # the residual check is collective
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
