@@ -26,6 +26,8 @@ import torch
 
 from ..device import no_gc
 
+GEMV_LDS_DOUBLES = 8192   # sem_block_gemv stages S m operand doubles in LDS (include/sem_ops.h)
+
 
 def batched_inverse(A):
     """torch.linalg.inv of a batch of blocks.  The batched rocSOLVER getrf behind it has been seen
@@ -288,6 +290,15 @@ class VelocityJacobianSolver:
                     and xrow.dtype == yrow.dtype == torch.int64 and tuple(M.shape) == (yrow.numel(), m, S * m)
                     and tuple(xrow.shape) == (S, yrow.numel())):
                 raise ValueError("sem_block_gemv: operator / index layout")
+            if S * m > GEMV_LDS_DOUBLES:   # operands beyond the kernel's LDS staging (cfg5: m = 3074): batched GEMV
+                rhs = torch.cat([torch.where((r >= 0)[:, None], t[r.clamp(min=0)], 0.0) for t, r in zip(srcs, xrow)],
+                                dim=1)
+                out = torch.bmm(M, rhs[..., None])[..., 0]
+                if acc:
+                    y[yrow] += out
+                else:
+                    y[yrow] = out
+                return
             src = (P * S)(*(P(t.data_ptr()) for t in srcs))
             ld = (C.c_int64 * S)(*(t.stride(0) for t in srcs))
             _lib.check(lib.sem_block_gemv(yrow.numel(), m, S, P(M.data_ptr()), src, ld, P(xrow.data_ptr()),

@@ -200,3 +200,22 @@ def test_column_ranged_blocks_and_chunked_factor(gpu, P, nex, ney, Re):
     got = np.hstack((xu.cpu().numpy(), xv.cpu().numpy()))
     want = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
     assert np.abs(got - want).max() <= 1e-9 * np.abs(want).max()
+
+
+def test_interface_sweep_batched_gemv_fallback(gpu, monkeypatch):
+    """Interface blocks too wide for sem_block_gemv's LDS staging (S m > 8192 doubles: cfg5's
+    m = 2 N_y = 3074 with three operands) go through a batched GEMV; forced here on a small mesh, the
+    solve equals the HIP-kernel sweep's."""
+    from sem_amd.solvers import velocity_solve as VS
+    P, nex, ney, Re = 4, 8, 3, 700.0
+    ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    ns = _device_solver(P, nex, ney, Re, u, v)
+    ns._velocity_graph = False
+    vs = ns._velocity_solver()
+    r = np.random.default_rng(3)
+    bu, bv = ns._dev(r.uniform(-1, 1, ns.N)), ns._dev(r.uniform(-1, 1, ns.N))
+    want = [t.clone() for t in vs.solve(bu, bv)]
+    monkeypatch.setattr(VS, "GEMV_LDS_DOUBLES", 1)
+    got = vs.solve(bu, bv)
+    for a, b in zip(got, want):
+        assert torch.abs(a - b).max() <= 1e-12 * torch.abs(b).max()

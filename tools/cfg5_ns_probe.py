@@ -49,6 +49,7 @@ def main():
     out["factor_peak_GB"] = torch.cuda.max_memory_allocated(dev) / 1e9
     out["interior_dense_GB_one_shot"] = vs.interior_bytes() / 1e9
     out["resident_GB"] = torch.cuda.memory_allocated(dev) / 1e9
+    print(json.dumps(out), flush=True)
     r = np.random.default_rng(7)
     bu, bv = (ns._dev(r.uniform(-1, 1, N)) for _ in range(2))
     xu, xv = vs.solve(bu, bv)
@@ -61,6 +62,7 @@ def main():
     ju, jv, _ = ns._get_dresiduals(xu, xv, torch.zeros_like(xu))
     out["velocity_solve_rel_residual"] = float(max((ju - bu).abs().max(), (jv - bv).abs().max()) /
                                              max(bu.abs().max(), bv.abs().max()))
+    print(json.dumps(out), flush=True)
     del vs_tmp
     if args.update:
         t0 = time.perf_counter()
