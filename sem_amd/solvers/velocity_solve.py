@@ -89,7 +89,7 @@ class VelocityJacobianSolver:
         """Bytes of the dense A_II blocks of the whole mesh."""
         return self.nex * self.nI * self.nI * 8
 
-    def factor_from(self, fill, budget_bytes=48 << 30):
+    def factor_from(self, fill, budget_bytes=24 << 30):
         """Assemble and factor.  fill(blocks, cols) writes the pieces (sem_velocity_blocks) with
         blocks["AII"] holding the dense interiors of element columns cols = (c0, c1).  When the whole
         mesh's A_II fits in budget_bytes this is one fill + factor(); otherwise (cfg5: 1.17 TB of
