@@ -29,11 +29,8 @@ from ..device import no_gc
 GEMV_LDS_DOUBLES = 8192   # sem_block_gemv stages S m operand doubles in LDS (include/sem_ops.h)
 
 
-def batched_inverse(A):
-    """torch.linalg.inv of a batch of blocks.  The batched rocSOLVER getrf behind it has been seen
-    to fail its workspace allocation for some (n, batch) shapes (64 blocks of 455^2 on MI355X,
-    HIPBLAS_STATUS_ALLOC_FAILED) where smaller batches go through: on that error the batch is
-    inverted in chunks, halving down to single blocks.  The result is the same either way."""
+def _inverse(A):
+    """torch.linalg.inv of a batch; on a getrf workspace-allocation failure the batch is halved."""
     try:
         return torch.linalg.inv(A)
     except RuntimeError as e:
@@ -42,7 +39,41 @@ def batched_inverse(A):
     out = torch.empty_like(A)
     step = max(1, A.shape[0] // 2)
     for i in range(0, A.shape[0], step):
-        out[i:i + step] = batched_inverse(A[i:i + step])
+        out[i:i + step] = _inverse(A[i:i + step])
+    return out
+
+
+def _bad_blocks(A, X, tol=1e-6):
+    """Blocks whose computed inverse misses: max |A X - I| above tol (a right inverse is O(cond eps))."""
+    E = A @ X
+    E.diagonal(dim1=-2, dim2=-1).sub_(1.0)
+    return torch.nonzero(E.abs().amax(dim=(-2, -1)) > tol).flatten()
+
+
+def batched_inverse(A, max_batch=128):
+    """Inverses of a batch of blocks (rocSOLVER getrf/getri through torch), checked.
+
+    Measured on MI355X (tools/chunk_probe.py, profiles/r02/cfg5/chunk_probe.txt): the batched
+    inverse returns wrong blocks, without an error, for some shapes -- 121^2 blocks (the one-component
+    element interiors at P = 12) in batches of 384 and more -- and has been seen to fail its workspace
+    allocation for others (64 blocks of 455^2).  So the batch is inverted in slices of max_batch blocks,
+    every block is checked through its residual A X - I, and a block that misses is inverted again on
+    its own (then by a solve against the identity) before giving up."""
+    if A.dim() < 3:
+        return torch.linalg.inv(A)
+    out = torch.empty_like(A)
+    for i in range(0, A.shape[0], max_batch):
+        a = A[i:i + max_batch]
+        x = _inverse(a)
+        for j in _bad_blocks(a, x).tolist():
+            xj = torch.linalg.inv(a[j])
+            if _bad_blocks(a[j:j + 1], xj[None]).numel():
+                eye = torch.eye(a.shape[-1], dtype=a.dtype, device=a.device)
+                xj = torch.linalg.solve(a[j], eye)
+                if _bad_blocks(a[j:j + 1], xj[None]).numel():
+                    raise RuntimeError("velocity solve: an interior block could not be inverted accurately")
+            x[j] = xj
+        out[i:i + max_batch] = x
     return out
 
 

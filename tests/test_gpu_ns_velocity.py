@@ -86,7 +86,8 @@ def test_ns_update_matches_oracle_update(gpu):
         assert np.abs(a - b).max() <= 1e-6 * max(1.0, np.abs(b).max())
 
 
-@pytest.mark.parametrize("P,nex,ney,Pe", [(4, 3, 2, 40.0), (8, 4, 4, 710.0), (1, 4, 3, 10.0), (5, 3, 6, 250.0)])
+@pytest.mark.parametrize("P,nex,ney,Pe", [(4, 3, 2, 40.0), (8, 4, 4, 710.0), (1, 4, 3, 10.0), (5, 3, 6, 250.0),
+                                           (12, 3, 2, 710.0), (12, 2, 5, 40.0)])
 def test_scalar_blocks_and_solve_match_oracle_cd_jacobian(gpu, P, nex, ney, Pe):
     """ncomp=1 (the CD solver's preconditioner): sem_velocity_blocks writes the pieces of the
     oracle's Dirichlet-row-replaced CD Jacobian, and the condensed solve matches SciPy's."""
@@ -112,7 +113,8 @@ def test_scalar_blocks_and_solve_match_oracle_cd_jacobian(gpu, P, nex, ney, Pe):
         cd._mesh.velocity_blocks(blocks, c_stiff=1.0, juv=cd._dev(b), ncomp=1)
 
 
-@pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 2, 100.0), (8, 4, 4, 1000.0), (5, 3, 6, 250.0), (2, 7, 2, 300.0)])
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 2, 100.0), (8, 4, 4, 1000.0), (5, 3, 6, 250.0), (2, 7, 2, 300.0),
+                                           (12, 3, 2, 1000.0), (12, 2, 5, 100.0)])
 def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     """sem_nested_solve + sem_interface_rhs (ns_condense.hip) against the torch formulation of the
     same condensation, for the velocity pair and the one-component CD Jacobian."""
@@ -136,7 +138,8 @@ def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     assert (y_hip - y_torch).abs().max().item() <= 1e-12 * y_torch.abs().max().item()
 
 
-@pytest.mark.parametrize("nb,m,S", [(1, 770, 3), (2, 385, 2), (40, 200, 3), (24, 770, 2), (3, 17, 1)])
+@pytest.mark.parametrize("nb,m,S", [(1, 770, 3), (2, 385, 2), (40, 200, 3), (24, 770, 2), (3, 17, 1), (5, 1537, 3),
+                                    (4, 1537, 2), (1, 2730, 3)])
 def test_block_gemv_wide_and_narrow(gpu, nb, m, S):
     """sem_block_gemv (both launch forms: wide 16-row workgroups for big levels, narrow one-row-per-wave
     for the last cyclic-reduction levels) against torch, with absent operands and accumulation."""
