@@ -4,7 +4,7 @@
 # counterparts that solve the Newton updates).
 set -o pipefail
 O=gpurun_out/r02c5; mkdir -p $O
-timeout -k 10 1100 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29614 \
+timeout -k 10 800 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29614 \
   tools/bous_cfg5_solve.py --backend gloo --Ra 1e3 --out $O/cfg5_ra1e3.json > $O/cfg5.log 2>&1; rc=$?
 grep -v "GMRES: [0-9]" $O/cfg5.log | tail -8 | cut -c1-700
 exit $rc
