@@ -16,6 +16,7 @@ Schur-complement Krylov solve with the mass-diagonal preconditioner (NavierStoke
 lines (sem_amd/solvers/velocity_solve.py, blocks written by the sem_velocity_blocks HIP kernel)
 instead of host SuperLU, and the Schur system runs the device GMRES.  No CSR matrix is formed.
 """
+import gc
 import time
 
 import numpy as np
@@ -280,6 +281,9 @@ class NavierStokesSolver:
             return self._velo
         tStart = time.perf_counter()
         m = self._mesh
+        if self.N > 1_000_000:   # the previous linearisation's factor and graphs go before the next one
+            gc.collect()
+            torch.cuda.empty_cache()
         vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior,
                                     sweep=self._velocity_sweep)
         vs.factor_from(lambda b, cols: m.velocity_blocks(b, cols=cols, dir_mask=self._dir.mask,
@@ -360,7 +364,9 @@ class NavierStokesSolver:
             if 'LGMRES_iter' in self._iprint or (prog and it[0] % prog == 0):
                 print(f'NavierStokes GMRES: {it[0]}\t{est}', flush=True)
 
-        restart = max(1, min(self.N, self._max_basis))
+        # the basis and its preconditioned images (2 restart N doubles) within 32 GB: unrestarted up to
+        # max_basis on the configurations of record, restarted at ~420 vectors at cfg5 (N = 2.36 M)
+        restart = max(1, min(self.N, self._max_basis, int(32e9 // (16 * self.N))))
         if self._recycle_bytes and self._schur_recycle is None:
             cap = min(self.N, max(restart + 1, int(self._recycle_bytes // (16 * self.N))))
             self._schur_recycle = Recycle(self.N, torch.float64, self._mesh.device, cap)
