@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--Ra", type=float, default=1e3)
     ap.add_argument("--mode", default="JNK")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--continuation", default="", help="Ra stages before --Ra (each starts from the last)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     if "RANK" not in os.environ:
@@ -35,43 +36,53 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group(args.backend)
     rank, world = dist.get_rank(), dist.get_world_size()
+    import gc
+
     from sem_amd.solvers.boussinesq import partitioned_coupler
     Re, Pr = 1e3, 0.71
-    c = partitioned_coupler(dist, 1.0, 1.0, Re, args.Ra, Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
-                            mode=args.mode, iprint=2 if rank == 0 else 0)
-    make_ns, make_cd = c.ns._central_solver, c.cd._central_solver
+    x, stages = None, []
+    for Ra in [float(r) for r in args.continuation.split(",") if r] + [args.Ra]:
+        c = partitioned_coupler(dist, 1.0, 1.0, Re, Ra, Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
+                                mode=args.mode, iprint=2 if rank == 0 else 0)
+        make_ns, make_cd = c.ns._central_solver, c.cd._central_solver
 
-    def central_ns():   # progress lines from rank 0's whole-mesh solves (long Krylov solves at this size)
-        t = make_ns()
-        t._progress, t._iprint = 250, ["LU_suc"]
-        return t
+        def central_ns(make_ns=make_ns):   # progress lines from rank 0's whole-mesh solves
+            t = make_ns()
+            t._progress, t._iprint = 250, ["LU_suc"]
+            return t
 
-    def central_cd():
-        t = make_cd()
-        t._progress = 250
-        return t
+        def central_cd(make_cd=make_cd):
+            t = make_cd()
+            t._progress = 250
+            return t
 
-    c.ns._central_solver, c.cd._central_solver = central_ns, central_cd
-    t0 = time.perf_counter()
-    T, u, v, p = c.solve()
-    dt = time.perf_counter() - t0
+        c.ns._central_solver, c.cd._central_solver = central_ns, central_cd
+        t0 = time.perf_counter()
+        T, u, v, p = c.solve(x)
+        dt = time.perf_counter() - t0
+        x = np.concatenate([T, u, v, p])
+        res = float(np.linalg.norm(c.residuals(x)))   # collective
+        if rank == 0:
+            s = np.linspace(0.0, 1.0, 1001)
+            um = np.asarray(c.ns._get_interpol(u, np.meshgrid([0.5], s, indexing="ij")))[0] * Re * Pr
+            vm = np.asarray(c.ns._get_interpol(v, np.meshgrid(s, [0.5], indexing="ij")))[:, 0] * Re * Pr
+            st = {"Ra": Ra, "newton_iters": c.iterations, "seconds": dt, "timing": c.timing, "calls": c.calls,
+                  "u_max_midline": float(um.max()), "u_max_y": float(s[um.argmax()]),
+                  "v_max_midline": float(vm.max()), "v_max_x": float(s[vm.argmax()]),
+                  "residual_2norm": res, "tolerance": float(c.atol_nonlin)}
+            stages.append(st)
+            print(json.dumps(st), flush=True)
+        del c
+        gc.collect()
+        torch.cuda.empty_cache()
     if rank == 0:
-        s = np.linspace(0.0, 1.0, 1001)
-        um = np.asarray(c.ns._get_interpol(u, np.meshgrid([0.5], s, indexing="ij")))[0] * Re * Pr
-        vm = np.asarray(c.ns._get_interpol(v, np.meshgrid(s, [0.5], indexing="ij")))[:, 0] * Re * Pr
         out = {"config": f"cfg5 element-partitioned Boussinesq {args.mode} Ra={args.Ra:g}, {args.ne}x{args.ne} P={args.P}",
-               "ranks": world, "backend": args.backend, "DOF": int(c.DOF), "newton_iters": c.iterations,
-               "seconds": dt, "timing": c.timing, "calls": c.calls,
-               "u_max_midline": float(um.max()), "u_max_y": float(s[um.argmax()]),
-               "v_max_midline": float(vm.max()), "v_max_x": float(s[vm.argmax()]),
-               "residual_2norm": float(np.linalg.norm(c.residuals(np.concatenate([T, u, v, p])))),
-               "tolerance": float(c.atol_nonlin), "device": torch.cuda.get_device_name(dev)}
+               "ranks": world, "backend": args.backend, "DOF": int(x.size), "stages": stages,
+               "device": torch.cuda.get_device_name(dev)}
         print(json.dumps(out), flush=True)
         if args.out:
             with open(args.out, "w") as f:
                 json.dump(out, f)
-    else:
-        c.residuals(np.concatenate([T, u, v, p]))   # the residual check is collective
     dist.destroy_process_group()
 
 
