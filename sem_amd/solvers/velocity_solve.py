@@ -43,11 +43,16 @@ def _inverse(A):
     return out
 
 
-def _bad_blocks(A, X, tol=1e-6):
-    """Blocks whose computed inverse misses: max |A X - I| above tol (a right inverse is O(cond eps))."""
+def _bad_blocks(A, X):
+    """Blocks whose computed inverse misses: max |A X - I| above max(1e-6, 1e-12 n |A|max |X|max).  A
+    backward-stable inverse leaves a residual of order n eps |A| |X| (at most ~1e-13 n |A| |X|), so the
+    bound accepts ill-conditioned blocks and rejects the O(1) residual of a wrong one."""
     E = A @ X
     E.diagonal(dim1=-2, dim2=-1).sub_(1.0)
-    return torch.nonzero(E.abs().amax(dim=(-2, -1)) > tol).flatten()
+    n = A.shape[-1]
+    scale = A.abs().amax(dim=(-2, -1)) * X.abs().amax(dim=(-2, -1))
+    tol = torch.clamp(1e-12 * n * scale, min=1e-6)
+    return torch.nonzero(~(E.abs().amax(dim=(-2, -1)) <= tol)).flatten()
 
 
 def batched_inverse(A, max_batch=128):
