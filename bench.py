@@ -200,14 +200,21 @@ def cpu_baseline(P, ne, Pe, seconds):
                       f"(oracle/sem_oracle.py restatement of ConvectionDiffusion_Solver.py:85-87,112-119)"}
 
 
-def load_pmc(workload):
-    """HBM traffic per launch measured with rocprofv3 PMC passes (profiles/pmc_traffic.json)."""
+def load_pmc(workload, kernel):
+    """HBM traffic per launch measured with rocprofv3 PMC passes (profiles/pmc_traffic.json, written by
+    tools/pmc_traffic.py), and the exact kernel instantiation it was measured on; only an entry measured
+    on the kernel family this run launches (kernel_name() plus its template flags) is used."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get(workload, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get("workloads", {}).get(workload, {})
     except (OSError, ValueError):
-        return None
+        return None, None
+    k = e.get("kernel", "")
+    fam = kernel[:-1] if kernel.endswith(">") else kernel
+    if not (k == kernel or k.startswith(fam + ",")):
+        return None, None
+    return e.get("hbm_bytes_per_launch"), k
 
 
 def main():
@@ -287,6 +294,7 @@ def main():
     g1000_us = graph_kernel_us(apply_only, dev)
     achieved = bytes_launch / kern_s / 1e9
     workload = f"cd_matvec_{ne}x{ne}_P{P}"
+    traffic, traffic_kernel = load_pmc(workload, mesh.kernel_name())
     out = {
         "metric": BASELINE_METRIC,
         "work": "y = K T + Pe (u.Gx T + v.Gy T), Dirichlet identity rows on x=0,1: the Laplacian+convection "
@@ -307,7 +315,7 @@ def main():
                        if world > 1 else ""),
                    "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": use_graph},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_kernel": traffic_kernel,
                      "kernel": mesh.kernel_name(), "bytes_per_launch": bytes_launch,
                      "flops_per_launch": flops_launch, "kernel_us": kern_s * 1e6,
                      "kernel_us_from": "timed region / launches (HIP events on the launch stream)",
@@ -343,10 +351,12 @@ def main():
         kb = graph_kernel_us(lambda: big.apply(Tb, yb, **kwb), dev, launches=50, trials=3) * 1e-6
         bb = 32.0 * big.n_local
         wl = f"cd_matvec_{args.hbm_ne}x{args.hbm_ne}_P{P}"
+        tb, tbk = load_pmc(wl, big.kernel_name())
         out["roofline_hbm"] = {"workload": wl, "kernel": big.kernel_name(), "dofs": big.n_local,
                                "value": big.n_local / kb, "unit": "DOF-updates/s",
                                "bound": "hbm", "achieved": bb / kb / 1e9, "peak": HBM_PEAK_GBS, "unit_bw": "GB/s",
-                               "frac": bb / kb / 1e9 / HBM_PEAK_GBS, "traffic": load_pmc(wl), "kernel_us": kb * 1e6}
+                               "frac": bb / kb / 1e9 / HBM_PEAK_GBS, "traffic": tb, "traffic_kernel": tbk,
+                               "kernel_us": kb * 1e6}
         del Tb, ub, vb, yb
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -293,20 +293,30 @@ class ConvectionDiffusionSolver:
         part = self._part
         if self._sys_uv is None:
             raise RuntimeError("ConvectionDiffusion: _get_residuals must run before _get_update")
-        if self._twin_stale:
+        stale = self._twin_stale
+        if stale:
             u, v = (self._global(a) for a in self._sys_uv)
-            if part.rank == 0:
-                if self._twin is None:
-                    self._twin = self._central_solver()
-                self._twin._get_residuals(np.zeros(self.N), u, v)
             self._twin_stale = False
         b = self._global(dres)
         x0 = None if dT0 is None else self._global(dT0)
         out = torch.zeros(self.N + 1, dtype=torch.float64)
+        err = None
         if part.rank == 0:
-            out[:self.N] = torch.from_numpy(np.asarray(self._twin._get_update(b, dT0=x0)))
-            out[-1] = float(getattr(self._twin, "matvecs", -1))
+            try:   # a rank-0 failure is broadcast as a NaN status: every rank raises, none waits
+                if stale:
+                    if self._twin is None:
+                        self._twin = self._central_solver()
+                    self._twin._get_residuals(np.zeros(self.N), u, v)
+                out[:self.N] = torch.from_numpy(np.asarray(self._twin._get_update(b, dT0=x0)))
+                out[-1] = float(getattr(self._twin, "matvecs", -1))
+            except (RuntimeError, ValueError) as e:
+                err = e
+                out[-1] = float("nan")
         out = part.broadcast(out)
+        if err is not None:
+            raise err
+        if torch.isnan(out[-1]):
+            raise RuntimeError("ConvectionDiffusion: the update failed on rank 0 (see its error)")
         self.matvecs = int(out[-1].item())
         dT = out[:self.N].cpu().numpy()
         return self._dev(dT) if isinstance(dres, torch.Tensor) else dT

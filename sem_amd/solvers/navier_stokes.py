@@ -247,24 +247,36 @@ class NavierStokesSolver:
         lin = self._lin
         if lin is None:
             raise RuntimeError("NavierStokes: _calc_jacobians must run before _get_update")
-        if lin.get("stale"):
+        stale = lin.get("stale")
+        if stale:
             us, vs = (self._global(a) for a in lin["sys"])
             uj, vj = (self._global(a) for a in lin["jac"])
-            if part.rank == 0:
-                if self._twin is None:
-                    self._twin = self._central_solver()
-                z = np.zeros(self.N)
-                self._twin._get_residuals(us, vs, z, z)
-                self._twin._calc_jacobians(uj, vj)
             lin["stale"] = False
         rhs = [self._global(a) for a in (dres_u, dres_v, dres_cont)]
         x0 = [None if a is None else self._global(a) for a in (du0, dv0, dp0)]
         out = torch.zeros(3 * self.N + 1, dtype=torch.float64)
+        err = None
         if part.rank == 0:
-            d = self._twin._get_update(*rhs, du0=x0[0], dv0=x0[1], dp0=x0[2])
-            out[:3 * self.N] = torch.from_numpy(np.concatenate([np.asarray(a) for a in d]))
-            out[-1] = float(getattr(self._twin, "schur_matvecs", -1))
+            # a failure on rank 0 (non-convergence, a singular block, out of memory) travels in the
+            # broadcast as a NaN status, so every rank raises instead of waiting in the collective
+            try:
+                if stale:
+                    if self._twin is None:
+                        self._twin = self._central_solver()
+                    z = np.zeros(self.N)
+                    self._twin._get_residuals(us, vs, z, z)
+                    self._twin._calc_jacobians(uj, vj)
+                d = self._twin._get_update(*rhs, du0=x0[0], dv0=x0[1], dp0=x0[2])
+                out[:3 * self.N] = torch.from_numpy(np.concatenate([np.asarray(a) for a in d]))
+                out[-1] = float(getattr(self._twin, "schur_matvecs", -1))
+            except (RuntimeError, ValueError) as e:
+                err = e
+                out[-1] = float("nan")
         out = part.broadcast(out)
+        if err is not None:
+            raise err
+        if torch.isnan(out[-1]):
+            raise RuntimeError("NavierStokes: the update failed on rank 0 (see its error)")
         self.schur_matvecs = int(out[-1].item())
         d = [out[i * self.N:(i + 1) * self.N].cpu().numpy() for i in range(3)]
         if isinstance(dres_u, torch.Tensor):
@@ -364,8 +376,10 @@ class NavierStokesSolver:
             if 'LGMRES_iter' in self._iprint or (prog and it[0] % prog == 0):
                 print(f'NavierStokes GMRES: {it[0]}\t{est}', flush=True)
 
-        # the basis and its preconditioned images (2 restart N doubles) within 32 GB: unrestarted up to
-        # max_basis on the configurations of record, restarted at ~420 vectors at cfg5 (N = 2.36 M)
+        # the basis and its preconditioned images (2 restart N doubles = 16 N bytes per vector) within
+        # 32 GB: unrestarted up to max_basis on cfg3/cfg4, restarted at 846 vectors on a whole-mesh cfg5
+        # solver (N = 1537^2 = 2.36 M; 31.9 GB).  The velocity factor, the Schur graph's buffers and
+        # the Hessenberg matrix come on top of this budget.
         restart = max(1, min(self.N, self._max_basis, int(32e9 // (16 * self.N))))
         if self._recycle_bytes and self._schur_recycle is None:
             cap = min(self.N, max(restart + 1, int(self._recycle_bytes // (16 * self.N))))

@@ -22,6 +22,10 @@ Everything is device memory: cfg3 (32^2, P = 8) holds 3.3 GB of A_II factors, cf
 condensation itself is unit-tested on CPU against SciPy's sparse solve
 (tests/test_velocity_solve.py); the block assembly needs the GPU.
 """
+import contextlib
+import os
+import time
+
 import torch
 
 from ..device import no_gc
@@ -44,14 +48,16 @@ def _inverse(A):
 
 
 def _bad_blocks(A, X):
-    """Blocks whose computed inverse misses: max |A X - I| above max(1e-6, 1e-12 n |A|max |X|max).  A
-    backward-stable inverse leaves a residual of order n eps |A| |X| (at most ~1e-13 n |A| |X|), so the
-    bound accepts ill-conditioned blocks and rejects the O(1) residual of a wrong one."""
+    """Blocks whose computed inverse misses: max |A X - I| above 8 n^2 eps |A|max |X|max.  Entry (i, j)
+    of A X sums n products bounded by |A|max |X|max, so forming it rounds by at most n eps n |A| |X|,
+    and a backward-stable inverse adds an error of the same order: the bound is purely relative, it
+    accepts ill-conditioned blocks (large |A| |X|) and rejects a wrong inverse, whose residual is of
+    order |A| |X| itself."""
     E = A @ X
     E.diagonal(dim1=-2, dim2=-1).sub_(1.0)
     n = A.shape[-1]
     scale = A.abs().amax(dim=(-2, -1)) * X.abs().amax(dim=(-2, -1))
-    tol = torch.clamp(1e-12 * n * scale, min=1e-6)
+    tol = 8.0 * n * n * torch.finfo(A.dtype).eps * scale
     return torch.nonzero(~(E.abs().amax(dim=(-2, -1)) <= tol)).flatten()
 
 
@@ -108,6 +114,22 @@ class VelocityJacobianSolver:
         self.device = torch.device(device)
         self.interior = interior
         self.factored = False
+        # SEM_PROFILE_FACTOR=1: per-phase wall times of the factorisation (device-synchronised)
+        self.profile = os.environ.get("SEM_PROFILE_FACTOR", "") == "1"
+        self.timing = {}
+
+    @contextlib.contextmanager
+    def _phase(self, name):
+        if not self.profile:
+            yield
+            return
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        yield
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.timing[name] = self.timing.get(name, 0.0) + time.perf_counter() - t0
 
     # ------------------------------------------------------------------ assembly
     def empty_blocks(self, with_interior=True):
@@ -149,9 +171,10 @@ class VelocityJacobianSolver:
         S_diag = S_up = S_lo = None
         for c0 in range(0, nex, chunk):
             c1 = min(nex, c0 + chunk)
-            blocks["AII"] = torch.zeros((c1 - c0, self.nI, self.nI), **z)
-            fill(blocks, (c0, c1))
-            AII = blocks.pop("AII")
+            with self._phase("fill"):
+                blocks["AII"] = torch.zeros((c1 - c0, self.nI, self.nI), **z)
+                fill(blocks, (c0, c1))
+                AII = blocks.pop("AII")
             Xi[c0:c1], Yie[c0:c1], Aei[c0:c1], Sinv[c0:c1] = self._nested_pieces(AII)
             del AII
             if S_diag is None:   # every fill writes the line pieces in full: take them from the first
@@ -159,20 +182,23 @@ class VelocityJacobianSolver:
                 S_diag = blocks["D"].clone()
                 S_up, S_lo = torch.diag_embed(blocks["E"]), torch.diag_embed(blocks["F"])
             self._Xi, self._Yie, self._Aei, self._Se_inv = Xi, Yie, Aei, Sinv
-            AIB = torch.diag_embed(aIB[c0:c1]).permute(0, 1, 3, 2, 4).reshape(c1 - c0, self.nI, 2 * m)
-            W = self._nested_solve(AIB, slice(c0, c1))
-            del AIB
-            C = self._interface_coupling(aBI[c0:c1], W)
-            del W
-            S_diag[c0:c1] -= C[:, 0, :, 0, :]
-            S_diag[c0 + 1:c1 + 1] -= C[:, 1, :, 1, :]
-            S_up[c0:c1] -= C[:, 0, :, 1, :]
-            S_lo[c0:c1] -= C[:, 1, :, 0, :]
-            del C
+            with self._phase("W"):
+                AIB = torch.diag_embed(aIB[c0:c1]).permute(0, 1, 3, 2, 4).reshape(c1 - c0, self.nI, 2 * m)
+                W = self._nested_solve(AIB, slice(c0, c1))
+                del AIB
+            with self._phase("coupling"):
+                C = self._interface_coupling(aBI[c0:c1], W)
+                del W
+                S_diag[c0:c1] -= C[:, 0, :, 0, :]
+                S_diag[c0 + 1:c1 + 1] -= C[:, 1, :, 1, :]
+                S_up[c0:c1] -= C[:, 0, :, 1, :]
+                S_lo[c0:c1] -= C[:, 1, :, 0, :]
+                del C
         self._nested_finish()
         self.W = None
         self.aBI, self.aIB = aBI, aIB
-        self._sweep_factor(S_diag, S_up, S_lo)
+        with self._phase("sweep_factor"):
+            self._sweep_factor(S_diag, S_up, S_lo)
 
     def _interface_coupling(self, aBI, W):
         """C[e, s, r, t, k] = sum_l aBI[e, s, l, r] W[e, l, r, t, k]: A_BI A_II^-1 A_IB per column."""
@@ -378,19 +404,24 @@ class VelocityJacobianSolver:
         nex, ney = AII.shape[0], self.ney
         pi, pe, pel = self._pi, self._pe, self._pe_el
         e = torch.arange(nex, device=self.device)[:, None, None, None]
-        A_ii = AII[e, pi[None, :, :, None], pi[None, :, None, :]]     # (nex, ney, ni, ni)
-        A_ie = AII[e, pi[None, :, :, None], pel[None, :, None, :]]    # (nex, ney, ni, 2 ne1)
-        A_ei = AII[e, pel[None, :, :, None], pi[None, :, None, :]]    # (nex, ney, 2 ne1, ni)
-        S_e = AII[e[:, :, 0], pe[None, :, None], pe[None, None, :]]   # (nex, n_e, n_e)
-        Xi = batched_inverse(A_ii.reshape(-1, *A_ii.shape[-2:])).view(A_ii.shape)
-        Yie = Xi @ A_ie
-        C = (A_ei @ Yie).view(nex, ney, 2, self._ne1, 2, self._ne1)
-        S = S_e.view(nex, ney + 1, self._ne1, ney + 1, self._ne1)
-        n = torch.arange(ney, device=self.device)
-        for a in range(2):          # element n touches edge rows k = n + a, columns k = n + b
-            for b in range(2):
-                S[:, n + a, :, n + b, :] -= C[:, :, a, :, b, :].permute(1, 0, 2, 3)  # index dims lead
-        return Xi, Yie, A_ei, batched_inverse(S_e)
+        with self._phase("gather"):
+            A_ii = AII[e, pi[None, :, :, None], pi[None, :, None, :]]     # (nex, ney, ni, ni)
+            A_ie = AII[e, pi[None, :, :, None], pel[None, :, None, :]]    # (nex, ney, ni, 2 ne1)
+            A_ei = AII[e, pel[None, :, :, None], pi[None, :, None, :]]    # (nex, ney, 2 ne1, ni)
+            S_e = AII[e[:, :, 0], pe[None, :, None], pe[None, None, :]]   # (nex, n_e, n_e)
+        with self._phase("inv_element"):
+            Xi = batched_inverse(A_ii.reshape(-1, *A_ii.shape[-2:])).view(A_ii.shape)
+        with self._phase("edge_schur"):
+            Yie = Xi @ A_ie
+            C = (A_ei @ Yie).view(nex, ney, 2, self._ne1, 2, self._ne1)
+            S = S_e.view(nex, ney + 1, self._ne1, ney + 1, self._ne1)
+            n = torch.arange(ney, device=self.device)
+            for a in range(2):          # element n touches edge rows k = n + a, columns k = n + b
+                for b in range(2):
+                    S[:, n + a, :, n + b, :] -= C[:, :, a, :, b, :].permute(1, 0, 2, 3)  # index dims lead
+        with self._phase("inv_edge"):
+            Se_inv = batched_inverse(S_e)
+        return Xi, Yie, A_ei, Se_inv
 
     def _nested_factor(self, AII):
         self._nested_index()

@@ -12,7 +12,20 @@ whose reference run is infeasible in this container: the reference's 8-D convect
         oracle's Newton iteration with SuperLU velocity solves and the Schur-complement LGMRES
         (NavierStokes_Solver.py:162-270).  Saved: u, v, p, the Newton count and residual history.
 
-Usage:  python tests/golden/make_oracle_fixtures.py cd64|ns8      (cd64: ~6 minutes, ns8: ~40 s)
+  cfg4: BASELINE cfg4 (Boussinesq, Ra = 1e6, 48 x 48 elements, P = 8 for both solvers) at the converged
+        state of the device's Ra continuation (tests/golden/cfg4_state.npz: [T, u, v, p], written by
+        tools/bous_solve.py after Newton 5 of the Ra = 1e6 stage, profiles/r02/bous/b48_ra1e6_part2.log).
+        Saved: the oracle's coupled residual there (ConvectionDiffusion_Solver.py:73-92 with u, v from
+        the NS field; NavierStokes_Solver.py:93-121 with T from the CD field; the couplers' PG group,
+        OpenMDAO/Boussinesq_SequentialCoupler.py:66-73) as block norms and strided samples, and the
+        oracle's CD Newton update for a seeded right-hand side -- the exact solution of the reference's
+        linearised system (_get_dresiduals at du = dv = 0, Dirichlet identity rows) by a sparse direct
+        solve, which the reference's LGMRES approximates to mtol sqrt(N).  The oracle's NS update (SuperLU of
+        the 296,450^2 velocity Jacobian inside an LGMRES Schur solve of ~2,000 iterations) does not finish
+        in this container: the SuperLU factorisation alone ran past 10 minutes, so the GPU test pins the
+        device NS update by the oracle's linearised operator instead (tests/test_gpu_cfg4.py).
+
+Usage:  python tests/golden/make_oracle_fixtures.py cd64|ns8|cfg4   (cd64: ~6 minutes, ns8: ~40 s)
 """
 import os
 import sys
@@ -62,5 +75,49 @@ def gen_ns8():
     print("ns8", ns.N, len(hist) - 1, [h[0] for h in hist])
 
 
+CFG4 = dict(Ne=48, P=8, Re=1e3, Ra=1e6, Pr=0.71, stride=97, seed=44)
+
+
+def cfg4_rhs(N, seed=CFG4["seed"]):
+    """The seeded right-hand sides of the cfg4 update checks (shared with tests/test_gpu_cfg4.py)."""
+    r = np.random.default_rng(seed)
+    return r.uniform(-1, 1, N), tuple(r.uniform(-1, 1, N) for _ in range(3))
+
+
+def gen_cfg4():
+    from oracle import sem_oracle as O
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    c = CFG4
+    P, ne, Re, Ra, Pr = c["P"], c["Ne"], c["Re"], c["Ra"], c["Pr"]
+    x = np.load(os.path.join(HERE, "cfg4_state.npz"))["x"]
+    N = (ne * P + 1) ** 2
+    T, u, v, p = x[:N], x[N:2 * N], x[2 * N:3 * N], x[3 * N:]
+    t0 = time.perf_counter()
+    cd = O.CDOracle(1.0, 1.0, Re * Pr, P, ne, ne, T_W=0.5, T_E=-0.5)
+    ns = O.NSOracle(1.0, 1.0, Re, Ra / Pr, P, ne, ne)
+    rT = cd.residuals(T, u, v)
+    ru, rv, rc = ns.residuals(u, v, p, T)
+    R = np.concatenate((rT, ru, rv, rc))
+    s = c["stride"]
+    # CD update: dres_op = Sys with the Dirichlet rows as identity rows (:104-121 at du = dv = 0)
+    bT, _ = cfg4_rhs(N)
+    A = cd.Sys.tolil()
+    A[cd.mask, :] = 0
+    A[cd.mask, cd.mask] = 1
+    A = A.tocsc()
+    dT = spla.spsolve(A, bT)
+    res_cd = np.linalg.norm(cd.dresiduals(dT) - bT)
+    np.savez_compressed(os.path.join(HERE, "cfg4_oracle.npz"), N=np.array(N), DOF=np.array(4 * N),
+                        R_norm=np.array(np.linalg.norm(R)),
+                        R_block_norms=np.array([np.linalg.norm(a) for a in (rT, ru, rv, rc)]),
+                        R_block_amax=np.array([np.abs(a).max() for a in (rT, ru, rv, rc)]),
+                        sample_idx=np.arange(0, 4 * N, s), R_sample=R[::s],
+                        cd_update_norm=np.array(np.linalg.norm(dT)), cd_update_sample=dT[::s],
+                        cd_update_oracle_residual=np.array(res_cd), seconds=np.array(time.perf_counter() - t0))
+    print("cfg4", N, np.linalg.norm(R), [np.linalg.norm(a) for a in (rT, ru, rv, rc)], np.linalg.norm(dT), res_cd,
+          time.perf_counter() - t0)
+
+
 if __name__ == "__main__":
-    {"cd64": gen_cd64, "ns8": gen_ns8}[sys.argv[1]]()
+    {"cd64": gen_cd64, "ns8": gen_ns8, "cfg4": gen_cfg4}[sys.argv[1]]()

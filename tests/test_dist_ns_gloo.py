@@ -103,3 +103,70 @@ def test_partitioned_ns_solver_gloo(world, case):
         assert e["update"] < 1e-9, (rank, e)
         assert e["newton"][0] == e["newton"][1], (rank, e)
         assert e["solve"] < 1e-8, (rank, e)
+
+
+def _fail_worker(rank, world, port, which, q):
+    """Rank 0's whole-mesh update raises (as a Schur Krylov solve that fails to converge does); every
+    rank must raise, none may stay blocked in the broadcast."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    sys.path.insert(0, here)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cpu_mesh import CPUStripMesh
+        from oracle_solvers import OracleCD, OracleNS
+        from sem_amd.parallel import Partition
+        from sem_amd.solvers import ConvectionDiffusionSolver, NavierStokesSolver
+        P, nex, ney = 4, 4, 3
+        part = Partition(dist, mesh_factory=CPUStripMesh)
+        z = None
+        if which == "ns":
+            s = NavierStokesSolver(1.0, 1.0, 100.0, 0.0, P, nex, ney, u_N=1.0, iprint=[], partition=part)
+            twin = OracleNS(1.0, 1.0, 100.0, 0.0, P, nex, ney)
+            z = np.zeros(s.N)
+            s._get_residuals(z, z, z, z)
+            s._calc_jacobians(z, z)
+        else:
+            s = ConvectionDiffusionSolver(1.0, 1.0, 40.0, P, nex, ney, T_W=0.5, T_E=-0.5, partition=part,
+                                          partition_update="central")
+            twin = OracleCD(1.0, 1.0, 40.0, P, nex, ney, T_W=0.5, T_E=-0.5)
+            z = np.zeros(s.N)
+            s._get_residuals(z, z, z)
+
+        def boom(*a, **k):
+            raise RuntimeError("LGMRES: Failed to converge in 1 iterations")
+
+        twin._get_update = boom
+        s._central_solver = lambda: twin
+        try:
+            s._get_update(z, z, z) if which == "ns" else s._get_update(z)
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("which", ["ns", "cd"])
+def test_rank0_update_failure_reaches_every_rank(which):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, 2, port, which, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res, t0 = {}, time.time()
+    while len(res) < 2:
+        try:
+            k, v = q.get(timeout=2)
+            res[k] = v
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead and time.time() - t0 < 120, f"rank failed or hung (exit codes {dead})"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert "Failed to converge" in res[0]
+    assert "failed on rank 0" in res[1]

@@ -49,6 +49,8 @@ def main():
     out["factor_peak_GB"] = torch.cuda.max_memory_allocated(dev) / 1e9
     out["interior_dense_GB_one_shot"] = vs.interior_bytes() / 1e9
     out["resident_GB"] = torch.cuda.memory_allocated(dev) / 1e9
+    if vs.timing:   # SEM_PROFILE_FACTOR=1
+        out["factor_phases_s"] = vs.timing
     print(json.dumps(out), flush=True)
     r = np.random.default_rng(7)
     bu, bv = (ns._dev(r.uniform(-1, 1, N)) for _ in range(2))

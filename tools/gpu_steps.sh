@@ -1,0 +1,42 @@
+#!/bin/bash
+# GPU steps by name, for gpurun:  TAG=r03a tools/gpu_steps.sh cfg4 inv cfg5factor pmcbench
+# Each step runs under its own time limit; a failure, abort or timeout ends the call (no retries, no
+# further GPU step).  Logs and profiles under gpurun_out/$TAG/.
+set -o pipefail
+O=gpurun_out/${TAG:-r03}
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+PYT="python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread"
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  tail -n "${TAILN:-6}" "$O/$name.log"
+  if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; exit $rc; fi
+}
+for s in "$@"; do
+  case $s in
+    gpu)        step gputests 1100 $PYT -q -m gpu tests ;;
+    cfg4)       step cfg4 300 $PYT tests/test_gpu_cfg4.py ;;
+    nsapply)    step nsapply 300 $PYT tests/test_gpu_ns_apply.py ;;
+    velocity)   step velocity 600 $PYT tests/test_gpu_ns_velocity.py ;;
+    smoke)      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)      step bench 600 python bench.py ;;
+    inv)        step inv 300 python tools/inv_repro.py ;;
+    cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
+    cfg5ns)     SEM_PROFILE_FACTOR=1 step cfg5ns 900 python tools/cfg5_ns_probe.py ;;
+    pmcbench)
+      tools/pmc_run.sh "$O/pmc_cal" -- python tools/kbench.py --dss 1024 || exit 1
+      tools/pmc_run.sh "$O/pmc_cd64" -- python tools/kbench.py --meshes 8:64 --reps 200 || exit 1
+      tools/pmc_run.sh "$O/pmc_cd1024" -- python tools/kbench.py --meshes 8:1024 --reps 20 || exit 1
+      tools/pmc_run.sh "$O/pmc_mfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1
+      tools/pmc_run.sh "$O/pmc_dot2" -- python tools/sweep_bench.py || exit 1 ;;
+    benchtrace)
+      step bench 600 python bench.py
+      step benchtrace 600 rocprofv3 --kernel-trace --stats -d "$O/benchtrace" -o trace --output-format csv -- \
+        python bench.py --cpu-seconds 0 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "all steps ok"
