@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 6
+#define SEM_ABI_VERSION 7
 
 enum sem_status {
   SEM_OK = 0,
@@ -256,6 +256,20 @@ int sem_line_block_sizes(const sem_handle* h, int ncomp, int64_t* sizes);
 int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes);
 int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* A_II, double* D, double* aIB, double* aBI,
                         double* E, double* F, void* stream);
+/* ABI 7: the same Jacobian with the interior rows of element columns [col_begin, col_end) written straight
+ * into the layout of the nested condensation (VelocityJacobianSolver.factor_condensed) instead of a dense
+ * A_II per column: per element n of a column the interior block A_ii (ni x ni), its couplings to the
+ * column's horizontal edges n, n+1 A_ie (ni x 2 ne1) and A_ei (2 ne1 x ni); per column the block-tridiagonal
+ * edge operator A_ee as diagonal blocks Aed (N_ey+1 of ne1 x ne1), upper blocks Aeu (edge k -> k+1) and
+ * lower blocks Ael (edge k+1 -> k), N_ey each.  Row-major blocks; element-interior unknown
+ * ((l-1) nc + c)(P-1) + j-1 = line l, component c, y node nP + j; edge unknown (l-1) nc + c.  The interface
+ * pieces D, aIB, aBI, E, F are as sem_velocity_blocks writes them.  P >= 2.  Per-column sizes (doubles)
+ * from sem_condensed_block_sizes: sizes[0..5] = A_ii, A_ie, A_ei, Aed, Aeu, Ael (times col_end - col_begin
+ * columns).  Replaces the 9 GB dense column interiors the ABI-6 path assembled per cfg5 column. */
+int sem_condensed_block_sizes(const sem_handle* h, int ncomp, int64_t* sizes);
+int sem_condensed_blocks(sem_handle* h, const sem_velocity_desc* d, double* Aii, double* Aie, double* Aei,
+                         double* Aed, double* Aeu, double* Ael, double* D, double* aIB, double* aBI, double* E,
+                         double* F, void* stream);
 
 /* ---- nested interior solve of the condensation (velocity / CD Jacobian) ---- */
 /* y = A_II^-1 r for every element column at once, from the factor VelocityJacobianSolver keeps

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE = range(6)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
@@ -93,6 +93,8 @@ _SIGS = {
     "sem_velocity_block_sizes": (C.c_int, [C.c_void_p, _i64p]),
     "sem_line_block_sizes": (C.c_int, [C.c_void_p, C.c_int, _i64p]),
     "sem_velocity_blocks": (C.c_int, [C.c_void_p, C.POINTER(SemVelocityDesc)] + [C.c_void_p] * 7),
+    "sem_condensed_block_sizes": (C.c_int, [C.c_void_p, C.c_int, _i64p]),
+    "sem_condensed_blocks": (C.c_int, [C.c_void_p, C.POINTER(SemVelocityDesc)] + [C.c_void_p] * 12),
     "sem_ns_apply": (C.c_int, [C.c_void_p, C.POINTER(SemNsDesc)] + [C.c_void_p] * 7),
     "sem_nested_solve": (C.c_int, [C.POINTER(SemNestedDesc), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_int64, C.c_void_p]),

@@ -10,15 +10,14 @@
 // rc = p - g_p (:116 / :160) -- written before the Neumann rows in the residual (so a pin on the
 // boundary is overwritten, as the reference's statement order does) and after them in the differential.
 //
-// One thread per node (x-major numbering, SEM.py:110), every operator in its tensor-product form with the
-// 1-D direct-stiffness sums of the GLL tables (the algebra of the apply kernels and of
-// ns_velocity.hip).  On an element-column strip handle (multi-GPU partition) the x-direction sums run
-// over the strip's own element columns, so the two interface lines carry partial sums that the
-// interface exchange adds up; pointwise terms, Dirichlet rows and the pinned-pressure row of the
-// right interface line are left to its right-hand owner (the rule of the apply kernels), so the
-// exchanged sum is the whole-mesh row.  The operands are read through L1/L2 (each value is reused by the 2P+1 threads whose
-// windows cover it); the launch is latency-bound at the Navier-Stokes sizes (N <= 10^6), where replacing
-// the 7 sem_apply launches of each output set is the point.
+// Tiled (ns_apply_tile): one workgroup per tile of element nodes stages u, v, p of the tile and its halo
+// in LDS with coalesced loads, then forms every owned node's three outputs from LDS (x-major numbering,
+// SEM.py:110; every operator in its tensor-product form with the 1-D direct-stiffness sums of the GLL
+// tables -- the algebra of the apply kernels and of ns_velocity.hip).  On an element-column strip handle
+// (multi-GPU partition) the x-direction sums run over the strip's own element columns, so the two
+// interface lines carry partial sums that the interface exchange adds up; pointwise terms, Dirichlet rows
+// and the pinned-pressure row of the right interface line are left to its right-hand owner (the rule of
+// the apply kernels), so the exchanged sum is the whole-mesh row.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -44,39 +43,25 @@ struct NsArgs {
   unsigned sides;
 };
 
-// K_s / G_s sums of one 1-D direction: global node g (element e = g / P, local index i) of a direction
-// whose held elements are [e_lo, e_hi); x[k * stride] is held 1-D node k + off of the line through the
-// thread's node (off = the first held line).
-__device__ __forceinline__ void dir_sums(const double* __restrict__ x, int64_t stride, int g, int off, int P,
-                                         int e_lo, int e_hi, const double* Ks, const double* Gs, double& k,
-                                         double& gr) {
-  const int n = P + 1, e = g / P, i = g - e * P;
-  k = 0.0;
-  gr = 0.0;
+// One 1-D direction of the operators at one node: calls f(row, q, off) for the node's element row(s) of
+// the K_s / G_s tables -- row i of its element (interior index i != 0), or at an element boundary (i == 0)
+// row P of the element on the left (if held: e > e_lo) and row 0 of the element on the right (if
+// e < e_hi) -- where off is the offset of that element's node q from the node in the staged arrays
+// (`stride` steps one node along the direction: the LDS pitch across lines, 1 along a line).
+template <int P, class F>
+__device__ __forceinline__ void dir_rows(int stride, int e, int i, int e_lo, int e_hi, F&& f) {
   if (i != 0) {
-    const double* xb = x + static_cast<int64_t>(e * P - off) * stride;
-    for (int q = 0; q <= P; ++q) {
-      const double t = xb[q * stride];
-      k = fma(Ks[i * n + q], t, k);
-      gr = fma(Gs[i * n + q], t, gr);
-    }
+#pragma unroll
+    for (int q = 0; q <= P; ++q) f(i, q, (q - i) * stride);
     return;
   }
-  if (e > e_lo) {  // row P of the element on the left
-    const double* xb = x + static_cast<int64_t>((e - 1) * P - off) * stride;
-    for (int q = 0; q <= P; ++q) {
-      const double t = xb[q * stride];
-      k = fma(Ks[P * n + q], t, k);
-      gr = fma(Gs[P * n + q], t, gr);
-    }
+  if (e > e_lo) {
+#pragma unroll
+    for (int q = 0; q <= P; ++q) f(P, q, (q - P) * stride);
   }
-  if (e < e_hi) {  // row 0 of the element on the right
-    const double* xb = x + static_cast<int64_t>(e * P - off) * stride;
-    for (int q = 0; q <= P; ++q) {
-      const double t = xb[q * stride];
-      k = fma(Ks[q], t, k);
-      gr = fma(Gs[q], t, gr);
-    }
+  if (e < e_hi) {
+#pragma unroll
+    for (int q = 0; q <= P; ++q) f(0, q, q * stride);
   }
 }
 
@@ -85,81 +70,162 @@ __device__ __forceinline__ double wsum1(int g, int P, int e_lo, int e_hi, const 
   return i != 0 ? w[i] : (e > e_lo ? w[P] : 0.0) + (e < e_hi ? w[0] : 0.0);
 }
 
-__global__ __launch_bounds__(256) void ns_apply_kernel(const NsArgs a) {
-  extern __shared__ double tab[];
-  const int P = a.P, n = P + 1, ntab = 2 * n * n + n;
-  for (int i = threadIdx.x; i < ntab; i += blockDim.x) tab[i] = a.tab[i];
+// Tile shape: TXE element columns x TYE element rows of owned nodes (lines [gx0, gx0 + TXE P), columns
+// [gy0, gy0 + TYE P); the closing line / column of the strip belongs to a ghost tile one position past the
+// last element).  Staged: the owned block plus the P lines / columns before it (the left / lower
+// neighbour element of the tile's first line / column) and the one after it (the closing node of its last
+// element).
+template <int P>
+struct NsTile {
+  static constexpr int TXE = 1;
+  static constexpr int TYE = (32 / P) > 0 ? 32 / P : 1;
+  static constexpr int BX = TXE * P, BY = TYE * P;
+  static constexpr int SX = BX + P + 1, SY = BY + P + 1;
+  static constexpr int PITCH = SY | 1;  // odd: lanes striding across staged lines hit distinct banks
+  static constexpr int THREADS = 256;
+};
+
+// One workgroup per tile (XCD-aware order: the 8 XCDs take contiguous runs of tiles, so neighbouring
+// tiles -- which stage each other's halo -- share an L2).  Phase 1 stages u, v, p of the tile and its halo
+// in LDS with loads coalesced along the lines; phase 2 forms every owned node's outputs from LDS only.
+// The Sys rows use the assembled 1-D coefficients (cK K + Re c G of the node's row combined before the
+// dot product, as the reference's CSR row of Sys = K + Re (diag(u) G_x + diag(v) G_y) holds them).
+template <int P>
+__global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y, int ntiles, int per_xcd) {
+  using T = NsTile<P>;
+  constexpr int n = P + 1, BX = T::BX, BY = T::BY, SX = T::SX, SY = T::SY, PIT = T::PITCH;
+  __shared__ double tab[2 * n * n + n];
+  __shared__ double su[SX * PIT], sv[SX * PIT], sp[SX * PIT];
+  const int b = blockIdx.x;
+  const int tile = (b & 7) * per_xcd + (b >> 3);
+  if (tile >= ntiles) return;
+  const int tx = tile / tiles_y, ty = tile - tx * tiles_y;
+  const int eb = a.ex_begin, ee = a.ex_end, lb0 = a.lb0, lb1 = a.lb1, NY = a.NY;
+  const int gx0 = (eb + tx * T::TXE) * P, gy0 = ty * T::TYE * P;
+  const int sx0 = gx0 - P, sy0 = gy0 - P;  // staged origin
+  for (int i = threadIdx.x; i < 2 * n * n + n; i += T::THREADS) tab[i] = a.tab[i];
+  // phase 1: staging (nodes outside the strip / mesh stay unset and are never read)
+  const int64_t pitch = a.pitch;
+  for (int k = threadIdx.x; k < SX * SY; k += T::THREADS) {
+    const int r = k / SY, c = k - r * SY;
+    const int gx = sx0 + r, gy = sy0 + c;
+    if (gx < lb0 || gx > lb1 || gy < 0 || gy >= NY) continue;
+    const int64_t lx = gx - lb0;
+    if (a.u) su[r * PIT + c] = a.u[lx * pitch + gy];
+    if (a.v) sv[r * PIT + c] = a.v[lx * pitch + gy];
+    if (a.p) sp[r * PIT + c] = a.p[lx * NY + gy];
+  }
   __syncthreads();
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= a.n_local) return;
-  const int lx = static_cast<int>(t / a.NY), gy = static_cast<int>(t - static_cast<int64_t>(lx) * a.NY);
-  const int gx = a.lb0 + lx;                              // global line
   const double* Ks = tab;
   const double* Gs = tab + n * n;
   const double* w = tab + 2 * n * n;
-  const double mx = wsum1(gx, P, a.ex_begin, a.ex_end, w), my = wsum1(gy, P, 0, a.ney, w);
-  const int64_t q = t;                                    // node in the plain (local) vectors
-  const int64_t qv = static_cast<int64_t>(lx) * a.pitch + gy;  // node in u, v, ru, rv
-  // the right interface line of a strip is owned by the strip on its right
-  const bool own = !(gx == a.lb1 && a.ex_end < a.nex);
-  const bool dir = a.mask ? a.mask[q] != 0
-                          : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
-                             ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1));
   const bool want_uv = a.ru || a.rv;
-  // x-direction lines run across lines (stride pitch / NY), y-direction along a line (stride 1)
-  double kxu = 0, gxu = 0, kyu = 0, gyu = 0, kxv = 0, gxv = 0, kyv = 0, gyv = 0, kxp = 0, gxp = 0, kyp = 0, gyp = 0;
-  const double u0 = a.u ? a.u[qv] : 0.0, v0 = a.v ? a.v[qv] : 0.0;
-  const int eb = a.ex_begin, ee = a.ex_end, lb = a.lb0;
-  if (a.u && ((want_uv && !dir) || a.rc)) {
-    dir_sums(a.u + gy, a.pitch, gx, lb, P, eb, ee, Ks, Gs, kxu, gxu);
-    dir_sums(a.u + static_cast<int64_t>(lx) * a.pitch, 1, gy, 0, P, 0, a.ney, Ks, Gs, kyu, gyu);
-  }
-  if (a.v && ((want_uv && !dir) || a.rc)) {
-    dir_sums(a.v + gy, a.pitch, gx, lb, P, eb, ee, Ks, Gs, kxv, gxv);
-    dir_sums(a.v + static_cast<int64_t>(lx) * a.pitch, 1, gy, 0, P, 0, a.ney, Ks, Gs, kyv, gyv);
-  }
-  if (a.p) {
-    dir_sums(a.p + gy, a.NY, gx, lb, P, eb, ee, Ks, Gs, kxp, gxp);
-    dir_sums(a.p + static_cast<int64_t>(lx) * a.NY, 1, gy, 0, P, 0, a.ney, Ks, Gs, kyp, gyp);
-  }
-  if (want_uv) {
-    if (dir) {
-      if (a.ru) a.ru[qv] = own ? u0 - (a.gu ? a.gu[q] : 0.0) : 0.0;
-      if (a.rv) a.rv[qv] = own ? v0 - (a.gv ? a.gv[q] : 0.0) : 0.0;
-    } else {
-      const double cu = a.cu ? a.cu[q] : 1.0, cv = a.cv ? a.cv[q] : 1.0;
-      const double fx = a.fKx * my, fy = a.fKy * mx, fm = a.fM * mx * my;
-      const double gxc = a.fX * cu * my, gyc = a.fY * cv * mx;
-      if (a.ru) {
-        double z = fx * kxu + gxc * gxu + fy * kyu + gyc * gyu + fm * u0;
-        if (a.juu && own) z = fma(a.juu[q], u0, z);
-        if (a.juv && own) z = fma(a.juv[q], v0, z);
-        a.ru[qv] = fma(a.hy * my, gxp, z);
-      }
-      if (a.rv) {
-        double z = fx * kxv + gxc * gxv + fy * kyv + gyc * gyv + fm * v0;
-        if (a.jvu && own) z = fma(a.jvu[q], u0, z);
-        if (a.jvv && own) z = fma(a.jvv[q], v0, z);
-        z = fma(a.hx * mx, gyp, z);
-        if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
-        a.rv[qv] = z;
+  for (int k = threadIdx.x; k < BX * BY; k += T::THREADS) {
+    const int ox = k / BY, oy = k - ox * BY;
+    const int gx = gx0 + ox, gy = gy0 + oy;
+    if (gx > lb1 || gy >= NY) continue;
+    const int ex = gx / P, ix = gx - ex * P, ey = gy / P, iy = gy - ey * P;
+    const double mx = wsum1(gx, P, eb, ee, w), my = wsum1(gy, P, 0, a.ney, w);
+    const int64_t q = static_cast<int64_t>(gx - lb0) * NY + gy;   // node in the plain (local) vectors
+    const int64_t qv = static_cast<int64_t>(gx - lb0) * pitch + gy;  // node in u, v, ru, rv
+    const int sidx = (ox + P) * PIT + (oy + P);                    // node in the staged arrays
+    const bool own = !(gx == lb1 && ee < a.nex);  // the right interface line of a strip: its right owner's
+    const bool dir = a.mask ? a.mask[q] != 0
+                            : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
+                               ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
+    const double u0 = a.u ? su[sidx] : 0.0, v0 = a.v ? sv[sidx] : 0.0;
+    if (want_uv) {
+      if (dir) {
+        if (a.ru) a.ru[qv] = own ? u0 - (a.gu ? a.gu[q] : 0.0) : 0.0;
+        if (a.rv) a.rv[qv] = own ? v0 - (a.gv ? a.gv[q] : 0.0) : 0.0;
+      } else {
+        const double cu = a.cu ? a.cu[q] : 1.0, cv = a.cv ? a.cv[q] : 1.0;
+        const double fx = a.fKx * my, gxc = a.fX * cu * my;  // x rows of Sys: fx K + gxc G
+        const double fy = a.fKy * mx, gyc = a.fY * cv * mx;  // y rows of Sys: fy K + gyc G
+        double Su = 0.0, Sv = 0.0, gxp = 0.0, gyp = 0.0;
+        const bool hu = a.u != nullptr, hv = a.v != nullptr, hp = a.p != nullptr;
+        if (hu || hv) {
+          dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
+            const double co = fma(gxc, Gs[row * n + c], fx * Ks[row * n + c]);
+            if (hu) Su = fma(co, su[sidx + off], Su);
+            if (hv) Sv = fma(co, sv[sidx + off], Sv);
+          });
+          dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
+            const double co = fma(gyc, Gs[row * n + c], fy * Ks[row * n + c]);
+            if (hu) Su = fma(co, su[sidx + off], Su);
+            if (hv) Sv = fma(co, sv[sidx + off], Sv);
+          });
+        }
+        if (hp) {
+          if (a.ru) dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
+            gxp = fma(Gs[row * n + c], sp[sidx + off], gxp);
+          });
+          if (a.rv) dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
+            gyp = fma(Gs[row * n + c], sp[sidx + off], gyp);
+          });
+        }
+        const double fm = a.fM * mx * my;
+        if (a.ru) {
+          double z = fma(fm, u0, Su);
+          if (a.juu && own) z = fma(a.juu[q], u0, z);
+          if (a.juv && own) z = fma(a.juv[q], v0, z);
+          a.ru[qv] = fma(a.hy * my, gxp, z);
+        }
+        if (a.rv) {
+          double z = fma(fm, v0, Sv);
+          if (a.jvu && own) z = fma(a.jvu[q], u0, z);
+          if (a.jvv && own) z = fma(a.jvv[q], v0, z);
+          z = fma(a.hx * mx, gyp, z);
+          if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
+          a.rv[qv] = z;
+        }
       }
     }
+    if (a.rc) {
+      const bool pinned = static_cast<int64_t>(gx) * NY + gy == a.pin;
+      const double pinrow = own ? (a.p ? sp[sidx] : 0.0) - a.pin_val : 0.0;
+      double z;
+      if (pinned && !a.pin_first) {
+        z = pinrow;
+      } else if (dir) {  // the (K p) row: sx my Kx p + sy mx Ky p, coefficients combined on the diagonal
+        double kp = 0.0;
+        if (a.p) {
+          const double fx = a.sx * my, fy = a.sy * mx;
+          dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
+            kp = fma(fx * Ks[row * n + c], sp[sidx + off], kp);
+          });
+          dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
+            kp = fma(fy * Ks[row * n + c], sp[sidx + off], kp);
+          });
+        }
+        z = kp;
+      } else if (pinned) {
+        z = pinrow;
+      } else {
+        double gxu = 0.0, gyv = 0.0;
+        if (a.u) dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
+          gxu = fma(Gs[row * n + c], su[sidx + off], gxu);
+        });
+        if (a.v) dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
+          gyv = fma(Gs[row * n + c], sv[sidx + off], gyv);
+        });
+        z = a.c_div * (a.hy * my * gxu + a.hx * mx * gyv);
+      }
+      a.rc[q] = z;
+    }
   }
-  if (a.rc) {
-    const bool pinned = static_cast<int64_t>(gx) * a.NY + gy == a.pin;
-    const double pinrow = own ? (a.p ? a.p[q] : 0.0) - a.pin_val : 0.0;
-    double z;
-    if (pinned && !a.pin_first)
-      z = pinrow;
-    else if (dir)
-      z = a.sx * my * kxp + a.sy * mx * kyp;  // (K p) row
-    else if (pinned)
-      z = pinrow;
-    else
-      z = a.c_div * (a.hy * my * gxu + a.hx * mx * gyv);
-    a.rc[q] = z;
-  }
+}
+
+template <int P>
+static void launch_ns_tile(const NsArgs& a, hipStream_t s) {
+  using T = NsTile<P>;
+  const int ncols = a.ex_end - a.ex_begin;
+  const int tiles_x = (ncols + T::TXE) / T::TXE;  // positions 0..ncols (ncols: the closing line)
+  const int tiles_y = (a.ney + T::TYE) / T::TYE;
+  const int ntiles = tiles_x * tiles_y;
+  const int per_xcd = (ntiles + 7) / 8;
+  hipLaunchKernelGGL(ns_apply_tile<P>, dim3(static_cast<unsigned>(8 * per_xcd)), dim3(T::THREADS), 0, s, a, tiles_y,
+                     ntiles, per_xcd);
 }
 
 static int hip_check_ns(hipError_t e, const char* what) {
@@ -226,11 +292,19 @@ int sem_ns_apply(sem_handle* h, const sem_ns_desc* d, const double* u, const dou
   a.lb0 = static_cast<int>(h->line_begin);
   a.lb1 = static_cast<int>(h->line_end);
   a.n_local = h->n_local;
-  const int n = h->P + 1;
-  const size_t lds = (2 * n * n + n) * sizeof(double);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(sem::ns_apply_kernel, dim3(static_cast<unsigned>((h->n_local + 255) / 256)), dim3(256), lds, s,
-                     a);
+  switch (h->P) {
+#define SEM_NSCASE(PP)                 \
+  case PP:                             \
+    sem::launch_ns_tile<PP>(a, s);     \
+    break;
+    SEM_NSCASE(1) SEM_NSCASE(2) SEM_NSCASE(3) SEM_NSCASE(4) SEM_NSCASE(5) SEM_NSCASE(6) SEM_NSCASE(7) SEM_NSCASE(8)
+    SEM_NSCASE(9) SEM_NSCASE(10) SEM_NSCASE(11) SEM_NSCASE(12) SEM_NSCASE(13) SEM_NSCASE(14) SEM_NSCASE(15)
+    SEM_NSCASE(16)
+#undef SEM_NSCASE
+    default:
+      return sem::set_error(SEM_EUNSUPPORTED, "polynomial order outside compiled range");
+  }
   return sem::hip_check_ns(hipGetLastError(), "ns apply launch");
 }
 

@@ -46,12 +46,107 @@ struct VelocityArgs {
   int c0, c1;  // element columns whose A_II blocks are written (A_II indexed from c0)
   unsigned sides;
   double *AII, *D, *aIB, *aBI, *E, *F;
+  // ABI 7, condensed layout of the interior rows of columns [c0, c1) (instead of the dense AII):
+  //   Aii [e][n][ni][ni], Aie [e][n][ni][2 ne1], Aei [e][n][2 ne1][ni]        (element n of column e)
+  //   Aed [e][k][ne1][ne1] (edge k with itself), Aeu [e][k][ne1][ne1] (row edge k, column edge k+1),
+  //   Ael [e][k][ne1][ne1] (row edge k+1, column edge k)
+  // element-interior index ((l-1) nc + c)(P-1) + j-1 (node (line l, component c, y node nP + j)),
+  // edge index (l-1) nc + c (node (l, c, kP)); e counted from c0.
+  double *Aii, *Aie, *Aei, *Aed, *Aeu, *Ael;
 };
 
 __device__ __forceinline__ bool is_dirichlet(const VelocityArgs& a, int gx, int gy) {
   if (a.mask) return a.mask[static_cast<int64_t>(gx) * a.NY + gy] != 0;
   return ((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
          ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1);
+}
+
+// Interior row (column L, line l, component c, node gy) of a non-Dirichlet node in the condensed layout:
+// its x couplings (the other interior lines of the column, same c and gy), y couplings (its line's nodes
+// in the element(s) holding gy), the other component at the node, and the diagonal, each written to the
+// block that holds the pair; the interface couplings go to aIB as in the dense layout.
+__device__ void condensed_row(const VelocityArgs& a, int L, int l, int c, int gy, int r, bool dir, double mx,
+                              double my, double cu, double cv, const double* Ks, const double* Gs) {
+  const int P = a.P, n = P + 1, nc = a.nc, ne1 = nc * (P - 1), ni = ne1 * (P - 1);
+  const int ey = gy / P, j = gy - ey * P;
+  const int64_t col = L - a.c0;
+  const int64_t node = static_cast<int64_t>(L * P + l) * a.NY + gy;
+  double* ib = a.aIB + (static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 * a.nc * a.NY + r;
+  const int mm = nc * a.NY;
+  const double fx = a.fKx * my, gxc = a.fX * cu * my;
+  const double fy = a.fKy * mx, gyc = a.fY * cv * mx;
+  auto xk = [&](int i, int k) { return fx * Ks[i * n + k] + gxc * Gs[i * n + k]; };
+  auto yk = [&](int i, int k) { return fy * Ks[i * n + k] + gyc * Gs[i * n + k]; };
+  const int lc = (l - 1) * nc + c;  // position of (l, c) among a node's interior-line unknowns
+  if (j != 0) {  // element interior of element ey
+    const int64_t el = col * a.ney + ey;
+    const int ri = lc * (P - 1) + j - 1;
+    double* Ar = a.Aii + (el * ni + ri) * ni;
+    if (dir) {
+      Ar[ri] = 1.0;
+      ib[0] = 0.0;
+      ib[mm] = 0.0;
+      return;
+    }
+    double* Er = a.Aie + (el * ni + ri) * 2 * ne1;
+    double dg = a.fM * mx * my + (c == 0 ? (a.juu ? a.juu[node] : 0.0) : (a.jvv ? a.jvv[node] : 0.0)) + xk(l, l);
+    for (int k = 1; k < P; ++k)
+      if (k != l) Ar[((k - 1) * nc + c) * (P - 1) + j - 1] = xk(l, k);
+    ib[0] = xk(l, 0);
+    ib[mm] = xk(l, P);
+    for (int q = 0; q <= P; ++q) {
+      const double v = yk(j, q);
+      if (q == j) dg += v;
+      else if (q == 0) Er[lc] = v;
+      else if (q == P) Er[ne1 + lc] = v;
+      else Ar[lc * (P - 1) + q - 1] = v;
+    }
+    if (nc == 2) {
+      const double* jc = c == 0 ? a.juv : a.jvu;
+      if (jc) Ar[((l - 1) * nc + 1 - c) * (P - 1) + j - 1] = jc[node];
+    }
+    Ar[ri] = dg;
+    return;
+  }
+  // edge k = ey (gy = kP): row lc of edge k
+  const int k = ey;
+  double* Dr = a.Aed + ((col * (a.ney + 1) + k) * ne1 + lc) * ne1;
+  if (dir) {
+    Dr[lc] = 1.0;
+    ib[0] = 0.0;
+    ib[mm] = 0.0;
+    return;
+  }
+  double dg = a.fM * mx * my + (c == 0 ? (a.juu ? a.juu[node] : 0.0) : (a.jvv ? a.jvv[node] : 0.0)) + xk(l, l);
+  for (int kk = 1; kk < P; ++kk)
+    if (kk != l) Dr[(kk - 1) * nc + c] = xk(l, kk);
+  ib[0] = xk(l, 0);
+  ib[mm] = xk(l, P);
+  if (k > 0) {  // element k-1 below: the edge is its top edge (rows ne1.. of its A_ei)
+    const int64_t el = col * a.ney + k - 1;
+    double* Fr = a.Aei + (el * 2 * ne1 + ne1 + lc) * ni;
+    for (int q = 0; q <= P; ++q) {
+      const double v = yk(P, q);
+      if (q == P) dg += v;
+      else if (q == 0) a.Ael[((col * a.ney + k - 1) * ne1 + lc) * ne1 + lc] = v;
+      else Fr[lc * (P - 1) + q - 1] = v;
+    }
+  }
+  if (k < a.ney) {  // element k above: the edge is its bottom edge (rows 0.. of its A_ei)
+    const int64_t el = col * a.ney + k;
+    double* Fr = a.Aei + (el * 2 * ne1 + lc) * ni;
+    for (int q = 0; q <= P; ++q) {
+      const double v = yk(0, q);
+      if (q == 0) dg += v;
+      else if (q == P) a.Aeu[((col * a.ney + k) * ne1 + lc) * ne1 + lc] = v;
+      else Fr[lc * (P - 1) + q - 1] = v;
+    }
+  }
+  if (nc == 2) {
+    const double* jc = c == 0 ? a.juv : a.jvu;
+    if (jc) Dr[(l - 1) * nc + 1 - c] = jc[node];
+  }
+  Dr[lc] = dg;
 }
 
 // One thread per Jacobian row: row = line gx (0..NX-1), component c, node gy.
@@ -84,6 +179,13 @@ __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs
     const double fx = a.fKx * my, gxc = a.fX * cu * my;
     ib[0] = fx * Ks[l * n] + gxc * Gs[l * n];
     ib[m] = fx * Ks[l * n + P] + gxc * Gs[l * n + P];
+    return;
+  }
+  if (l != 0 && a.Aii) {  // ABI 7: condensed layout
+    const int ey = gy / P, j = gy - ey * P;
+    const double mx = w[l];
+    const double my = j != 0 ? w[j] : (ey > 0 ? w[P] : 0.0) + (ey < a.ney ? w[0] : 0.0);
+    condensed_row(a, L, l, c, gy, r, dir, mx, my, a.cu ? a.cu[node] : 1.0, a.cv ? a.cv[node] : 1.0, Ks, Gs);
     return;
   }
   if (l == 0) {
@@ -198,10 +300,27 @@ int sem_line_block_sizes(const sem_handle* h, int ncomp, int64_t* sizes) {
 
 int sem_velocity_block_sizes(const sem_handle* h, int64_t* sizes) { return sem_line_block_sizes(h, 2, sizes); }
 
-int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, double* D, double* aIB, double* aBI,
-                        double* E, double* F, void* stream) {
+int sem_condensed_block_sizes(const sem_handle* h, int ncomp, int64_t* sizes) {
+  if (!h || !sizes) return sem::set_error(SEM_EINVAL, "null argument");
+  if (ncomp != 1 && ncomp != 2) return sem::set_error(SEM_EINVAL, "ncomp must be 1 or 2");
+  if (h->P < 2) return sem::set_error(SEM_EINVAL, "the condensed layout needs P >= 2");
+  const int64_t ne1 = static_cast<int64_t>(ncomp) * (h->P - 1), ni = ne1 * (h->P - 1), ney = h->ney;
+  sizes[0] = ney * ni * ni;         // A_ii
+  sizes[1] = ney * ni * 2 * ne1;    // A_ie
+  sizes[2] = ney * 2 * ne1 * ni;    // A_ei
+  sizes[3] = (ney + 1) * ne1 * ne1; // A_ee diagonal blocks
+  sizes[4] = ney * ne1 * ne1;       // A_ee upper (edge k -> k+1)
+  sizes[5] = ney * ne1 * ne1;       // A_ee lower (edge k+1 -> k)
+  return SEM_OK;
+}
+
+static int velocity_blocks_impl(sem_handle* h, const sem_velocity_desc* d, double* AII, double* const* cond, double* D,
+                                double* aIB, double* aBI, double* E, double* F, void* stream) {
   if (!h || !d || !D || !E || !F) return sem::set_error(SEM_EINVAL, "null argument");
-  if (h->P > 1 && (!AII || !aIB || !aBI)) return sem::set_error(SEM_EINVAL, "null interior block");
+  if (h->P > 1 && ((!AII && !cond) || !aIB || !aBI)) return sem::set_error(SEM_EINVAL, "null interior block");
+  if (cond)
+    for (int i = 0; i < 6; ++i)
+      if (!cond[i]) return sem::set_error(SEM_EINVAL, "null condensed block");
   if (h->ex_begin != 0 || h->ex_end != h->nex)
     return sem::set_error(SEM_EUNSUPPORTED, "the velocity blocks need a whole-mesh handle");
   int cur = -1;
@@ -217,9 +336,17 @@ int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, 
   sem_line_block_sizes(h, nc, sz);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int st;
-  const int64_t szA = sz[0] / h->nex * (c1 - c0);
-  if (h->P > 1 && (st = sem::hip_check_v(hipMemsetAsync(AII, 0, szA * sizeof(double), s), "memset A_II")))
-    return st;
+  if (cond) {
+    int64_t cs[6];
+    sem_condensed_block_sizes(h, nc, cs);
+    for (int i = 0; i < 6; ++i)
+      if ((st = sem::hip_check_v(hipMemsetAsync(cond[i], 0, cs[i] * (c1 - c0) * sizeof(double), s), "memset blocks")))
+        return st;
+  } else {
+    const int64_t szA = sz[0] / h->nex * (c1 - c0);
+    if (h->P > 1 && (st = sem::hip_check_v(hipMemsetAsync(AII, 0, szA * sizeof(double), s), "memset A_II")))
+      return st;
+  }
   if ((st = sem::hip_check_v(hipMemsetAsync(D, 0, sz[1] * sizeof(double), s), "memset D"))) return st;
   sem::VelocityArgs a{};
   a.tab = h->d_tab;
@@ -250,9 +377,31 @@ int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, 
   a.aBI = aBI;
   a.E = E;
   a.F = F;
+  if (cond) {
+    a.AII = nullptr;
+    a.Aii = cond[0];
+    a.Aie = cond[1];
+    a.Aei = cond[2];
+    a.Aed = cond[3];
+    a.Aeu = cond[4];
+    a.Ael = cond[5];
+  }
   const int64_t rows = h->NX * nc * h->NY;
   hipLaunchKernelGGL(sem::velocity_blocks_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)), dim3(256), 0, s, a);
   return sem::hip_check_v(hipGetLastError(), "velocity blocks launch");
+}
+
+int sem_velocity_blocks(sem_handle* h, const sem_velocity_desc* d, double* AII, double* D, double* aIB, double* aBI,
+                        double* E, double* F, void* stream) {
+  return velocity_blocks_impl(h, d, AII, nullptr, D, aIB, aBI, E, F, stream);
+}
+
+int sem_condensed_blocks(sem_handle* h, const sem_velocity_desc* d, double* Aii, double* Aie, double* Aei,
+                         double* Aed, double* Aeu, double* Ael, double* D, double* aIB, double* aBI, double* E,
+                         double* F, void* stream) {
+  if (h && h->P < 2) return sem::set_error(SEM_EINVAL, "the condensed layout needs P >= 2");
+  double* cond[6] = {Aii, Aie, Aei, Aed, Aeu, Ael};
+  return velocity_blocks_impl(h, d, nullptr, cond, D, aIB, aBI, E, F, stream);
 }
 
 }  // extern "C"

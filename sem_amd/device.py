@@ -168,6 +168,38 @@ class Mesh:
                                                  self.stream_ptr(stream)))
         return blocks
 
+    def condensed_blocks(self, blocks, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None, cv=None,
+                         juu=None, juv=None, jvu=None, jvv=None, dir_mask=None, dir_sides=0, ncomp=2, cols=None,
+                         stream=None):
+        """The velocity (ncomp=2) or scalar (ncomp=1) Jacobian in the nested condensation's layout
+        (include/sem_ops.h, sem_condensed_blocks, ABI 7): blocks["Aii", "Aie", "Aei", "Aed", "Aeu", "Ael"]
+        hold element columns cols = (c0, c1); "D", "aIB", "aBI", "E", "F" the whole mesh's interface pieces."""
+        for nm, t in (("cu", cu), ("cv", cv), ("juu", juu), ("juv", juv), ("jvu", jvu), ("jvv", jvv)):
+            self._vec(t, nm)
+        if dir_mask is not None and (dir_mask.dtype != torch.uint8 or dir_mask.numel() != self.n_local):
+            raise ValueError("dir_mask must be a uint8 tensor of n_local entries")
+        c0, c1 = (0, self.nex) if cols is None else (int(cols[0]), int(cols[1]))
+        if not 0 <= c0 < c1 <= self.nex:
+            raise ValueError("cols must be a non-empty element-column range")
+        line = (C.c_int64 * 6)()
+        _lib.check(self._lib.sem_line_block_sizes(self._h, int(ncomp), line))
+        cs = (C.c_int64 * 6)()
+        _lib.check(self._lib.sem_condensed_block_sizes(self._h, int(ncomp), cs))
+        cnames = ("Aii", "Aie", "Aei", "Aed", "Aeu", "Ael")
+        lnames = ("D", "aIB", "aBI", "E", "F")
+        want = [(nm, cs[i] * (c1 - c0)) for i, nm in enumerate(cnames)] + list(zip(lnames, list(line)[1:]))
+        for nm, sz in want:
+            t = blocks.get(nm)
+            if t is None or t.numel() != sz or t.dtype != torch.float64 or t.device != self.device \
+                    or not t.is_contiguous():
+                raise ValueError(f"block {nm} must be a contiguous float64 tensor of {sz} entries on {self.device}")
+        d = _lib.SemVelocityDesc(float(c_mass), float(c_stiff), float(c_gradx), float(c_grady), _ptr(cu), _ptr(cv),
+                                 _ptr(juu), _ptr(juv), _ptr(jvu), _ptr(jvv), _ptr(dir_mask), int(dir_sides),
+                                 int(ncomp), c0, c1)
+        _lib.check(self._lib.sem_condensed_blocks(self._h, C.byref(d), *(_ptr(blocks[nm]) for nm in cnames + lnames),
+                                                  self.stream_ptr(stream)))
+        return blocks
+
     def _line_view(self, t, name):
         """u, v, ru, rv of sem_ns_apply: a plain vector, or an (NX, NY) view with row stride >= NY."""
         if t is None:

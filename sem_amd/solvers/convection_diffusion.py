@@ -229,9 +229,8 @@ class ConvectionDiffusionSolver:
             m = self._mesh
             vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
             cX, cu, cY, cv, d = self._Sys._coeffs()
-            vs.factor_from(lambda b, cols: m.velocity_blocks(b, cols=cols, c_mass=self._Sys.cM, c_stiff=self._Sys.cK,
-                                                             c_gradx=cX, cu=cu, c_grady=cY, cv=cv, juu=d, ncomp=1,
-                                                             **self._dir.kw()))
+            vs.factor_mesh(m, c_mass=self._Sys.cM, c_stiff=self._Sys.cK, c_gradx=cX, cu=cu, c_grady=cY, cv=cv, juu=d,
+                           **self._dir.kw())
             if m.device.type == "cuda":
                 vs.capture()
             self._factor = vs

@@ -298,8 +298,7 @@ class NavierStokesSolver:
             torch.cuda.empty_cache()
         vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior,
                                     sweep=self._velocity_sweep)
-        vs.factor_from(lambda b, cols: m.velocity_blocks(b, cols=cols, dir_mask=self._dir.mask,
-                                                         dir_sides=self._dir.sides, **self._jac_kw))
+        vs.factor_mesh(m, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
         if self._velocity_graph:
             vs.capture()
         self._velo = vs
@@ -316,7 +315,7 @@ class NavierStokesSolver:
             vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
             mask = torch.zeros(m.n_local, dtype=torch.uint8, device=m.device)
             mask[self._pin if self._pin >= 0 else self.N // 2] = 1
-            vs.factor_from(lambda b, cols: m.velocity_blocks(b, cols=cols, c_stiff=1.0, ncomp=1, dir_mask=mask))
+            vs.factor_mesh(m, c_stiff=1.0, dir_mask=mask)
             if self._velocity_graph and m.device.type == "cuda":
                 vs.capture()
             self._Ap = vs

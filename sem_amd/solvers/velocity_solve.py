@@ -117,6 +117,8 @@ class VelocityJacobianSolver:
         # SEM_PROFILE_FACTOR=1: per-phase wall times of the factorisation (device-synchronised)
         self.profile = os.environ.get("SEM_PROFILE_FACTOR", "") == "1"
         self.timing = {}
+        # edge Schur systems up to this size are inverted densely (pivoted); larger ones by block LU
+        self.edge_dense_max = 1024
 
     @contextlib.contextmanager
     def _phase(self, name):
@@ -148,57 +150,271 @@ class VelocityJacobianSolver:
         return self.nex * self.nI * self.nI * 8
 
     def factor_from(self, fill, budget_bytes=24 << 30):
-        """Assemble and factor.  fill(blocks, cols) writes the pieces (sem_velocity_blocks) with
-        blocks["AII"] holding the dense interiors of element columns cols = (c0, c1).  When the whole
-        mesh's A_II fits in budget_bytes this is one fill + factor(); otherwise (cfg5: 1.17 TB of
-        dense interiors at 128^2, P = 12) the nested condensation runs a chunk of columns at a time,
-        each chunk's A_II assembled, condensed and freed before the next."""
-        per_col = self.nI * self.nI * 8 + 3 * self.nI * 2 * self.m * 8   # A_II + A_IB, W, work per column
-        if self.P == 1 or self.nex * per_col <= budget_bytes:
-            blocks = self.empty_blocks()
-            fill(blocks, (0, self.nex))
-            return self.factor(blocks.pop("AII"), **blocks)
-        if self.interior != "nested":
-            raise ValueError("column-chunked factorisation needs interior='nested'")
-        chunk = max(1, int(budget_bytes // per_col))
-        blocks = self.empty_blocks(with_interior=False)
-        self._nested_index()
-        P, nex, ney, m = self.P, self.nex, self.ney, self.m
-        ni, ne1, n_e = self._pi.shape[1], self._ne1, self._pe.numel()
+        """Assemble the dense-interior layout (sem_velocity_blocks: fill(blocks, cols) with blocks["AII"]
+        holding the dense interiors of element columns cols = (c0, c1)) and factor it.  Used by the "lu" /
+        "inverse" interior variants and by tests; the default nested interior assembles the condensed
+        layout directly (factor_mesh -> factor_condensed)."""
+        if self.P > 1 and self.nex * self.nI * self.nI * 8 > budget_bytes:
+            raise ValueError("the dense column interiors exceed the memory budget: use factor_mesh (condensed)")
+        blocks = self.empty_blocks()
+        fill(blocks, (0, self.nex))
+        return self.factor(blocks.pop("AII"), **blocks)
+
+    # ------------------------------------------------------------------ condensed assembly (ABI 7)
+    # The nested condensation straight from its pieces: the HIP kernel (sem_condensed_blocks) writes
+    # every element's interior block A_ii, its couplings A_ie / A_ei to the column's horizontal edges, and
+    # the block-tridiagonal edge operator A_ee -- no dense column interior A_II (9 GB per column at cfg5).
+    # With Xi = A_ii^-1 and the edge Schur complement S_e = A_ee - A_ei Xi A_ie, the interface coupling
+    # of a column, A_BI A_II^-1 A_IB, is
+    #     C = A_Bi Xi A_iB + Z_B S_e^-1 Z_e,  Z_e = A_eB - A_ei Xi A_iB,  Z_B = A_Be - A_Bi Xi A_ie,
+    # where A_iB / A_Bi couple an element's interior to the interface nodes at the same y (group G_n of
+    # the interface unknowns: (s, c, nP + j)) and A_eB / A_Be couple an edge to the interface nodes at its
+    # y (group H_k: (s, c, kP)).  Z_e is block-banded (the columns of G_n live on edges n, n+1; those of H_k
+    # on edge k), so V = S_e^-1 Z_e and Z_B V are batched products of thin blocks: O(n_e m ne1) per
+    # column instead of the O(n_I^2 m) of A_II^-1 A_IB.
+    def condensed_empty(self, ncols):
+        """Zeroed per-column condensed pieces of ncols element columns (sem_condensed_blocks layout)."""
+        P, ney, nc = self.P, self.ney, self.ncomp
+        ne1 = nc * (P - 1)
+        ni = ne1 * (P - 1)
         z = dict(dtype=torch.float64, device=self.device)
-        Xi, Yie = torch.empty((nex, ney, ni, ni), **z), torch.empty((nex, ney, ni, 2 * ne1), **z)
-        Aei, Sinv = torch.empty((nex, ney, 2 * ne1, ni), **z), torch.empty((nex, n_e, n_e), **z)
+        return dict(Aii=torch.zeros((ncols, ney, ni, ni), **z), Aie=torch.zeros((ncols, ney, ni, 2 * ne1), **z),
+                    Aei=torch.zeros((ncols, ney, 2 * ne1, ni), **z), Aed=torch.zeros((ncols, ney + 1, ne1, ne1), **z),
+                    Aeu=torch.zeros((ncols, ney, ne1, ne1), **z), Ael=torch.zeros((ncols, ney, ne1, ne1), **z))
+
+    def condense_dense(self, AII):
+        """The condensed pieces of dense column interiors AII (ncols, nI, nI): the layout
+        sem_condensed_blocks writes, taken from the dense blocks (CPU tests, interior="nested" factor())."""
+        self._nested_index()
+        ncols, ney, ne1 = AII.shape[0], self.ney, self._ne1
+        pi, pe, pel = self._pi, self._pe, self._pe_el
+        e = torch.arange(ncols, device=AII.device)[:, None, None, None]
+        out = dict(Aii=AII[e, pi[None, :, :, None], pi[None, :, None, :]],
+                   Aie=AII[e, pi[None, :, :, None], pel[None, :, None, :]],
+                   Aei=AII[e, pel[None, :, :, None], pi[None, :, None, :]])
+        Aee = AII[e[:, :, 0], pe[None, :, None], pe[None, None, :]].view(ncols, ney + 1, ne1, ney + 1, ne1)
+        k = torch.arange(ney + 1, device=AII.device)
+        out["Aed"] = Aee[:, k, :, k, :].permute(1, 0, 2, 3).contiguous()
+        out["Aeu"] = Aee[:, k[:-1], :, k[1:], :].permute(1, 0, 2, 3).contiguous()
+        out["Ael"] = Aee[:, k[1:], :, k[:-1], :].permute(1, 0, 2, 3).contiguous()
+        return out
+
+    def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
+        """Assemble on the device (HIP) and factor the Jacobian with the coefficients kw (the keywords of
+        device.Mesh.condensed_blocks / velocity_blocks): the condensed layout for the nested interior,
+        the dense column interiors for the "lu" / "inverse" variants."""
+        kw = dict(kw, ncomp=self.ncomp)
+        if self.P > 1 and self.interior == "nested":
+            return self.factor_condensed(lambda b, cols: mesh.condensed_blocks(b, cols=cols, **kw), budget_bytes)
+        return self.factor_from(lambda b, cols: mesh.velocity_blocks(b, cols=cols, **kw), budget_bytes)
+
+    def _alloc_factor(self):
+        """Storage of the nested factor.  On the GPU the blocks are kept column-major (the layout
+        sem_nested_solve reads) and the row-major names are transposed views of it."""
+        nex, ney, ne1 = self.nex, self.ney, self._ne1
+        ni, n_e = self._pi.shape[1], self._pe.numel()
+        z = dict(dtype=torch.float64, device=self.device)
+        shapes = ((nex, ney, ni, ni), (nex, ney, 2 * ne1, ni), (nex, ney, ni, 2 * ne1), (nex, n_e, n_e))
+        if self.device.type == "cuda":
+            T = [torch.empty(s[:-2] + (s[-1], s[-2]), **z) for s in shapes]
+            self._hipT = tuple(T)
+            self._Xi, self._Aei, self._Yie, self._Se_inv = (t.transpose(-1, -2) for t in T)
+        else:
+            self._hipT = None
+            self._Xi, self._Aei, self._Yie, self._Se_inv = (torch.empty(s, **z) for s in shapes)
+
+    def factor_condensed(self, fill, budget_bytes=24 << 30, pieces=None, line=None, chunk_cols=None):
+        """Factor from condensed pieces: fill(blocks, cols) writes the pieces of element columns cols and the
+        interface pieces (sem_condensed_blocks), a chunk of columns at a time within budget_bytes of work
+        memory; or pieces / line given directly (CPU, from condense_dense)."""
+        P, nex, ney, m = self.P, self.nex, self.ney, self.m
+        self._nested_index()
+        ne1 = self._ne1
+        ni, n_e = ne1 * (P - 1), (ney + 1) * ne1
+        per_col = 8 * (3 * ney * ni * ni + 6 * ney * ni * 2 * ne1 + 3 * n_e * n_e + 4 * n_e * 2 * m
+                       + 2 * ney * 2 * ne1 * 2 * m + 3 * (2 * m) ** 2)
+        chunk = nex if pieces is not None else max(1, min(nex, int(budget_bytes // per_col)))
+        if chunk_cols:
+            chunk = int(chunk_cols)
+        self._alloc_factor()
         S_diag = S_up = S_lo = None
         for c0 in range(0, nex, chunk):
             c1 = min(nex, c0 + chunk)
-            with self._phase("fill"):
-                blocks["AII"] = torch.zeros((c1 - c0, self.nI, self.nI), **z)
-                fill(blocks, (c0, c1))
-                AII = blocks.pop("AII")
-            Xi[c0:c1], Yie[c0:c1], Aei[c0:c1], Sinv[c0:c1] = self._nested_pieces(AII)
-            del AII
-            if S_diag is None:   # every fill writes the line pieces in full: take them from the first
-                aIB, aBI = blocks["aIB"], blocks["aBI"]
-                S_diag = blocks["D"].clone()
-                S_up, S_lo = torch.diag_embed(blocks["E"]), torch.diag_embed(blocks["F"])
-            self._Xi, self._Yie, self._Aei, self._Se_inv = Xi, Yie, Aei, Sinv
-            with self._phase("W"):
-                AIB = torch.diag_embed(aIB[c0:c1]).permute(0, 1, 3, 2, 4).reshape(c1 - c0, self.nI, 2 * m)
-                W = self._nested_solve(AIB, slice(c0, c1))
-                del AIB
+            if pieces is None:
+                with self._phase("fill"):
+                    if line is None:
+                        line = self.empty_blocks(with_interior=False)
+                    blk = dict(line)
+                    blk.update(self.condensed_empty(c1 - c0))
+                    fill(blk, (c0, c1))
+            else:
+                blk = dict(line)
+                blk.update(pieces)
+            if S_diag is None:   # every fill writes the interface pieces in full: take them from the first
+                aIB, aBI = blk["aIB"], blk["aBI"]
+                S_diag = blk["D"].clone()
+                S_up, S_lo = torch.diag_embed(blk["E"]), torch.diag_embed(blk["F"])
+            C = self._condense_chunk(blk, aIB, aBI, c0, c1)
+            del blk
             with self._phase("coupling"):
-                C = self._interface_coupling(aBI[c0:c1], W)
-                del W
-                S_diag[c0:c1] -= C[:, 0, :, 0, :]
-                S_diag[c0 + 1:c1 + 1] -= C[:, 1, :, 1, :]
-                S_up[c0:c1] -= C[:, 0, :, 1, :]
-                S_lo[c0:c1] -= C[:, 1, :, 0, :]
+                S_diag[c0:c1] -= C[:, :m, :m]
+                S_diag[c0 + 1:c1 + 1] -= C[:, m:, m:]
+                S_up[c0:c1] -= C[:, :m, m:]
+                S_lo[c0:c1] -= C[:, m:, :m]
                 del C
         self._nested_finish()
         self.W = None
         self.aBI, self.aIB = aBI, aIB
         with self._phase("sweep_factor"):
             self._sweep_factor(S_diag, S_up, S_lo)
+
+    def _group_perm(self):
+        """Interface-unknown order of the coupling products: groups G_0..G_{ney-1} ((s, c, j) each), then
+        H_0..H_ney ((s, c) each); returns, for every line-layout index s m + c N_y + gy, its group index."""
+        if getattr(self, "_gperm", None) is None:
+            P, ney, nc, NY, m = self.P, self.ney, self.ncomp, self.NY, self.m
+            dev = self.device
+            s = torch.arange(2, device=dev)
+            c = torch.arange(nc, device=dev)
+            n = torch.arange(ney, device=dev)
+            j = torch.arange(1, P, device=dev)
+            k = torch.arange(ney + 1, device=dev)
+            g_line = (s[None, :, None, None] * m + c[None, None, :, None] * NY + n[:, None, None, None] * P
+                      + j[None, None, None, :]).reshape(-1)
+            h_line = (s[None, :, None] * m + c[None, None, :] * NY + k[:, None, None] * P).reshape(-1)
+            lines = torch.cat((g_line, h_line))
+            inv = torch.empty_like(lines)
+            inv[lines] = torch.arange(lines.numel(), device=dev)
+            self._gperm = inv
+        return self._gperm
+
+    def _condense_chunk(self, blk, aIB, aBI, c0, c1):
+        """Factor pieces of columns [c0, c1) into the solver's arrays and their interface coupling
+        C = A_BI A_II^-1 A_IB (cc, 2m, 2m) in the line layout (s m + c N_y + gy)."""
+        P, ney, nc, NY, m = self.P, self.ney, self.ncomp, self.NY, self.m
+        ne1 = self._ne1
+        ni, n_e, G, cc = ne1 * (P - 1), (ney + 1) * ne1, 2 * ne1, c1 - c0
+        dev, f64 = self.device, torch.float64
+        Aii, Aie = blk["Aii"].view(cc, ney, ni, ni), blk["Aie"].view(cc, ney, ni, G)
+        Aei = blk["Aei"].view(cc, ney, G, ni)
+        with self._phase("inv_element"):
+            Xi = batched_inverse(Aii.reshape(-1, ni, ni)).view(cc, ney, ni, ni)
+        with self._phase("edge_schur"):
+            Yie = Xi @ Aie
+            Cee = Aei @ Yie                                   # (cc, ney, 2 ne1, 2 ne1): rows / cols edges n, n+1
+            Sd = blk["Aed"].view(cc, ney + 1, ne1, ne1).clone()
+            Sd[:, :-1] -= Cee[:, :, :ne1, :ne1]
+            Sd[:, 1:] -= Cee[:, :, ne1:, ne1:]
+            Su = blk["Aeu"].view(cc, ney, ne1, ne1) - Cee[:, :, :ne1, ne1:]
+            Sl = blk["Ael"].view(cc, ney, ne1, ne1) - Cee[:, :, ne1:, :ne1]
+            del Cee
+        with self._phase("inv_edge"):
+            Se_inv = self._blocktri_inverse(Sd, Su, Sl)
+        self._Xi[c0:c1], self._Yie[c0:c1], self._Aei[c0:c1], self._Se_inv[c0:c1] = Xi, Yie, Aei, Se_inv
+        with self._phase("coupling_pieces"):
+            eye_c = torch.eye(nc, dtype=f64, device=dev)
+            eye_j = torch.eye(P - 1, dtype=f64, device=dev)
+            gy_i = (torch.arange(ney, device=dev)[:, None] * P + torch.arange(1, P, device=dev)[None, :]).reshape(-1)
+            gy_e = torch.arange(ney + 1, device=dev) * P
+            vIB = aIB[c0:c1].view(cc, P - 1, 2, nc, NY)          # [e, l, s, c, gy]
+            vBI = aBI[c0:c1].view(cc, 2, P - 1, nc, NY)          # [e, s, l, c, gy]
+            # A_iB[e, n, (l c j), (s c' j')] and A_Bi[e, n, (s c j), (l c' j')], diagonal in (c, j)
+            a = vIB[..., gy_i].view(cc, P - 1, 2, nc, ney, P - 1)
+            AiB = torch.einsum("elscnj,cd,jk->enlcjsdk", a, eye_c, eye_j).reshape(cc, ney, ni, G)
+            b = vBI[..., gy_i].view(cc, 2, P - 1, nc, ney, P - 1)
+            ABi = torch.einsum("eslcnj,cd,jk->enscjldk", b, eye_c, eye_j).reshape(cc, ney, G, ni)
+            # A_eB[e, k, (l c), (s c')], A_Be[e, k, (s c), (l c')]
+            AeB = torch.einsum("elsck,cd->eklcsd", vIB[..., gy_e], eye_c).reshape(cc, ney + 1, ne1, 2 * nc)
+            ABe = torch.einsum("eslck,cd->ekscld", vBI[..., gy_e], eye_c).reshape(cc, ney + 1, 2 * nc, ne1)
+            XiB = Xi @ AiB                                     # (cc, ney, ni, G)
+            C_GG = ABi @ XiB                                   # (cc, ney, G, G)
+            ZeG = -(Aei @ XiB)                                 # rows: edges n, n+1
+            ZBG = -(ABi @ Yie)                                 # cols: edges n, n+1
+            del AiB, XiB, Xi, Yie
+        with self._phase("coupling_products"):
+            # V = S_e^-1 Z_e in the group order of the columns
+            SeW = Se_inv.unfold(2, G, ne1).permute(0, 2, 1, 3)           # (cc, ney, n_e, 2 ne1): edges n, n+1
+            VG = SeW @ ZeG                                                # (cc, ney, n_e, G)
+            SeH = Se_inv.view(cc, n_e, ney + 1, ne1).permute(0, 2, 1, 3)  # (cc, ney+1, n_e, ne1)
+            VH = SeH @ AeB                                                # (cc, ney+1, n_e, 2 nc)
+            V = torch.cat((VG.permute(0, 2, 1, 3).reshape(cc, n_e, ney * G),
+                           VH.permute(0, 2, 1, 3).reshape(cc, n_e, (ney + 1) * 2 * nc)), dim=2)
+            del VG, VH, SeW, SeH
+            # C = Z_B V (+ A_Bi Xi A_iB on the G diagonal blocks), rows in group order
+            Vw = V.unfold(1, G, ne1).transpose(-1, -2)                    # (cc, ney, 2 ne1, 2m): rows edges n, n+1
+            CG = ZBG @ Vw                                                 # (cc, ney, G, 2m)
+            CH = ABe @ V.view(cc, ney + 1, ne1, 2 * m)                    # (cc, ney+1, 2 nc, 2m)
+            del Vw, V
+            Cg = torch.cat((CG.reshape(cc, ney * G, 2 * m), CH.reshape(cc, (ney + 1) * 2 * nc, 2 * m)), dim=1)
+            del CG, CH
+            Cv = Cg[:, :ney * G, :ney * G].view(cc, ney, G, ney, G)
+            n = torch.arange(ney, device=dev)
+            Cv[:, n, :, n, :] += C_GG.permute(1, 0, 2, 3)
+            inv = self._group_perm()
+            return Cg[:, inv][:, :, inv]
+
+    def _blocktri_inverse(self, Sd, Su, Sl):
+        """Dense inverse of block-tridiagonal matrices (batched over columns): diagonal blocks Sd (cc, nb, b, b),
+        upper Su[k] (row block k, column block k+1), lower Sl[k] (row k+1, column k).  Block LU with pivoted
+        inverses of the pivot blocks, then the block-Thomas solve against the identity; the result is
+        checked through its residual S X - I (block-tridiagonal times dense: cheap) and a column whose
+        elimination without inter-block pivoting lost accuracy is inverted densely instead."""
+        cc, nb, b = Sd.shape[0], Sd.shape[1], Sd.shape[2]
+        n = nb * b
+        dev, f64 = Sd.device, Sd.dtype
+        if n <= self.edge_dense_max:   # small edge systems: one pivoted dense inverse per column
+            S = self._blocktri_dense(Sd, Su, Sl)
+            return batched_inverse(S)
+        # pivot-block inverses without raising: a singular or ill-conditioned pivot shows in the final check
+        inv = lambda A: torch.linalg.inv_ex(A)[0]  # noqa: E731
+        Dinv = torch.empty_like(Sd)
+        Uh = torch.empty_like(Su)
+        Dinv[:, 0] = inv(Sd[:, 0])
+        for k in range(1, nb):
+            Uh[:, k - 1] = Dinv[:, k - 1] @ Su[:, k - 1]
+            Dinv[:, k] = inv(Sd[:, k] - Sl[:, k - 1] @ Uh[:, k - 1])
+        X = torch.zeros((cc, nb, b, n), dtype=f64, device=dev)
+        # forward: Z_k = Dinv_k (I_k - Sl_{k-1} Z_{k-1}); Z_k is zero beyond column block k
+        X[:, 0, :, :b] = Dinv[:, 0]
+        for k in range(1, nb):
+            w = k * b
+            R = -(Sl[:, k - 1] @ X[:, k - 1, :, :w])
+            X[:, k, :, :w] = Dinv[:, k] @ R
+            X[:, k, :, w:w + b] = Dinv[:, k]
+        # back: X_k = Z_k - Uh_k X_{k+1}
+        for k in range(nb - 2, -1, -1):
+            X[:, k] -= Uh[:, k] @ X[:, k + 1]
+        X = X.view(cc, n, n)
+        res = self._blocktri_residual(Sd, Su, Sl, X)
+        bad = torch.nonzero(~(res <= 8.0 * n * n * torch.finfo(f64).eps)).flatten().tolist()
+        if bad:
+            S = self._blocktri_dense(Sd[bad], Su[bad], Sl[bad])
+            X[bad] = batched_inverse(S)
+        return X
+
+    @staticmethod
+    def _blocktri_dense(Sd, Su, Sl):
+        cc, nb, b = Sd.shape[0], Sd.shape[1], Sd.shape[2]
+        S = torch.zeros((cc, nb, b, nb, b), dtype=Sd.dtype, device=Sd.device)
+        k = torch.arange(nb, device=Sd.device)
+        S[:, k, :, k, :] = Sd.permute(1, 0, 2, 3)
+        S[:, k[:-1], :, k[1:], :] = Su.permute(1, 0, 2, 3)
+        S[:, k[1:], :, k[:-1], :] = Sl.permute(1, 0, 2, 3)
+        return S.view(cc, nb * b, nb * b)
+
+    @staticmethod
+    def _blocktri_residual(Sd, Su, Sl, X):
+        """max |S X - I| / (|S|max |X|max) per column, S block tridiagonal."""
+        cc, nb, b = Sd.shape[0], Sd.shape[1], Sd.shape[2]
+        Xb = X.view(cc, nb, b, nb * b)
+        R = Sd @ Xb
+        R[:, :-1] += Su @ Xb[:, 1:]
+        R[:, 1:] += Sl @ Xb[:, :-1]
+        Rv = R.view(cc, nb * b, nb * b)
+        Rv.diagonal(dim1=-2, dim2=-1).sub_(1.0)
+        smax = torch.maximum(torch.maximum(Sd.abs().amax(dim=(1, 2, 3)), Su.abs().amax(dim=(1, 2, 3))),
+                             Sl.abs().amax(dim=(1, 2, 3))) if nb > 1 else Sd.abs().amax(dim=(1, 2, 3))
+        return Rv.abs().amax(dim=(1, 2)) / (smax * X.abs().amax(dim=(1, 2)))
 
     def _interface_coupling(self, aBI, W):
         """C[e, s, r, t, k] = sum_l aBI[e, s, l, r] W[e, l, r, t, k]: A_BI A_II^-1 A_IB per column."""
@@ -212,19 +428,18 @@ class VelocityJacobianSolver:
     def factor(self, AII, D, aIB, aBI, E, F):
         """Condense and factor.  AII is consumed (its storage is reused for the LU factors)."""
         P, nex, m = self.P, self.nex, self.m
+        if P > 1 and self.interior == "nested":   # the condensed path, pieces taken from the dense blocks
+            pieces = self.condense_dense(AII)
+            del AII
+            return self.factor_condensed(None, pieces=pieces, line=dict(D=D, aIB=aIB, aBI=aBI, E=E, F=F))
         if P > 1:
             # dense A_IB (nex, nI, 2m): rows (l, r), column block s holds aIB[e, l, s, r] on its diagonal
             AIB = torch.diag_embed(aIB).permute(0, 1, 3, 2, 4).reshape(nex, self.nI, 2 * m)
-            if self.interior == "nested":
-                self._nested_factor(AII)
-                del AII
-                W = self._nested_solve(AIB)
-            else:
-                LU, piv, info = torch.linalg.lu_factor_ex(AII)
-                del AII
-                if int(info.max().item()) > 0:
-                    raise RuntimeError("velocity Jacobian: singular interior block")
-                W = torch.linalg.lu_solve(LU, piv, AIB)
+            LU, piv, info = torch.linalg.lu_factor_ex(AII)
+            del AII
+            if int(info.max().item()) > 0:
+                raise RuntimeError("velocity Jacobian: singular interior block")
+            W = torch.linalg.lu_solve(LU, piv, AIB)
             del AIB
             C = self._interface_coupling(aBI, W)   # A_BI W for both interface lines
             S_diag = D.clone()
@@ -240,7 +455,7 @@ class VelocityJacobianSolver:
                 self.LU = self.piv = None
             elif self.interior == "lu":
                 self.LU, self.piv = LU, piv
-            self.W = W.view(nex, self.nI, 2, m) if self.interior != "nested" else None
+            self.W = W.view(nex, self.nI, 2, m)
             self.aBI, self.aIB = aBI, aIB
         else:
             S_diag, S_up, S_lo = D, torch.diag_embed(E), torch.diag_embed(F)
@@ -398,40 +613,11 @@ class VelocityJacobianSolver:
         self._pe = pe.reshape(-1)                                       # (n_e,)
         self._pe_el = torch.cat((pe[:-1].reshape(ney, -1), pe[1:].reshape(ney, -1)), dim=1)  # edges k=n, n+1
 
-    def _nested_pieces(self, AII):
-        """Element-interior inverses Xi, Xi A_ie, A_ei and the inverse edge Schur blocks of the
-        columns whose dense interiors AII holds."""
-        nex, ney = AII.shape[0], self.ney
-        pi, pe, pel = self._pi, self._pe, self._pe_el
-        e = torch.arange(nex, device=self.device)[:, None, None, None]
-        with self._phase("gather"):
-            A_ii = AII[e, pi[None, :, :, None], pi[None, :, None, :]]     # (nex, ney, ni, ni)
-            A_ie = AII[e, pi[None, :, :, None], pel[None, :, None, :]]    # (nex, ney, ni, 2 ne1)
-            A_ei = AII[e, pel[None, :, :, None], pi[None, :, None, :]]    # (nex, ney, 2 ne1, ni)
-            S_e = AII[e[:, :, 0], pe[None, :, None], pe[None, None, :]]   # (nex, n_e, n_e)
-        with self._phase("inv_element"):
-            Xi = batched_inverse(A_ii.reshape(-1, *A_ii.shape[-2:])).view(A_ii.shape)
-        with self._phase("edge_schur"):
-            Yie = Xi @ A_ie
-            C = (A_ei @ Yie).view(nex, ney, 2, self._ne1, 2, self._ne1)
-            S = S_e.view(nex, ney + 1, self._ne1, ney + 1, self._ne1)
-            n = torch.arange(ney, device=self.device)
-            for a in range(2):          # element n touches edge rows k = n + a, columns k = n + b
-                for b in range(2):
-                    S[:, n + a, :, n + b, :] -= C[:, :, a, :, b, :].permute(1, 0, 2, 3)  # index dims lead
-        with self._phase("inv_edge"):
-            Se_inv = batched_inverse(S_e)
-        return Xi, Yie, A_ei, Se_inv
-
-    def _nested_factor(self, AII):
-        self._nested_index()
-        self._Xi, self._Yie, self._Aei, self._Se_inv = self._nested_pieces(AII)
-        self._nested_finish()
-
     def _nested_finish(self):
         if self.device.type == "cuda":   # column-major blocks for sem_nested_solve (ns_condense.hip)
-            self._hipT = tuple(t.transpose(-1, -2).contiguous() for t in
-                               (self._Xi, self._Aei, self._Yie, self._Se_inv))
+            if getattr(self, "_hipT", None) is None:
+                self._hipT = tuple(t.transpose(-1, -2).contiguous() for t in
+                                   (self._Xi, self._Aei, self._Yie, self._Se_inv))
             self._pi, self._pe = self._pi.contiguous(), self._pe.contiguous()
 
     def _nested_solve(self, R, cols=slice(None)):

@@ -55,10 +55,11 @@ def test_cfg4_coupled_residual_matches_oracle(cfg4):
     # converged: the residual is round-off of terms of order |Sys||x|; both sides agree far below atol
     assert np.abs(R[idx] - want).max() <= 1e-3 * c.atol_nonlin
     assert abs(np.linalg.norm(R) - float(fx["R_norm"])) <= 1e-3 * c.atol_nonlin
-    # live oracle on the full vector, and at a seeded perturbation where R is O(|Sys||x|): the 1e-13 bar
+    # live oracle on the full vector at a seeded 10 % perturbation of the state, where R is of the order of
+    # the operator terms (no cancellation to the converged round-off): the 1e-13 bar of SURVEY 8c
     o_cd, o_ns = cfg4["cd"], cfg4["ns"]
     r = np.random.default_rng(45)
-    xp = x * (1.0 + 1e-3 * r.uniform(-1, 1, x.size))
+    xp = x * (1.0 + 0.1 * r.uniform(-1, 1, x.size))
     Rp = c.residuals(xp)
     Tp, up, vp, pp = (xp[i * N:(i + 1) * N] for i in range(4))
     blocks = (o_cd.residuals(Tp, up, vp),) + tuple(o_ns.residuals(up, vp, pp, Tp))

@@ -33,14 +33,14 @@ def test_fused_residuals_match_oracle(gpu, P, nex, ney, Re, Gr):
     got = ns._get_residuals(u, v, p, T)
     want = ref.residuals(u, v, p, T)
     for a, b in zip(got, want):
-        assert _rel(a, b) < 1e-12
+        assert _rel(a, b) < 1e-13
     ref.calc_jacobians(u, v)
     ns._calc_jacobians(u, v)
     for t in (dT, None):
         got = ns._get_dresiduals(du, dv, dp, t)
         want = ref.dresiduals(du, dv, dp, t)
         for a, b in zip(got, want):
-            assert _rel(a, b) < 1e-12
+            assert _rel(a, b) < 1e-13
 
 
 def test_pin_on_the_boundary_follows_the_statement_order(gpu):

@@ -170,12 +170,12 @@ def test_block_gemv_wide_and_narrow(gpu, nb, m, S):
     assert (y - want).abs().max().item() <= 1e-12 * want.abs().max().item()
 
 
-@pytest.mark.parametrize("P,nex,ney,Re", [(4, 8, 3, 700.0), (6, 5, 2, 1000.0)])
-def test_column_ranged_blocks_and_chunked_factor(gpu, P, nex, ney, Re):
-    """sem_velocity_blocks with an A_II column range (ABI 6) writes exactly those columns' dense
-    interiors and every other piece in full; the column-chunked factorisation it feeds (the cfg5 path,
-    VelocityJacobianSolver.factor_from below its memory budget) solves the Jacobian like the one-shot
-    factorisation."""
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 8, 3, 700.0), (6, 5, 2, 1000.0), (12, 3, 2, 1000.0), (2, 6, 5, 300.0)])
+def test_condensed_blocks_and_chunked_factor(gpu, P, nex, ney, Re):
+    """sem_condensed_blocks (ABI 7) writes, for an element-column range, exactly (bitwise) the condensed
+    pieces of the dense column interiors sem_velocity_blocks writes, and the interface pieces in full; the
+    column-chunked condensed factorisation (factor_mesh with a budget below one column, the cfg5 path),
+    with the edge Schur blocks inverted densely or by the checked block LU, solves like SciPy."""
     from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
     ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
     ns = _device_solver(P, nex, ney, Re, u, v)
@@ -184,25 +184,30 @@ def test_column_ranged_blocks_and_chunked_factor(gpu, P, nex, ney, Re):
     vs = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
     full = vs.empty_blocks()
     ns._mesh.velocity_blocks(full, **kw)
-    for c0, c1 in ((0, 1), (2, 5), (nex - 1, nex)):
+    want = vs.condense_dense(full["AII"])
+    for c0, c1 in ((0, 1), (1, nex), (nex - 1, nex)):
         part = vs.empty_blocks(with_interior=False)
-        part["AII"] = torch.zeros((c1 - c0, vs.nI, vs.nI), dtype=torch.float64, device=ns._mesh.device)
+        part.update(vs.condensed_empty(c1 - c0))
         part["aIB"].fill_(7.0)   # every piece is rewritten
-        ns._mesh.velocity_blocks(part, cols=(c0, c1), **kw)
-        assert torch.equal(part["AII"], full["AII"][c0:c1])
+        for k in vs.condensed_empty(1):
+            part[k].fill_(5.0)   # and zeroed first
+        ns._mesh.condensed_blocks(part, cols=(c0, c1), **kw)
+        for k, w in want.items():
+            assert torch.equal(part[k], w[c0:c1]), k
         for k in ("D", "aIB", "aBI", "E", "F"):
             assert torch.equal(part[k], full[k]), k
     with pytest.raises(ValueError):
-        ns._mesh.velocity_blocks(full, cols=(3, 3), **kw)
-    ch = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
-    per_col = ch.nI * ch.nI * 8 + 3 * ch.nI * 2 * ch.m * 8
-    ch.factor_from(lambda b, cols: ns._mesh.velocity_blocks(b, cols=cols, **kw), budget_bytes=2 * per_col)
+        ns._mesh.condensed_blocks(part, cols=(2, 2), **kw)
     r = np.random.default_rng(3)
     bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
-    xu, xv = ch.solve(ns._dev(bu), ns._dev(bv))
-    got = np.hstack((xu.cpu().numpy(), xv.cpu().numpy()))
-    want = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
-    assert np.abs(got - want).max() <= 1e-9 * np.abs(want).max()
+    sol = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
+    for edge_dense_max in (1024, 0):
+        ch = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
+        ch.edge_dense_max = edge_dense_max
+        ch.factor_mesh(ns._mesh, budget_bytes=1, **kw)
+        xu, xv = ch.solve(ns._dev(bu), ns._dev(bv))
+        got = np.hstack((xu.cpu().numpy(), xv.cpu().numpy()))
+        assert np.abs(got - sol).max() <= 1e-9 * np.abs(sol).max()
 
 
 def test_interface_sweep_batched_gemv_fallback(gpu, monkeypatch):

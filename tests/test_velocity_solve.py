@@ -60,29 +60,52 @@ def test_scalar_condensation_solves_the_cd_jacobian(P, nex, ney, Pe, sweep):
         vs.solve(torch.as_tensor(b), torch.as_tensor(b))
 
 
-@pytest.mark.parametrize("P,nex,ney,Re", [(4, 5, 2, 100.0), (3, 6, 2, 50.0), (6, 3, 2, 1000.0)])
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 5, 2, 100.0), (3, 6, 2, 50.0), (6, 3, 2, 1000.0), (5, 4, 7, 400.0)])
 @pytest.mark.parametrize("chunk_cols", [1, 2])
-def test_column_chunked_factor_matches_one_shot(P, nex, ney, Re, chunk_cols):
-    """factor_from with a budget of chunk_cols columns (the cfg5 path: dense interiors assembled,
-    condensed and freed a chunk at a time, sem_velocity_blocks' col_begin/col_end) gives the solve of
-    the one-shot factorisation."""
+@pytest.mark.parametrize("edge", ["dense", "blocklu"])
+def test_condensed_chunked_factor_matches_sparse_lu(P, nex, ney, Re, chunk_cols, edge):
+    """factor_condensed (the ABI-7 path: the condensed pieces of chunk_cols element columns at a time,
+    sem_condensed_blocks' col_begin/col_end contract) solves the Jacobian; the edge Schur blocks inverted
+    densely or by the checked block LU of their block-tridiagonal form."""
     ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
     pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
+    ch = VelocityJacobianSolver(P, nex, ney, "cpu")
+    cond = ch.condense_dense(pcs["AII"])
 
-    def fill(blocks, cols):   # the kernel's contract: A_II of columns cols, every other piece in full
+    def fill(blocks, cols):   # the kernel's contract: condensed pieces of columns cols, line pieces in full
         c0, c1 = cols
         for k in ("D", "aIB", "aBI", "E", "F"):
             blocks[k].copy_(pcs[k])
-        blocks["AII"].copy_(pcs["AII"][c0:c1])
+        for k, v in cond.items():
+            blocks[k].copy_(v[c0:c1])
 
-    one = VelocityJacobianSolver(P, nex, ney, "cpu")
-    one.factor(pcs["AII"].clone(), pcs["D"], pcs["aIB"], pcs["aBI"], pcs["E"], pcs["F"])
-    ch = VelocityJacobianSolver(P, nex, ney, "cpu")
-    nI, m = ch.nI, ch.m
-    ch.factor_from(fill, budget_bytes=chunk_cols * (nI * nI * 8 + 3 * nI * 2 * m * 8))
+    if edge == "blocklu":
+        ch.edge_dense_max = 0
+    ch.factor_condensed(fill, chunk_cols=chunk_cols)
     r = np.random.default_rng(9)
     bu, bv = (torch.as_tensor(r.uniform(-1, 1, ns.N)) for _ in range(2))
     want = spla.spsolve(ns.Jvelo.tocsc(), np.hstack((bu.numpy(), bv.numpy())))
-    for s in (ch, one):   # the same factor up to the summation order of the interface blocks
-        got = np.hstack([t.numpy() for t in s.solve(bu, bv)])
-        assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
+    got = np.hstack([t.numpy() for t in ch.solve(bu, bv)])
+    assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
+
+
+@pytest.mark.parametrize("nb,b,seed", [(1, 3, 0), (2, 5, 1), (9, 4, 2), (30, 6, 3)])
+def test_block_tridiagonal_inverse(nb, b, seed):
+    """_blocktri_inverse (block LU with pivoted pivot-block inverses, then block Thomas against I) equals the
+    dense inverse; a column that needs inter-block pivoting (a singular leading block) is detected by the
+    residual check and inverted densely."""
+    r = np.random.default_rng(seed)
+    cc = 3
+    Sd = torch.as_tensor(r.uniform(-1, 1, (cc, nb, b, b)) + 4 * b * np.eye(b))
+    Su = torch.as_tensor(r.uniform(-1, 1, (cc, nb - 1, b, b)))
+    Sl = torch.as_tensor(r.uniform(-1, 1, (cc, nb - 1, b, b)))
+    if nb > 1:
+        Sd[1, 0] = 0.0   # zero first pivot block: the block LU fails, the dense pivoted inverse does not
+        Su[1, 0] = torch.eye(b, dtype=torch.float64) * 3
+        Sl[1, 0] = torch.eye(b, dtype=torch.float64) * 2
+    vs = VelocityJacobianSolver(2, 1, 1, "cpu")
+    vs.edge_dense_max = 0
+    X = vs._blocktri_inverse(Sd, Su, Sl)
+    S = VelocityJacobianSolver._blocktri_dense(Sd, Su, Sl)
+    want = torch.linalg.inv(S)
+    assert torch.allclose(X, want, rtol=0, atol=1e-10 * want.abs().max().item())
