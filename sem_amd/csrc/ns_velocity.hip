@@ -44,6 +44,7 @@ struct VelocityArgs {
   int P, nex, ney, NY, NX;
   int nc;  // components per node: 2 (NS velocity [u | v]) or 1 (a scalar operator, e.g. the CD Jacobian)
   int c0, c1;  // element columns whose A_II blocks are written (A_II indexed from c0)
+  int eb, ee, lb0, lb1;  // element columns / global lines of the handle's strip (whole mesh: 0, nex, 0, NX-1)
   unsigned sides;
   double *AII, *D, *aIB, *aBI, *E, *F;
   // ABI 7, condensed layout of the interior rows of columns [c0, c1) (instead of the dense AII):
@@ -56,7 +57,7 @@ struct VelocityArgs {
 };
 
 __device__ __forceinline__ bool is_dirichlet(const VelocityArgs& a, int gx, int gy) {
-  if (a.mask) return a.mask[static_cast<int64_t>(gx) * a.NY + gy] != 0;
+  if (a.mask) return a.mask[static_cast<int64_t>(gx - a.lb0) * a.NY + gy] != 0;
   return ((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
          ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1);
 }
@@ -65,13 +66,12 @@ __device__ __forceinline__ bool is_dirichlet(const VelocityArgs& a, int gx, int 
 // its x couplings (the other interior lines of the column, same c and gy), y couplings (its line's nodes
 // in the element(s) holding gy), the other component at the node, and the diagonal, each written to the
 // block that holds the pair; the interface couplings go to aIB as in the dense layout.
-__device__ void condensed_row(const VelocityArgs& a, int L, int l, int c, int gy, int r, bool dir, double mx,
-                              double my, double cu, double cv, const double* Ks, const double* Gs) {
+__device__ void condensed_row(const VelocityArgs& a, int L, int l, int c, int gy, int r, int64_t node, bool dir,
+                              double mx, double my, double cu, double cv, const double* Ks, const double* Gs) {
   const int P = a.P, n = P + 1, nc = a.nc, ne1 = nc * (P - 1), ni = ne1 * (P - 1);
   const int ey = gy / P, j = gy - ey * P;
   const int64_t col = L - a.c0;
-  const int64_t node = static_cast<int64_t>(L * P + l) * a.NY + gy;
-  double* ib = a.aIB + (static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 * a.nc * a.NY + r;
+  double* ib = a.aIB + (static_cast<int64_t>(L - a.eb) * (P - 1) + l - 1) * 2 * a.nc * a.NY + r;
   const int mm = nc * a.NY;
   const double fx = a.fKx * my, gxc = a.fX * cu * my;
   const double fy = a.fKy * mx, gyc = a.fY * cv * mx;
@@ -149,25 +149,32 @@ __device__ void condensed_row(const VelocityArgs& a, int L, int l, int c, int gy
   Dr[lc] = dg;
 }
 
-// One thread per Jacobian row: row = line gx (0..NX-1), component c, node gy.
+// One thread per Jacobian row: row = line gx (the handle's lines lb0..lb1), component c, node gy.  On an
+// element-column strip handle (the partitioned solvers) the x sums run over the strip's own columns
+// [eb, ee): the strip's two interface lines get the partial rows of its side (their sums over the two
+// strips are the whole-mesh rows), and the pointwise Jacobian terms and Dirichlet identity rows of the
+// right interface line are left to the strip on its right (the rule of the apply kernels).
 __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs a) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int NY = a.NY, P = a.P, n = P + 1, m = a.nc * NY;
-  if (t >= static_cast<int64_t>(a.NX) * m) return;
-  const int gx = static_cast<int>(t / m), r = static_cast<int>(t - static_cast<int64_t>(gx) * m);
+  if (t >= static_cast<int64_t>(a.lb1 - a.lb0 + 1) * m) return;
+  const int lx = static_cast<int>(t / m), r = static_cast<int>(t - static_cast<int64_t>(lx) * m);
+  const int gx = a.lb0 + lx;
   const int c = r / NY, gy = r - c * NY;
   const double* Ks = a.tab;
   const double* Gs = a.tab + n * n;
   const double* w = a.tab + 2 * n * n;
   const int L = gx / P, l = gx - L * P;  // interface line L (l == 0) or interior line l of column L
-  const int64_t node = static_cast<int64_t>(gx) * NY + gy;
+  const int Ll = L - a.eb;               // the strip's local line / column index
+  const int64_t node = static_cast<int64_t>(lx) * NY + gy;
   const bool dir = is_dirichlet(a, gx, gy);
+  const bool own = !(gx == a.lb1 && a.ee < a.nex);  // the strip's right interface line: its right owner's
   const int nI = (P - 1) * m;
   // row pointer into the dense block holding this row, and the column offset of line-local node 0
   double* row;
   int64_t col0;  // column index of (this line, c = 0, gy = 0) within the block
   if (l != 0 && (L < a.c0 || L >= a.c1)) {  // interior row of a column outside the A_II range: aIB only
-    double* ib = a.aIB + (static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 * m + r;
+    double* ib = a.aIB + (static_cast<int64_t>(Ll) * (P - 1) + l - 1) * 2 * m + r;
     if (dir) {
       ib[0] = 0.0;
       ib[m] = 0.0;
@@ -185,35 +192,35 @@ __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs
     const int ey = gy / P, j = gy - ey * P;
     const double mx = w[l];
     const double my = j != 0 ? w[j] : (ey > 0 ? w[P] : 0.0) + (ey < a.ney ? w[0] : 0.0);
-    condensed_row(a, L, l, c, gy, r, dir, mx, my, a.cu ? a.cu[node] : 1.0, a.cv ? a.cv[node] : 1.0, Ks, Gs);
+    condensed_row(a, L, l, c, gy, r, node, dir, mx, my, a.cu ? a.cu[node] : 1.0, a.cv ? a.cv[node] : 1.0, Ks, Gs);
     return;
   }
   if (l == 0) {
-    row = a.D + (static_cast<int64_t>(L) * m + r) * m;
+    row = a.D + (static_cast<int64_t>(Ll) * m + r) * m;
     col0 = 0;
   } else {
     row = a.AII + (static_cast<int64_t>(L - a.c0) * nI + (l - 1) * m + r) * nI;
     col0 = static_cast<int64_t>(l - 1) * m;
   }
   const int64_t self = col0 + r;
-  if (dir) {  // identity row: no coupling to anything else
-    row[self] = 1.0;
+  if (dir) {  // identity row (its owner's): no coupling to anything else
+    if (own) row[self] = 1.0;
     if (l == 0) {
-      if (L < a.nex) {
-        a.E[static_cast<int64_t>(L) * m + r] = 0.0;
-        for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L) * 2 + 0) * (P - 1) + k - 1) * m + r] = 0.0;
+      if (L < a.ee) {
+        a.E[static_cast<int64_t>(Ll) * m + r] = 0.0;
+        for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(Ll) * 2 + 0) * (P - 1) + k - 1) * m + r] = 0.0;
       }
-      if (L > 0) {
-        a.F[static_cast<int64_t>(L - 1) * m + r] = 0.0;
-        for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L - 1) * 2 + 1) * (P - 1) + k - 1) * m + r] = 0.0;
+      if (L > a.eb) {
+        a.F[static_cast<int64_t>(Ll - 1) * m + r] = 0.0;
+        for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(Ll - 1) * 2 + 1) * (P - 1) + k - 1) * m + r] = 0.0;
       }
     } else {
-      for (int s = 0; s < 2; ++s) a.aIB[((static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 + s) * m + r] = 0.0;
+      for (int s = 0; s < 2; ++s) a.aIB[((static_cast<int64_t>(Ll) * (P - 1) + l - 1) * 2 + s) * m + r] = 0.0;
     }
     return;
   }
-  // assembled weights of this node's line (x) and column (y)
-  const double mx = l != 0 ? w[l] : (L > 0 ? w[P] : 0.0) + (L < a.nex ? w[0] : 0.0);
+  // assembled weights of this node's line (x, over the strip's columns) and column (y)
+  const double mx = l != 0 ? w[l] : (L > a.eb ? w[P] : 0.0) + (L < a.ee ? w[0] : 0.0);
   const int ey = gy / P, j = gy - ey * P;
   const double my = j != 0 ? w[j] : (ey > 0 ? w[P] : 0.0) + (ey < a.ney ? w[0] : 0.0);
   const double cu = a.cu ? a.cu[node] : 1.0, cv = a.cv ? a.cv[node] : 1.0;
@@ -222,13 +229,14 @@ __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs
   auto xk = [&](int i, int k) { return fx * Ks[i * n + k] + gxc * Gs[i * n + k]; };
   auto yk = [&](int i, int k) { return fy * Ks[i * n + k] + gyc * Gs[i * n + k]; };
 
-  // diagonal: x part + y part + mass + the Jacobian's own diagonal term
-  double dg = a.fM * mx * my + (c == 0 ? (a.juu ? a.juu[node] : 0.0) : (a.jvv ? a.jvv[node] : 0.0));
+  // diagonal: x part + y part + mass + the Jacobian's own diagonal term (its owner's)
+  double dg = a.fM * mx * my;
+  if (own) dg += c == 0 ? (a.juu ? a.juu[node] : 0.0) : (a.jvv ? a.jvv[node] : 0.0);
   if (l != 0) {
     dg += xk(l, l);
   } else {
-    if (L > 0) dg += xk(P, P);
-    if (L < a.nex) dg += xk(0, 0);
+    if (L > a.eb) dg += xk(P, P);
+    if (L < a.ee) dg += xk(0, 0);
   }
   // y coupling along the line (same component): elements ey-1 (row P) and ey (row j)
   const int64_t yb = col0 + static_cast<int64_t>(c) * NY;  // column of (this line, c, gy = 0)
@@ -251,7 +259,7 @@ __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs
   }
   row[self] += dg;
   // the other component at the same node: J_uv = diag(juv) (u rows), J_vu = diag(jvu) (v rows)
-  if (a.nc == 2) {
+  if (a.nc == 2 && own) {
     const double* jc = c == 0 ? a.juv : a.jvu;
     if (jc) row[col0 + (1 - c) * NY + gy] = jc[node];
   }
@@ -261,15 +269,15 @@ __global__ __launch_bounds__(256) void velocity_blocks_kernel(const VelocityArgs
     double* AIIrow = row;
     for (int k = 1; k < P; ++k)
       if (k != l) AIIrow[static_cast<int64_t>(k - 1) * m + r] = xk(l, k);
-    for (int s = 0; s < 2; ++s) a.aIB[((static_cast<int64_t>(L) * (P - 1) + l - 1) * 2 + s) * m + r] = xk(l, s * P);
+    for (int s = 0; s < 2; ++s) a.aIB[((static_cast<int64_t>(Ll) * (P - 1) + l - 1) * 2 + s) * m + r] = xk(l, s * P);
   } else {
-    if (L < a.nex) {  // left line of column L
-      for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L) * 2 + 0) * (P - 1) + k - 1) * m + r] = xk(0, k);
-      a.E[static_cast<int64_t>(L) * m + r] = xk(0, P);
+    if (L < a.ee) {  // left line of column L
+      for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(Ll) * 2 + 0) * (P - 1) + k - 1) * m + r] = xk(0, k);
+      a.E[static_cast<int64_t>(Ll) * m + r] = xk(0, P);
     }
-    if (L > 0) {  // right line of column L-1
-      for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(L - 1) * 2 + 1) * (P - 1) + k - 1) * m + r] = xk(P, k);
-      a.F[static_cast<int64_t>(L - 1) * m + r] = xk(P, 0);
+    if (L > a.eb) {  // right line of column L-1
+      for (int k = 1; k < P; ++k) a.aBI[((static_cast<int64_t>(Ll - 1) * 2 + 1) * (P - 1) + k - 1) * m + r] = xk(P, k);
+      a.F[static_cast<int64_t>(Ll - 1) * m + r] = xk(P, 0);
     }
   }
 }
@@ -286,9 +294,8 @@ extern "C" {
 int sem_line_block_sizes(const sem_handle* h, int ncomp, int64_t* sizes) {
   if (!h || !sizes) return sem::set_error(SEM_EINVAL, "null argument");
   if (ncomp != 1 && ncomp != 2) return sem::set_error(SEM_EINVAL, "ncomp must be 1 or 2");
-  if (h->ex_begin != 0 || h->ex_end != h->nex)
-    return sem::set_error(SEM_EUNSUPPORTED, "the velocity blocks need a whole-mesh handle");
-  const int64_t m = ncomp * h->NY, nI = static_cast<int64_t>(h->P - 1) * m, ne = h->nex;
+  // ABI 7: a strip handle's pieces cover its own element columns and lines
+  const int64_t m = ncomp * h->NY, nI = static_cast<int64_t>(h->P - 1) * m, ne = h->ex_end - h->ex_begin;
   sizes[0] = ne * nI * nI;             // A_II
   sizes[1] = (ne + 1) * m * m;         // D
   sizes[2] = ne * (h->P - 1) * 2 * m;  // aIB
@@ -321,8 +328,6 @@ static int velocity_blocks_impl(sem_handle* h, const sem_velocity_desc* d, doubl
   if (cond)
     for (int i = 0; i < 6; ++i)
       if (!cond[i]) return sem::set_error(SEM_EINVAL, "null condensed block");
-  if (h->ex_begin != 0 || h->ex_end != h->nex)
-    return sem::set_error(SEM_EUNSUPPORTED, "the velocity blocks need a whole-mesh handle");
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess || cur != h->device)
     return sem::set_error(SEM_EINVAL, "handle belongs to another device than the current one");
@@ -330,8 +335,10 @@ static int velocity_blocks_impl(sem_handle* h, const sem_velocity_desc* d, doubl
   if (nc != 1 && nc != 2) return sem::set_error(SEM_EINVAL, "ncomp must be 0, 1 or 2");
   if (nc == 1 && (d->juv || d->jvu || d->jvv))
     return sem::set_error(SEM_EINVAL, "a one-component operator has no juv / jvu / jvv term");
-  const int c0 = d->col_begin, c1 = d->col_end == 0 ? h->nex : d->col_end;
-  if (c0 < 0 || c1 > h->nex || c0 >= c1) return sem::set_error(SEM_EINVAL, "bad A_II column range");
+  // column range in global element columns, inside the handle's strip (col_end 0: to its end)
+  const int c0 = d->col_end == 0 && d->col_begin == 0 ? h->ex_begin : d->col_begin;
+  const int c1 = d->col_end == 0 ? h->ex_end : d->col_end;
+  if (c0 < h->ex_begin || c1 > h->ex_end || c0 >= c1) return sem::set_error(SEM_EINVAL, "bad A_II column range");
   int64_t sz[6];
   sem_line_block_sizes(h, nc, sz);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -343,7 +350,7 @@ static int velocity_blocks_impl(sem_handle* h, const sem_velocity_desc* d, doubl
       if ((st = sem::hip_check_v(hipMemsetAsync(cond[i], 0, cs[i] * (c1 - c0) * sizeof(double), s), "memset blocks")))
         return st;
   } else {
-    const int64_t szA = sz[0] / h->nex * (c1 - c0);
+    const int64_t szA = sz[0] / (h->ex_end - h->ex_begin) * (c1 - c0);
     if (h->P > 1 && (st = sem::hip_check_v(hipMemsetAsync(AII, 0, szA * sizeof(double), s), "memset A_II")))
       return st;
   }
@@ -371,6 +378,10 @@ static int velocity_blocks_impl(sem_handle* h, const sem_velocity_desc* d, doubl
   a.nc = nc;
   a.c0 = c0;
   a.c1 = c1;
+  a.eb = h->ex_begin;
+  a.ee = h->ex_end;
+  a.lb0 = static_cast<int>(h->line_begin);
+  a.lb1 = static_cast<int>(h->line_end);
   a.AII = AII;
   a.D = D;
   a.aIB = aIB;
@@ -386,7 +397,7 @@ static int velocity_blocks_impl(sem_handle* h, const sem_velocity_desc* d, doubl
     a.Aeu = cond[4];
     a.Ael = cond[5];
   }
-  const int64_t rows = h->NX * nc * h->NY;
+  const int64_t rows = (h->line_end - h->line_begin + 1) * nc * h->NY;
   hipLaunchKernelGGL(sem::velocity_blocks_kernel, dim3(static_cast<unsigned>((rows + 255) / 256)), dim3(256), 0, s, a);
   return sem::hip_check_v(hipGetLastError(), "velocity blocks launch");
 }

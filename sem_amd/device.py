@@ -152,10 +152,10 @@ class Mesh:
         sizes = (C.c_int64 * 6)()
         _lib.check(self._lib.sem_line_block_sizes(self._h, int(ncomp), sizes))
         names = ("AII", "D", "aIB", "aBI", "E", "F")
-        c0, c1 = (0, self.nex) if cols is None else (int(cols[0]), int(cols[1]))
-        if not 0 <= c0 < c1 <= self.nex:
-            raise ValueError("cols must be a non-empty element-column range")
-        sizes[0] = sizes[0] // self.nex * (c1 - c0)
+        c0, c1 = (self.ex_begin, self.ex_end) if cols is None else (int(cols[0]), int(cols[1]))
+        if not self.ex_begin <= c0 < c1 <= self.ex_end:
+            raise ValueError("cols must be a non-empty element-column range of the handle's strip")
+        sizes[0] = sizes[0] // (self.ex_end - self.ex_begin) * (c1 - c0)
         for nm, sz in zip(names, sizes):
             t = blocks.get(nm)
             if sz and (t is None or t.numel() != sz or t.dtype != torch.float64 or t.device != self.device
@@ -178,9 +178,9 @@ class Mesh:
             self._vec(t, nm)
         if dir_mask is not None and (dir_mask.dtype != torch.uint8 or dir_mask.numel() != self.n_local):
             raise ValueError("dir_mask must be a uint8 tensor of n_local entries")
-        c0, c1 = (0, self.nex) if cols is None else (int(cols[0]), int(cols[1]))
-        if not 0 <= c0 < c1 <= self.nex:
-            raise ValueError("cols must be a non-empty element-column range")
+        c0, c1 = (self.ex_begin, self.ex_end) if cols is None else (int(cols[0]), int(cols[1]))
+        if not self.ex_begin <= c0 < c1 <= self.ex_end:
+            raise ValueError("cols must be a non-empty element-column range of the handle's strip")
         line = (C.c_int64 * 6)()
         _lib.check(self._lib.sem_line_block_sizes(self._h, int(ncomp), line))
         cs = (C.c_int64 * 6)()

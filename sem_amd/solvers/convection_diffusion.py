@@ -97,17 +97,19 @@ class ConvectionDiffusionSolver:
         global NumPy vectors (local strips when given device tensors).
         partition_update: how a partitioned solver solves its Newton update -- "distributed": the
         device GMRES over the strips (every matvec a strip apply + exchange, inner products
-        all-reduced; unpreconditioned, as there is no whole-mesh factor); "central": the Sys velocity
-        field and the right-hand side are gathered, rank 0's whole-mesh counterpart
-        (_central_solver) solves with the condensed direct preconditioner, the update is broadcast."""
+        all-reduced), right-preconditioned by the element-partitioned condensed direct solve of the
+        Jacobian (strip_solve.StripLineSolver: each rank factors its own columns, the ranks share a
+        reduced system over the strip-boundary lines); "central": the Sys velocity field and the
+        right-hand side are gathered, rank 0's whole-mesh counterpart (_central_solver) solves with
+        the condensed direct preconditioner, the update is broadcast."""
         if krylov not in ("device", "scipy"):
             raise ValueError("krylov must be 'device' or 'scipy'")
         if partition is not None and krylov != "device":
             raise ValueError("a partitioned solver needs krylov='device'")
         if precond not in ("condensed", None):
             raise ValueError("precond must be 'condensed' or None")
-        # the condensation needs the whole mesh on one device; a partitioned solver runs plain GMRES
-        self._precond = precond if partition is None else None
+        # a partitioned solver preconditions with the element-partitioned condensation (strip_solve.py)
+        self._precond = precond
         if partition_update not in ("distributed", "central"):
             raise ValueError("partition_update must be 'distributed' or 'central'")
         self._partition_update = partition_update
@@ -221,13 +223,20 @@ class ConvectionDiffusionSolver:
 
     def _jacobian_solver(self):
         """Direct solve of dres_op = Sys with Dirichlet identity rows (ConvectionDiffusion_Solver.py:
-        104-121 at du = dv = 0): sem_velocity_blocks with one component writes the condensation
-        pieces, VelocityJacobianSolver factors them; kept until Sys changes (_get_residuals)."""
+        104-121 at du = dv = 0): sem_condensed_blocks with one component writes the condensation
+        pieces, VelocityJacobianSolver factors them (on a partitioned solver: StripLineSolver, each rank
+        its own strip); kept until Sys changes (_get_residuals)."""
         if self._factor is None:
             if self._Sys is None:
                 raise RuntimeError("ConvectionDiffusion: _get_residuals must run before _get_update")
             m = self._mesh
-            vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
+            if self._part is not None:
+                from .strip_solve import StripLineSolver
+                p = self._part
+                vs = StripLineSolver(self._P, self._N_ex, self._N_ey, m.device, p.part.bounds, p.rank, p.dist,
+                                     group=p.group, ncomp=1, gather_device=p.backend_device())
+            else:
+                vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, ncomp=1)
             cX, cu, cY, cv, d = self._Sys._coeffs()
             vs.factor_mesh(m, c_mass=self._Sys.cM, c_stiff=self._Sys.cK, c_gradx=cX, cu=cu, c_grady=cY, cv=cv, juu=d,
                            **self._dir.kw())
@@ -253,12 +262,12 @@ class ConvectionDiffusionSolver:
 
         restart = max(1, min(int(self.N * 0.3), self._max_basis))
         precond = None
-        if self._precond == "condensed":
+        if self._precond == "condensed" and (self._part is None or self._P > 1):
             precond = self._jacobian_solver().solve1
             restart = min(restart, 100)
         if self._part is not None:
             r = gmres(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
-                      restart=restart, callback=cb, inner=self._part.inner)
+                      restart=restart, precond=precond, callback=cb, inner=self._part.inner)
         else:
             if self._recycle_bytes and self._recycle is None:
                 n = self._mesh.n_local

@@ -24,10 +24,23 @@ import torch
 
 from .. import SEM, _lib
 from ..device import get_mesh, no_gc
-from ..krylov import Recycle, gcro
+from ..krylov import Recycle, gcro, gmres
 from ..operators import ConvectionTensor, SEMOperator
 from .convection_diffusion import DirichletRows
 from .velocity_solve import VelocityJacobianSolver
+
+
+def _mass_diagonal(P, nex, ney, dx, dy):
+    """Diagonal of the assembled mass matrix (SEM.py:170-183): (dx/2)(dy/2) wx_g wy_g with the GLL
+    weights summed over the elements holding each 1-D node."""
+    from .. import GLL
+    w = GLL.standard_nodes(P)[1]
+    wx, wy = np.zeros(nex * P + 1), np.zeros(ney * P + 1)
+    for e in range(nex):
+        wx[e * P:e * P + P + 1] += w
+    for e in range(ney):
+        wy[e * P:e * P + P + 1] += w
+    return ((dx / 2) * (dy / 2)) * np.outer(wx, wy).ravel()
 
 
 class NavierStokesSolver:
@@ -36,14 +49,16 @@ class NavierStokesSolver:
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
                  max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
                  recycle_bytes: float = 0.0, velocity_sweep: str = "cr", schur_precond: str = "mass",
-                 partition=None):
+                 partition=None, partition_update: str = "distributed"):
         """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip per
         rank: _get_residuals / _calc_jacobians / _get_dresiduals run the fused strip launch and sum the
-        interface lines of all three outputs with one collective; _get_update is the whole-mesh direct
-        velocity solve inside the Schur Krylov solve, run by rank 0 on a whole-mesh counterpart
-        (_central_solver) and broadcast -- its condensation couples every interface line, so it is not
-        split.  The reference methods take and return global NumPy vectors (local strips when given
-        device tensors).
+        interface lines of all three outputs with one collective.  partition_update: "distributed"
+        (default) -- _get_update runs on the strips: the velocity Jacobian is factored by the
+        element-partitioned condensation (strip_solve.StripLineSolver: each rank its own columns, a
+        reduced system over the strip-boundary lines shared by all), and the Schur-complement Krylov
+        solve runs over the strips (inner products all-reduced); "central" -- rank 0's whole-mesh
+        counterpart (_central_solver) solves and the update is broadcast.  The reference methods take
+        and return global NumPy vectors (local strips when given device tensors).
         recycle_bytes: device memory for a recycled Krylov subspace of the Schur-complement solves
         (sem_amd.krylov.Recycle, GCRO; 0 = off, the default): consecutive _get_update calls with one
         linearisation -- the Boussinesq coupler's block-Jacobi preconditioner -- then start from the
@@ -64,6 +79,11 @@ class NavierStokesSolver:
         velocities there are reproduced only by the reference's own preconditioner."""
         if schur_precond not in ("mass", "pcd"):
             raise ValueError("schur_precond must be 'mass' or 'pcd'")
+        if partition_update not in ("distributed", "central"):
+            raise ValueError("partition_update must be 'distributed' or 'central'")
+        if partition is not None and schur_precond != "mass" and partition_update == "distributed":
+            raise ValueError("the distributed update uses the mass-diagonal Schur preconditioner")
+        self._partition_update = partition_update
         self._schur_precond, self._Ap = schur_precond, None
         self._iprint = iprint
         self._recycle_bytes, self._schur_recycle = recycle_bytes, None
@@ -124,7 +144,11 @@ class NavierStokesSolver:
             raise ValueError("one pinned pressure node is supported")
         self._pin = int(pins[0]) if len(pins) else -1
         self._pin_val = float(dpp[self._pin]) if len(pins) else 0.0
-        if partition is not None:   # the update runs on the whole-mesh counterpart
+        if partition is not None:
+            # the reference's mass diagonal (NavierStokes_Solver.py:207-212) is the assembled one: on a
+            # shared line both strips hold the whole-mesh value
+            self._Mdiag = m.to_device(partition.local(_mass_diagonal(P, N_ex, N_ey, dx, dy)))
+            self._pin_local = self._pin - m.dof_begin if 0 <= self._pin - m.dof_begin < m.n_local else -1
             return
         self._Mdiag = m.to_device(self._M.diagonal())
         # PCD row weights: 1/M on the continuity rows, 0 on the replaced rows (and the reverse)
@@ -283,6 +307,84 @@ class NavierStokesSolver:
             return tuple(self._dev(a) for a in d)
         return tuple(d)
 
+    def _strip_velocity_solver(self):
+        """The element-partitioned velocity factor of this linearisation (strip_solve.StripLineSolver on
+        this rank's strip handle), kept until _calc_jacobians runs again."""
+        if self._velo is not None:
+            return self._velo
+        from .strip_solve import StripLineSolver
+        tStart = time.perf_counter()
+        m, p = self._mesh, self._part
+        vs = StripLineSolver(self._P, self._N_ex, self._N_ey, m.device, p.part.bounds, p.rank, p.dist, group=p.group,
+                             gather_device=p.backend_device())
+        vs.factor_mesh(m, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
+        self._velo = vs
+        if 'LU_suc' in self._iprint:
+            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec (element-partitioned)')
+        return vs
+
+    def _schur_strips(self, vs, dp):
+        """S dp on the strips (NavierStokes_Solver.py:194-203): the gradients of dp (interface lines summed
+        across strips), the partitioned velocity solve, the divergence (summed)."""
+        m, part, NY = self._mesh, self._part, self._mesh.NY
+        kw = self._ns_kw(pin_first=False)
+        gu, gv = torch.empty_like(dp), torch.empty_like(dp)
+        m.ns_apply(None, None, dp, gu, gv, **kw)
+        part.assemble(gu, gv)
+        X = vs._solve_lines(torch.stack((gu.view(-1, NY), gv.view(-1, NY)), dim=1).reshape(-1, 2 * NY))
+        rc = torch.empty_like(dp)
+        m.ns_apply(X[:, :NY].reshape(-1), X[:, NY:].reshape(-1), dp, rc=rc, c_div=-1.0, **kw)
+        part.assemble(rc)
+        return rc
+
+    def _get_update_strips(self, dres_u, dres_v, dres_cont, du0=None, dv0=None, dp0=None):
+        """_get_update (NavierStokes_Solver.py:162-236) on the strips: the element-partitioned velocity
+        solve inside the Schur-complement GMRES, whose inner products are all-reduced (a shared line
+        counted once); the reference's mass-diagonal preconditioner and stopping rule."""
+        vs = self._strip_velocity_solver()
+        m, part = self._mesh, self._part
+        kw = self._ns_kw(pin_first=False)
+        ru, rv, rc = self._dev(dres_u), self._dev(dres_v), self._dev(dres_cont)
+        fu, fv = vs.solve(ru, rv)
+        c0 = torch.empty_like(rc)
+        m.ns_apply(fu, fv, None, rc=c0, **kw)
+        part.assemble(c0)
+        b_schur = rc - c0
+        count = [0]
+
+        def schur_mv(dp):
+            count[0] += 1
+            return self._schur_strips(vs, dp)
+
+        pin = self._pin_local
+
+        def precon(c):
+            z = c / self._Mdiag
+            if pin >= 0:
+                z[pin] = c[pin]
+            return z
+
+        it = [0]
+        prog = getattr(self, "_progress", 0)
+
+        def cb(est):
+            it[0] += 1
+            if 'LGMRES_iter' in self._iprint or (prog and it[0] % prog == 0):
+                print(f'NavierStokes GMRES: {it[0]}\t{est}', flush=True)
+
+        restart = max(1, min(self.N, self._max_basis, int(32e9 // (16 * m.n_local))))
+        r = gmres(schur_mv, b_schur, x0=self._dev(dp0), atol=self._mtol * np.sqrt(self.N), rtol=0.0,
+                  restart=restart, precond=precon, callback=cb, inner=part.inner)
+        if r.info != 0:
+            raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {r.info} iterations')
+        dp = r.x
+        self.schur_matvecs = count[0]
+        b_u, b_v = torch.empty_like(dp), torch.empty_like(dp)
+        m.ns_apply(None, None, dp, b_u, b_v, **kw)
+        part.assemble(b_u, b_v)
+        du, dv = vs.solve(ru - b_u, rv - b_v)
+        return self._out(du, dres_u), self._out(dv, dres_u), self._out(dp, dres_u)
+
     def _velocity_solver(self):
         """Device factorisation of the Dirichlet-row-replaced velocity Jacobian -- the reference's
         `bmat` + `splu` (NavierStokes_Solver.py:176-184) -- by static condensation over node lines
@@ -339,7 +441,9 @@ class NavierStokesSolver:
         meshes (the Schur complement carries the spurious pressure modes of the equal-order
         discretisation), so the device GMRES runs unrestarted up to max_basis vectors."""
         if self._part is not None:
-            return self._get_update_partitioned(dres_u, dres_v, dres_cont, du0, dv0, dp0)
+            if self._partition_update == "central":
+                return self._get_update_partitioned(dres_u, dres_v, dres_cont, du0, dv0, dp0)
+            return self._get_update_strips(dres_u, dres_v, dres_cont, du0, dv0, dp0)
         vs = self._velocity_solver()
         m = self._mesh
         ru, rv, rc = self._dev(dres_u), self._dev(dres_v), self._dev(dres_cont)

@@ -1,0 +1,148 @@
+"""Element-partitioned condensed direct solve (the multi-GPU half of SURVEY.md 8f rank 4, cfg5).
+
+The reference solves its Newton updates in one process (SuperLU, NavierStokes_Solver.py:176-236; its
+only parallelism is the two-component ParallelGroup, OpenMDAO/Boussinesq_ParallelCoupler.py:68-100).
+Here every rank holds the element columns [eb, ee) of a strip partition (sem_amd/parallel.py) and its
+lines eb P .. ee P; neighbouring strips share one interface line.
+
+Factor, per rank (no communication until the last step):
+  1. the nested condensation of the rank's own columns (velocity_solve.py, factor_condensed) -- the HIP
+     kernel writes the strip's pieces (sem_condensed_blocks on a strip handle: partial rows on the two
+     interface lines, the pointwise terms and Dirichlet rows of a shared line left to its right owner),
+     giving the strip's block-tridiagonal interface system over its local lines 0..n (n = ee - eb);
+  2. the local interface lines 1..n-1 are eliminated by block LU (block Thomas with pivoted pivot-block
+     inverses), keeping the two strip-boundary lines: a 2 x 2 block system R (m x m blocks) per rank;
+  3. the R of all ranks are all-gathered (RCCL under "nccl") and every rank factors the reduced
+     block-tridiagonal system over the G + 1 strip-boundary lines (block cyclic reduction), whose
+     shared-line blocks are the sums of the two neighbours' partial blocks.
+Solve of J x = b (b on the rank's lines, equal on shared lines): interior solves of the own columns,
+the interface right-hand side (a shared line's b counted by its right owner only), local forward
+elimination to the two boundary lines, ONE all-gather of 2 m doubles per rank, the replicated reduced
+solve, local back substitution, interior back substitution.  x comes out on every rank's lines, equal
+on shared lines.
+"""
+import torch
+
+from .velocity_solve import VelocityJacobianSolver, batched_inverse
+
+
+class StripLineSolver(VelocityJacobianSolver):
+    """x = J^-1 b for a Jacobian whose element columns are strip-partitioned across the ranks of `dist`."""
+
+    def __init__(self, P, nex, ney, device, bounds, rank, dist, group=None, ncomp=2, gather_device=None):
+        """bounds: the StripPartition bounds (rank r holds element columns [bounds[r], bounds[r+1]));
+        gather_device: where the all-gathered blocks travel (the GPU under RCCL, the host under gloo)."""
+        eb, ee = bounds[rank], bounds[rank + 1]
+        super().__init__(P, ee - eb, ney, device, interior="nested", sweep="cr", ncomp=ncomp)
+        self.nex_global, self.eb, self.ee = nex, eb, ee
+        self.bounds, self.rank, self.G = list(bounds), rank, len(bounds) - 1
+        self.dist, self.group = dist, group
+        self.gather_device = torch.device(gather_device) if gather_device is not None else self.device
+        self.own_right = ee >= nex     # a shared right line belongs to the strip on its right
+
+    # ------------------------------------------------------------------ factor
+    def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
+        """Assemble the strip's condensed pieces on its strip handle (HIP) and factor."""
+        if mesh.ex_begin != self.eb or mesh.ex_end != self.ee:
+            raise ValueError("the mesh handle must hold this rank's strip")
+        kw = dict(kw, ncomp=self.ncomp)
+        eb = self.eb
+        if self.P == 1:
+            raise ValueError("the strip solve needs P >= 2")
+        return self.factor_condensed(
+            lambda b, cols: mesh.condensed_blocks(b, cols=(cols[0] + eb, cols[1] + eb), **kw), budget_bytes)
+
+    def _all_gather(self, t):
+        """[t of rank 0, ..., t of rank G-1] (same shape everywhere) on this solver's device."""
+        if self.G == 1:
+            return [t]
+        src = t.to(self.gather_device).contiguous()
+        out = [torch.empty_like(src) for _ in range(self.G)]
+        self.dist.all_gather(out, src, group=self.group)
+        return [o.to(self.device) for o in out]
+
+    def _sweep_factor(self, S_diag, S_up, S_lo):
+        """Local lines 0..n: eliminate 1..n-1 (block LU), keep the strip's boundary lines 0 and n."""
+        n, m = self.nex, self.m
+        dev, f64 = self.device, torch.float64
+        inv = lambda A: batched_inverse(A[None])[0]  # noqa: E731
+        if n == 1:
+            R = torch.stack((torch.stack((S_diag[0], S_up[0])), torch.stack((S_lo[0], S_diag[1]))))
+            self._T = None
+        else:
+            k = n - 1                           # interior lines 1..n-1 -> rows 0..k-1 of T
+            Dinv = torch.empty((k, m, m), dtype=f64, device=dev)
+            Uh = torch.empty((max(k - 1, 1), m, m), dtype=f64, device=dev)
+            Dinv[0] = inv(S_diag[1])
+            for i in range(1, k):
+                Uh[i - 1] = Dinv[i - 1] @ S_up[i]                      # T's upper block of row i-1
+                Dinv[i] = inv(S_diag[i + 1] - S_lo[i] @ Uh[i - 1])     # T's lower block of row i
+            # X0 = T^-1 [S_lo[0]; 0; ...] (coupling of the interior to line 0), X1 = T^-1 [0; ...; S_up[n-1]]
+            X0 = torch.empty((k, m, m), dtype=f64, device=dev)
+            X1 = torch.zeros((k, m, m), dtype=f64, device=dev)
+            X0[0] = Dinv[0] @ S_lo[0]
+            for i in range(1, k):
+                X0[i] = -(Dinv[i] @ (S_lo[i] @ X0[i - 1]))
+            X1[k - 1] = Dinv[k - 1] @ S_up[n - 1]
+            for i in range(k - 2, -1, -1):
+                X0[i] -= Uh[i] @ X0[i + 1]
+                X1[i] = -(Uh[i] @ X1[i + 1])
+            R = torch.stack((torch.stack((S_diag[0] - S_up[0] @ X0[0], -(S_up[0] @ X1[0]))),
+                             torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
+            self._T = (Dinv, Uh, S_lo[1:n - 1].contiguous() if n > 2 else None, X0, X1)
+        self._S_up0, self._S_lon = S_up[0].clone(), S_lo[n - 1].clone()
+        del S_diag, S_up, S_lo
+        # the reduced system over the G + 1 strip-boundary lines, factored on every rank
+        Rs = self._all_gather(R)
+        G = self.G
+        Rd = torch.zeros((G + 1, m, m), dtype=f64, device=dev)
+        Ru = torch.empty((G, m, m), dtype=f64, device=dev)
+        Rl = torch.empty((G, m, m), dtype=f64, device=dev)
+        for j, Rj in enumerate(Rs):
+            Rd[j] += Rj[0, 0]
+            Rd[j + 1] += Rj[1, 1]
+            Ru[j], Rl[j] = Rj[0, 1], Rj[1, 0]
+        del Rs
+        red = VelocityJacobianSolver(1, G, 1, dev)
+        red.m = m
+        red._cr_factor(Rd, Ru, Rl)
+        self._red = red
+        self.factored = True
+
+    # ------------------------------------------------------------------ solve
+    def _own_rhs(self, g, B):
+        if not self.own_right:          # the right line's right-hand side is its right owner's
+            g[-1] -= B[-1]
+
+    def _thomas(self, g):
+        """y = T^-1 g for the local interior lines (g: (k, m), overwritten)."""
+        Dinv, Uh, Slo, _, _ = self._T
+        k = g.shape[0]
+        g[0] = Dinv[0] @ g[0]
+        for i in range(1, k):
+            g[i] = Dinv[i] @ (g[i] - Slo[i - 1] @ g[i - 1])
+        for i in range(k - 2, -1, -1):
+            g[i] -= Uh[i] @ g[i + 1]
+        return g
+
+    def _iface_solve(self, g):
+        n = self.nex
+        if self._T is not None:
+            y = self._thomas(g[1:n].clone())
+            h = torch.stack((g[0] - self._S_up0 @ y[0], g[n] - self._S_lon @ y[-1]))
+        else:
+            y, h = None, torch.stack((g[0], g[1]))
+        hs = self._all_gather(h)
+        G = self.G
+        rhs = torch.zeros((G + 1, self.m), dtype=torch.float64, device=self.device)
+        for j, hj in enumerate(hs):
+            rhs[j] += hj[0]
+            rhs[j + 1] += hj[1]
+        xb = self._red._cr_solve(rhs)
+        x0, x1 = xb[self.rank], xb[self.rank + 1]
+        out = torch.empty_like(g)
+        out[0], out[n] = x0, x1
+        if y is not None:
+            _, _, _, X0, X1 = self._T
+            out[1:n] = y - (X0 @ x0[:, None])[..., 0] - (X1 @ x1[:, None])[..., 0]
+        return out

@@ -657,6 +657,14 @@ class VelocityJacobianSolver:
                                           p(self._pi), p(self._pe), p(T), p(Cw), p(Ye))
         return self._nd
 
+    def _own_rhs(self, g, B):
+        """Hook of the strip-partitioned solve (strip_solve.py): drop the right-hand side of an interface
+        line this part does not own.  Whole mesh: nothing to do."""
+
+    def _iface_solve(self, g):
+        """The interface system S xB = g (overwrites g)."""
+        return self._cr_solve(g)
+
     def _solve_lines_hip(self, B):
         """_solve_lines on the GPU with the nested interior solves and the interface right-hand side
         as HIP kernels (sem_amd/csrc/ns_condense.hip): 3 + 1 + CR + 3 launches, no gathers or copies."""
@@ -674,7 +682,8 @@ class VelocityJacobianSolver:
         _lib.check(lib.sem_nested_solve(C.byref(d), v(b1), P * m, None, None, v(yI.data_ptr()), self.nI, st))
         _lib.check(lib.sem_interface_rhs(P, nex, m, v(B.data_ptr()), m, v(self.aBI.data_ptr()), v(yI.data_ptr()),
                                          self.nI, v(g.data_ptr()), st))
-        xB = self._cr_solve(g)
+        self._own_rhs(g, B)
+        xB = self._iface_solve(g)
         out = torch.empty((NX, m), dtype=torch.float64, device=self.device)
         out[0::P] = xB
         _lib.check(lib.sem_nested_solve(C.byref(d), v(b1), P * m, v(self.aIB.data_ptr()), v(xB.data_ptr()),
@@ -699,8 +708,9 @@ class VelocityJacobianSolver:
             yIr = yI.view(nex, P - 1, m)
             g[:-1] -= (self.aBI[:, 0] * yIr).sum(1)
             g[1:] -= (self.aBI[:, 1] * yIr).sum(1)
+        self._own_rhs(g, B)
         if self.sweep == "cr":
-            xB = self._cr_solve(g)
+            xB = self._iface_solve(g)
         else:   # block Thomas with the pivot blocks' explicit inverses
             z = torch.empty_like(g)
             z[0] = self.Dinv[0] @ g[0]

@@ -129,6 +129,58 @@ class CPUStripMesh:
             rc.copy_(torch.from_numpy(z))
         return ru, rv, rc
 
+    def condensed_blocks(self, blocks, *, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None, cv=None,
+                         juu=None, juv=None, jvu=None, jvv=None, dir_mask=None, dir_sides=0, ncomp=2, cols=None,
+                         stream=None):
+        """sem_condensed_blocks (include/sem_ops.h) on the strip, from the oracle's assembled operators: the
+        whole-mesh Jacobian built from this strip's coefficient vectors (rows outside the strip unused),
+        Dirichlet rows as identity rows, cut to the strip's pieces (tests/velocity_blocks.extract layout),
+        the right interface line's own block left to the strip on its right (the two partial blocks of a
+        shared line sum to the whole-mesh block, as the kernel's do)."""
+        import scipy.sparse as sp
+        from oracle import sem_oracle as O
+        from velocity_blocks import extract
+        from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
+        P, nex, ney, dx, dy, N = self.P, self.nex, self.ney, self.dx, self.dy, self.N
+        if getattr(self, "_ops", None) is None:
+            self._ops = (O.global_mass_matrix(P, nex, ney, dx, dy), O.global_stiffness_matrix(P, nex, ney, dx, dy),
+                         *O.global_gradient_matrices(P, nex, ney, dx, dy))
+        M, K, Gx, Gy = self._ops
+        sl = slice(self.dof_begin, self.dof_begin + self.n_local)
+
+        def glob(t, fill=0.0):
+            a = np.full(N, fill)
+            if t is not None:
+                a[sl] = t.numpy()
+            return a
+
+        A = c_mass * M + c_stiff * K + c_gradx * sp.diags(glob(cu, 1.0)) @ Gx + c_grady * sp.diags(glob(cv, 1.0)) @ Gy
+        if ncomp == 2:
+            J = sp.bmat([[A + sp.diags(glob(juu)), sp.diags(glob(juv))], [sp.diags(glob(jvu)), A + sp.diags(glob(jvv))]])
+        else:
+            J = A + sp.diags(glob(juu))
+        _, dm, gq = self._own_dir(dir_mask, dir_sides)
+        dirg = np.zeros(N, dtype=bool)
+        dirg[gq[dm]] = True
+        mask = np.tile(dirg, ncomp)
+        J = J.tolil()
+        J[mask, :] = 0
+        J[mask, mask] = 1
+        pcs = extract(J.toarray(), P, nex, ney, ncomp=ncomp)
+        eb, ee = self.ex_begin, self.ex_end
+        c0, c1 = (eb, ee) if cols is None else cols
+        for k in ("aIB", "aBI", "E", "F"):
+            blocks[k].copy_(torch.as_tensor(pcs[k][eb:ee]).reshape(blocks[k].shape))
+        D = pcs["D"][eb:ee + 1].copy()
+        if ee < nex:
+            D[-1] = 0.0
+        blocks["D"].copy_(torch.as_tensor(D).reshape(blocks["D"].shape))
+        vs = VelocityJacobianSolver(P, ee - eb, ney, "cpu", ncomp=ncomp)
+        cond = vs.condense_dense(torch.as_tensor(pcs["AII"][c0:c1]))
+        for k, v in cond.items():
+            blocks[k].copy_(v.reshape(blocks[k].shape))
+        return blocks
+
     def interface_pack(self, y, bounds, buf, stream=None):
         r = bounds.index(self.ex_begin)
         left, right = (r - 1 if r > 0 else -1), (r if r < len(bounds) - 2 else -1)

@@ -29,6 +29,10 @@ def _worker(rank, port, mode, q):
     sys.path[:0] = [os.path.dirname(here), here]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=2)
+    import torch as _torch
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)   # ranks share the host: no BLAS / OpenMP oversubscription
+    _torch.set_num_threads(1)
     try:
         from sem_amd.solvers.boussinesq import ParallelBoussinesqCoupler
         cd, ns = _solvers()
@@ -83,6 +87,10 @@ def _worker_partitioned(rank, world, port, key, q, cd_update="central"):
     sys.path[:0] = [os.path.dirname(here), here]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch as _torch
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)   # ranks share the host: no BLAS / OpenMP oversubscription
+    _torch.set_num_threads(1)
     try:
         from conftest import golden
         from cpu_mesh import CPUStripMesh

@@ -62,6 +62,10 @@ def _worker(rank, world, port, P, nex, ney, q, kind="allreduce"):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch as _torch
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)   # ranks share the host: no BLAS / OpenMP oversubscription
+    _torch.set_num_threads(1)
     try:
         from oracle import sem_oracle as O
         from sem_amd.parallel import StripPartition
@@ -125,6 +129,10 @@ def _worker_gmres(rank, world, port, P, nex, ney, q, kind):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch as _torch
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)   # ranks share the host: no BLAS / OpenMP oversubscription
+    _torch.set_num_threads(1)
     try:
         from sem_amd.krylov import gmres
         from sem_amd.parallel import DistributedInner, StripPartition

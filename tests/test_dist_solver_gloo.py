@@ -33,6 +33,10 @@ def _worker(rank, world, port, case, q):
     sys.path.insert(0, here)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch as _torch
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)   # ranks share the host: no BLAS / OpenMP oversubscription
+    _torch.set_num_threads(1)
     try:
         from cpu_mesh import CPUStripMesh
         from oracle import sem_oracle as O
