@@ -205,7 +205,8 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
         beta = vnorm(r)
 
 
-def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None, precond=None, callback=None):
+def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None, precond=None, callback=None,
+               inner=None):
     """Left-preconditioned restarted GMRES, SciPy's `gmres` (scipy 1.15 iterative.py) restated on
     device tensors: the Arnoldi process runs on M^-1 A, the inner loop stops on the
     preconditioned residual estimate against an adaptive tolerance (gh-8400 control), and each
@@ -217,30 +218,38 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
     spurious pressure modes of the equal-order P_N-P_N discretisation) needs its right-hand side
     in that range; the Arnoldi vectors a right-preconditioned GMRES feeds M^-1 are not.
     `maxiter` counts restarts, as SciPy's does.  info = 0 on convergence, else maxiter.
+    inner(A, w) = A @ w over a partitioned vector (sem_amd.parallel: shared lines counted once, the
+    partial products all-reduced); norms follow it.
     """
     N = b.numel()
     dt, dev = b.dtype, b.device
     restart = min(N, restart or 20)
     maxiter = maxiter or 10 * N
     psolve = precond if precond is not None else (lambda t: t)
+    if inner is None:
+        dot = lambda A, w: A @ w  # noqa: E731
+        vnorm = lambda t: torch.linalg.vector_norm(t).item()  # noqa: E731
+    else:
+        dot = inner
+        vnorm = lambda t: math.sqrt(max(float(inner(t[None], t)[0]), 0.0))  # noqa: E731
     x = torch.zeros_like(b) if x0 is None else x0.clone()
-    bnorm = torch.linalg.vector_norm(b).item()
+    bnorm = vnorm(b)
     if bnorm == 0.0:
         return GMRESResult(torch.zeros_like(b), 0, 0, 0.0, 0)
     tol = max(atol, rtol * bnorm)
     eps = np.finfo(np.float64).eps
     ptol_max = 1.0
-    ptol = torch.linalg.vector_norm(psolve(b)).item() * min(ptol_max, tol / bnorm)
+    ptol = vnorm(psolve(b)) * min(ptol_max, tol / bnorm)
     V = torch.empty((restart + 1, N), dtype=dt, device=dev)
     total, matvecs = 0, 0
     r = b - matvec(x) if x0 is not None else b.clone()
     matvecs += x0 is not None
-    rnorm = torch.linalg.vector_norm(r).item()
+    rnorm = vnorm(r)
     if rnorm < tol:
         return GMRESResult(x, 0, 0, rnorm, matvecs)
     for _ in range(maxiter):
         z = psolve(r)
-        zn = torch.linalg.vector_norm(z).item()
+        zn = vnorm(z)
         V[0] = z / zn
         H = np.zeros((restart + 1, restart))
         cs, sn = np.zeros(restart), np.zeros(restart)
@@ -250,14 +259,14 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
         for k in range(restart):
             w = psolve(matvec(V[k]))
             matvecs += 1
-            h0 = torch.linalg.vector_norm(w).item()
+            h0 = vnorm(w)
             Vk = V[:k + 1]
-            h = Vk @ w                       # CGS2 in place of SciPy's MGS
+            h = dot(Vk, w)                   # CGS2 in place of SciPy's MGS
             w = w - Vk.T @ h
-            h2 = Vk @ w
+            h2 = dot(Vk, w)
             w = w - Vk.T @ h2
             H[:k + 1, k] = (h + h2).cpu().numpy()
-            hn = torch.linalg.vector_norm(w).item()
+            hn = vnorm(w)
             if hn <= eps * h0:               # exact-solution indicator
                 H[k + 1, k], breakdown = 0.0, True
             else:
@@ -287,7 +296,7 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
         x = x + V[:k_done].T @ torch.as_tensor(y, dtype=dt, device=dev)
         r = b - matvec(x)
         matvecs += 1
-        rnorm = torch.linalg.vector_norm(r).item()
+        rnorm = vnorm(r)
         if rnorm <= tol or breakdown:
             break
         if presid <= ptol:

@@ -70,6 +70,32 @@ class BoussinesqCoupler:
         self.atol_nonlin = mtol_nonlin * math.sqrt(self.DOF)
         self.maxiter = maxiter if maxiter is not None else {'JNK': 100, 'NJ': 1000, 'GS': 1000}[mode]
         self._same_mesh = (cd._P, cd._N_ex, cd._N_ey) == (ns._P, ns._N_ex, ns._N_ey)
+        # device mode: the coupled vector lives on the device as [T | u | v | p] of this rank's strips (the
+        # whole mesh when the solvers are not partitioned), the solver methods exchange device tensors, and
+        # the coupled Krylov / Newton iteration runs there -- no host copy of the 4 N vectors per step, and
+        # on a partition only the interface lines (inside the solver maps) and inner products cross ranks.
+        # Reference solver classes (duck-typed, NumPy) keep the host mode.
+        self._device = (getattr(cd, "_mesh", None) is not None and getattr(ns, "_mesh", None) is not None
+                        and self._same_mesh)
+        self._inner = None
+        if self._device:
+            self._ncd_loc, self._nns_loc = cd._mesh.n_local, ns._mesh.n_local
+            pcd, pns = getattr(cd, "_part", None), getattr(ns, "_part", None)
+            if (pcd is None) != (pns is None):
+                raise ValueError("partition both solvers or neither")
+            if pns is not None:
+                own = torch.cat((pcd.inner.own, pns.inner.own, pns.inner.own, pns.inner.own))
+                dist, group = pns.dist, pns.group
+                bdev = pns.backend_device()
+
+                def inner(A, w, own=own):
+                    h = A @ (w * own)
+                    if dist.get_world_size(group) > 1:
+                        hb = h.to(bdev)
+                        dist.all_reduce(hb, group=group)
+                        h = hb.to(h.device)
+                    return h
+                self._inner = inner
         self.iterations = 0
         self.timing = {k: 0.0 for k in ("residuals", "jacobian_apply", "cd_update", "ns_update")}
         self.calls = {k: 0 for k in self.timing}
@@ -85,6 +111,8 @@ class BoussinesqCoupler:
     def _to_cd(self, f_ns):
         """ConvectionDiffusion_Component.change_inputs (:23-36): NS field at the CD nodes."""
         if self._same_mesh:
+            if isinstance(f_ns, torch.Tensor):
+                return f_ns.clone()
             return np.array(f_ns, dtype=np.float64, copy=True)
         cd = self.cd
         shape = (2, cd._P * cd._N_ex + 1, cd._P * cd._N_ey + 1)
@@ -93,6 +121,8 @@ class BoussinesqCoupler:
     def _to_ns(self, f_cd):
         """NavierStokes_Component.change_inputs (:23-33): CD field at the NS nodes."""
         if self._same_mesh:
+            if isinstance(f_cd, torch.Tensor):
+                return f_cd.clone()
             return np.array(f_cd, dtype=np.float64, copy=True)
         ns = self.ns
         shape = (2, ns._P * ns._N_ex + 1, ns._P * ns._N_ey + 1)
@@ -100,16 +130,56 @@ class BoussinesqCoupler:
 
     # ------------------------------------------------------------------ packing
     def _split(self, x):
-        n, m = self.Ncd, self.Nns
+        n, m = (self._ncd_loc, self._nns_loc) if self._device else (self.Ncd, self.Nns)
         return x[:n], x[n:n + m], x[n + m:n + 2 * m], x[n + 2 * m:]
 
-    @staticmethod
-    def _join(*parts):
+    def _join(self, *parts):
+        if self._device:
+            return torch.cat([a.reshape(-1) for a in parts])
         return np.concatenate([np.asarray(a, dtype=np.float64) for a in parts])
 
+    def _norm(self, r):
+        if not self._device:
+            return np.linalg.norm(r)
+        if self._inner is None:
+            return torch.linalg.vector_norm(r).item()
+        return math.sqrt(float(self._inner(r[None], r)[0]))
+
+    def _zeros(self, n_global, n_local, like=None):
+        if self._device:
+            return torch.zeros(n_local, dtype=torch.float64, device=self.cd._mesh.device)
+        return np.zeros(n_global)
+
+    def to_local(self, x):
+        """The coupled vector in this coupler's working form: a device tensor of the local strips of
+        [T | u | v | p] (device mode) or the global NumPy vector."""
+        if not self._device:
+            return np.array(x, dtype=np.float64)
+        if isinstance(x, torch.Tensor):
+            return x.to(self.cd._mesh.device, torch.float64).contiguous()
+        x = np.asarray(x, dtype=np.float64)
+        n, m = self.Ncd, self.Nns
+        parts = (x[:n], x[n:n + m], x[n + m:n + 2 * m], x[n + 2 * m:])
+        return torch.cat([self.cd._dev(parts[0])] + [self.ns._dev(a) for a in parts[1:]])
+
+    def to_global(self, x):
+        """The global NumPy [T | u | v | p] of a working-form vector (gathered across strips)."""
+        if not self._device:
+            return np.asarray(x, dtype=np.float64)
+        T, u, v, p = self._split(x)
+        g = lambda s, t: s._out(t, np.zeros(0))  # noqa: E731  (NumPy-like: gathered to the host)
+        return np.concatenate((g(self.cd, T), g(self.ns, u), g(self.ns, v), g(self.ns, p)))
+
     # ------------------------------------------------------------------ component maps
+    def _host_call(self, fn, x):
+        """Device mode, called with a global NumPy vector (the OpenMDAO-style interface): the same map on the
+        working form, the result gathered back."""
+        return self.to_global(fn(self.to_local(x)))
+
     def residuals(self, x):
         """apply_nonlinear of both components (CD :38-39, NS :35-37)."""
+        if self._device and not isinstance(x, torch.Tensor):
+            return self._host_call(self.residuals, x)
         T, u, v, p = self._split(x)
         t0 = time.perf_counter()
         rT = self.cd._get_residuals(T, self._to_cd(u), self._to_cd(v))
@@ -120,12 +190,16 @@ class BoussinesqCoupler:
 
     def linearize(self, x):
         """linearize of both components (CD :41-42, NS :39-40); called after residuals(x)."""
+        if self._device and not isinstance(x, torch.Tensor):
+            x = self.to_local(x)
         T, u, v, _ = self._split(x)
         self.cd._calc_jacobians(T)
         self.ns._calc_jacobians(u, v)
 
     def jacobian_apply(self, dx):
         """apply_linear, fwd mode (CD :44-49, NS :42-50): the coupled Jacobian on dx."""
+        if self._device and not isinstance(dx, torch.Tensor):
+            return self._host_call(self.jacobian_apply, dx)
         dT, du, dv, dp = self._split(dx)
         t0 = time.perf_counter()
         rT = self.cd._get_dresiduals(dT, self._to_cd(du), self._to_cd(dv))
@@ -137,11 +211,13 @@ class BoussinesqCoupler:
     def block_jacobi(self, r):
         """LinearBlockJac(maxiter=1): each component's solve_linear on its own residual block
         (CD :51-57, NS :52-60), zero initial guesses."""
+        if self._device and not isinstance(r, torch.Tensor):
+            return self._host_call(self.block_jacobi, r)
         rT, ru, rv, rp = self._split(r)
         t0 = time.perf_counter()
-        dT = self._timed("cd_update", self.cd._get_update, rT, dT0=np.zeros(self.Ncd))
+        dT = self._timed("cd_update", self.cd._get_update, rT, dT0=self._zeros(self.Ncd, getattr(self, "_ncd_loc", 0)))
         t1 = time.perf_counter()
-        z = np.zeros(self.Nns)
+        z = self._zeros(self.Nns, getattr(self, "_nns_loc", 0))
         du, dv, dp = self._timed("ns_update", self.ns._get_update, ru, rv, rp, du0=z, dv0=z, dp0=z)
         if self.iprint >= 2:
             self._log(f'    block-Jacobi: CD {getattr(self.cd, "matvecs", "?")} matvecs {t1 - t0:.3f} s, '
@@ -150,6 +226,8 @@ class BoussinesqCoupler:
 
     def gauss_seidel_pass(self, x):
         """One pass of the subsystems' solve_nonlinear in group order (CD :59-61, NS :62-65)."""
+        if self._device and not isinstance(x, torch.Tensor):
+            return self._host_call(self.gauss_seidel_pass, x)
         T, u, v, p = self._split(x)
         T = self.cd._get_solution(self._to_cd(u), self._to_cd(v), T0=T)
         u, v, p = self.ns._get_solution(self._to_ns(T), u0=u, v0=v, p0=p)
@@ -165,15 +243,17 @@ class BoussinesqCoupler:
         checkpoint(x, k): called after every nonlinear iteration (long runs save their state);
         resume=True: x0 is such a saved state -- continue the Newton iteration without the initial
         subsystem pass."""
-        x = np.zeros(self.DOF) if x0 is None else np.array(x0, dtype=np.float64)
+        x = self.to_local(np.zeros(self.DOF) if x0 is None else x0)
         self._checkpoint = checkpoint
         x = self._solve_gs(x) if self.mode == 'GS' else self._solve_newton(x, initial_pass=not resume)
-        return tuple(np.array(a) for a in self._split(x))
+        xg = self.to_global(x)
+        n, m = self.Ncd, self.Nns
+        return xg[:n].copy(), xg[n:n + m].copy(), xg[n + m:n + 2 * m].copy(), xg[n + 2 * m:].copy()
 
     def _solve_gs(self, x):
         for k in range(self.maxiter):
             x = self.gauss_seidel_pass(x)
-            norm = np.linalg.norm(self.residuals(x))
+            norm = self._norm(self.residuals(x))
             self._log(f'NLBGS {k + 1} ; {norm}')
             self.iterations = k + 1
             if norm <= self.atol_nonlin:
@@ -184,7 +264,7 @@ class BoussinesqCoupler:
         if initial_pass:
             x = self.gauss_seidel_pass(x)  # solve_subsystems=True, max_sub_solves=0: at iteration 0 only
         r = self.residuals(x)
-        norm = np.linalg.norm(r)
+        norm = self._norm(r)
         self._log(f'Newton 0 ; {norm}')
         k = 0
         while norm > self.atol_nonlin:
@@ -194,26 +274,33 @@ class BoussinesqCoupler:
             if self.mode == 'JNK':
                 x = x + self._linear_jnk(-r)
                 r = self.residuals(x)
-                norm = np.linalg.norm(r)
+                norm = self._norm(r)
             else:
                 x, r, norm = self._armijo_goldstein(x, self.block_jacobi(-r), norm)
             k += 1
             self._log(f'Newton {k} ; {norm}')
             if getattr(self, "_checkpoint", None) is not None:
-                self._checkpoint(x, k)
+                self._checkpoint(self.to_global(x), k)
         self.iterations = k
         return x
 
     def _linear_jnk(self, b):
-        """GMRES on the coupled Jacobian, block-Jacobi preconditioned (ScipyKrylov :89-91)."""
-        mv = lambda t: torch.from_numpy(self.jacobian_apply(t.numpy()))  # noqa: E731
-        pc = lambda t: torch.from_numpy(self.block_jacobi(t.numpy()))  # noqa: E731
+        """GMRES on the coupled Jacobian, block-Jacobi preconditioned (ScipyKrylov :89-91).  Device mode: the
+        Krylov basis and every vector stay on the device (inner products across strips when partitioned)."""
         it = [0]
 
         def cb(presid):
             it[0] += 1
             self._log(f'  GMRES {it[0]} ; {presid}')
 
+        if self._device:
+            res = gmres_left(self.jacobian_apply, b, atol=self.atol_gmres, rtol=0.0, restart=self.restart,
+                             maxiter=5000, precond=self.block_jacobi, callback=cb, inner=self._inner)
+            if res.info != 0:
+                raise RuntimeError(f'GMRES failed to converge in {res.info} restarts')
+            return res.x
+        mv = lambda t: torch.from_numpy(self.jacobian_apply(t.numpy()))  # noqa: E731
+        pc = lambda t: torch.from_numpy(self.block_jacobi(t.numpy()))  # noqa: E731
         res = gmres_left(mv, torch.from_numpy(np.ascontiguousarray(b)), atol=self.atol_gmres, rtol=0.0,
                          restart=self.restart, maxiter=5000, precond=pc, callback=cb)
         if res.info != 0:
@@ -225,14 +312,14 @@ class BoussinesqCoupler:
         alpha = 1.0
         x_new = x + dx
         r_new = self.residuals(x_new)
-        n_new = np.linalg.norm(r_new)
+        n_new = self._norm(r_new)
         for _ in range(self.AGi):
             if n_new <= norm0 * (1.0 - self.AGc * alpha):
                 break
             alpha *= self.AGr
             x_new = x + alpha * dx
             r_new = self.residuals(x_new)
-            n_new = np.linalg.norm(r_new)
+            n_new = self._norm(r_new)
         return x_new, r_new, n_new
 
 
@@ -263,6 +350,7 @@ class ParallelBoussinesqCoupler(BoussinesqCoupler):
 
     def __init__(self, *args, dist=None, group=None, **kw):
         super().__init__(*args, **kw)
+        self._device = False   # the two blocks meet in a host-side all-reduce of the coupled vector
         if dist is None or dist.get_world_size(group) != 2:
             raise ValueError("the parallel coupler runs on exactly two ranks (CD on rank 0, NS on rank 1)")
         self.dist, self.group = dist, group
