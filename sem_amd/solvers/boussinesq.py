@@ -435,16 +435,18 @@ def run_parallel(points_plot, L_x, L_y, dist, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4,
 
 def partitioned_coupler(dist, L_x, L_y, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4, N_ex_cd=8, N_ey_cd=8, P_ns=4, N_ex_ns=8,
                         N_ey_ns=8, group=None, exchange="allreduce", overlap=True, mesh_factory=None,
-                        mtol_internal=1e-13, schur_precond="mass", cd_update="central", **kw):
+                        mtol_internal=1e-13, schur_precond="mass", cd_update="distributed", ns_update="distributed",
+                        **kw):
     """The element-partitioned Boussinesq coupler (BASELINE cfg5: 128 x 128, P = 12 over 8 GPUs): both
     solvers are strip-partitioned over every rank of `dist` (sem_amd.parallel.Partition -- each rank
     holds the same element-column strip range of the CD and the NS mesh, one GPU per rank), so every
-    residual and Jacobian apply is a strip launch plus the RCCL interface exchange; the Newton updates
-    (the block-Jacobi preconditioner's solves) run on rank 0's whole-mesh counterparts -- the NS
-    velocity / Schur solve, and the CD solve with its condensed direct preconditioner
-    (cd_update="central"; "distributed" runs the partitioned device GMRES over the strips instead).  The coupled Newton-Krylov iteration itself (OpenMDAO's NewtonSolver + ScipyKrylov on
-    the coupled vector, Boussinesq_SequentialCoupler.py:75-93) runs replicated on every rank on the
-    global vectors the solver methods return; the coupled vector stays on the host, as in OpenMDAO.
+    residual and Jacobian apply is a strip launch plus the RCCL interface exchange, and the Newton updates
+    (the block-Jacobi preconditioner's solves) are element-partitioned too (cd_update / ns_update =
+    "distributed", the default: strip_solve.StripLineSolver factors each rank's own columns and the ranks
+    share a reduced system over the strip-boundary lines; "central" hands a solve to rank 0's whole-mesh
+    counterpart).  The coupled Newton-Krylov iteration (OpenMDAO's NewtonSolver + ScipyKrylov on the coupled
+    vector, Boussinesq_SequentialCoupler.py:75-93) runs on every rank over its local strips of the coupled
+    vector, on the device, with all-reduced inner products.
     Same arguments as BoussinesqCoupler, plus the partition's (group, exchange protocol, overlap,
     mesh_factory for a CPU strip double)."""
     from ..parallel import Partition
@@ -454,6 +456,7 @@ def partitioned_coupler(dist, L_x, L_y, Re=1.e3, Ra=1.e3, Pr=0.71, P_cd=4, N_ex_
     cd = ConvectionDiffusionSolver(L_x=L_x, L_y=L_y, Pe=Re * Pr, P=P_cd, N_ex=N_ex_cd, N_ey=N_ey_cd, T_W=0.5, T_E=-0.5,
                                    mtol=mtol_internal, partition=part(), partition_update=cd_update)
     ns = NavierStokesSolver(L_x=L_x, L_y=L_y, Re=Re, Gr=Ra / Pr, P=P_ns, N_ex=N_ex_ns, N_ey=N_ey_ns, mtol=mtol_internal,
-                            mtol_newton=mtol_internal, iprint=[], schur_precond=schur_precond, partition=part())
+                            mtol_newton=mtol_internal, iprint=[], schur_precond=schur_precond, partition=part(),
+                            partition_update=ns_update)
     return BoussinesqCoupler(L_x, L_y, Re, Ra, Pr, P_cd, N_ex_cd, N_ey_cd, P_ns, N_ex_ns, N_ey_ns,
                              mtol_internal=mtol_internal, cd=cd, ns=ns, **kw)

@@ -62,7 +62,11 @@ class StripLineSolver(VelocityJacobianSolver):
         return [o.to(self.device) for o in out]
 
     def _sweep_factor(self, S_diag, S_up, S_lo):
-        """Local lines 0..n: eliminate 1..n-1 (block LU), keep the strip's boundary lines 0 and n."""
+        """Local lines 0..n: eliminate 1..n-1 (block LU), keep the strip's boundary lines 0 and n.  One
+        rank: the whole-mesh sweep."""
+        if self.G == 1:
+            self._T = None
+            return super()._sweep_factor(S_diag, S_up, S_lo)
         n, m = self.nex, self.m
         dev, f64 = self.device, torch.float64
         inv = lambda A: batched_inverse(A[None])[0]  # noqa: E731
@@ -126,6 +130,8 @@ class StripLineSolver(VelocityJacobianSolver):
         return g
 
     def _iface_solve(self, g):
+        if self.G == 1:
+            return super()._iface_solve(g)
         n = self.nex
         if self._T is not None:
             y = self._thomas(g[1:n].clone())

@@ -61,14 +61,18 @@ def _bad_blocks(A, X):
     return torch.nonzero(~(E.abs().amax(dim=(-2, -1)) <= tol)).flatten()
 
 
-def batched_inverse(A, max_batch=128):
-    """Inverses of a batch of blocks (rocSOLVER getrf/getri through torch), checked.
+def batched_inverse(A, max_batch=128, sample=8):
+    """Inverses of a batch of blocks (rocSOLVER getrf/getri through torch), sliced and spot-checked.
 
-    Measured on MI355X (tools/chunk_probe.py, profiles/r02/cfg5/chunk_probe.txt): the batched
-    inverse returns wrong blocks, without an error, for some shapes -- 121^2 blocks (the one-component
-    element interiors at P = 12) in batches of 384 and more -- and has been seen to fail its workspace
-    allocation for others (64 blocks of 455^2).  So the batch is inverted in slices of max_batch blocks,
-    every block is checked through its residual A X - I, and a block that misses is inverted again on
+    The batched LU of this ROCm stack is faulty (tools/inv_repro.py on MI355X,
+    profiles/r03/inv/inv_repro_mi355x.txt): on seeded, well-conditioned, contiguous 121^2 blocks
+    (U(-1, 1) + n I) torch.linalg.inv, inv_ex, lu_factor + lu_solve and solve -- every route goes through
+    hipblasDgetrfBatched -- return correct inverses (residual 2e-15) in batches up to 512 and wrong ones
+    without an error at 1024 (16 of 1024 blocks) and 4096 (950 of 4096); 242^2 blocks fail their workspace
+    allocation at batch 256.  The caller is not involved (fresh contiguous tensors, no views).  So the
+    batch is inverted in slices of max_batch (128, inside the measured safe range), and each slice is
+    spot-checked through the residual A X - I of `sample` blocks (its first, its last and evenly spaced
+    ones); a slice whose sample misses is checked in full, and a block that misses is inverted again on
     its own (then by a solve against the identity) before giving up."""
     if A.dim() < 3:
         return torch.linalg.inv(A)
@@ -76,7 +80,10 @@ def batched_inverse(A, max_batch=128):
     for i in range(0, A.shape[0], max_batch):
         a = A[i:i + max_batch]
         x = _inverse(a)
-        for j in _bad_blocks(a, x).tolist():
+        nb = a.shape[0]
+        pick = torch.linspace(0, nb - 1, min(nb, sample), device=a.device).round().long().unique()
+        bad = _bad_blocks(a[pick], x[pick])
+        for j in (_bad_blocks(a, x).tolist() if bad.numel() else []):
             xj = torch.linalg.inv(a[j])
             if _bad_blocks(a[j:j + 1], xj[None]).numel():
                 eye = torch.eye(a.shape[-1], dtype=a.dtype, device=a.device)

@@ -48,14 +48,16 @@ def test_rejects_a_wrong_inverse():
 
 def test_repairs_blocks_the_batched_call_got_wrong(monkeypatch):
     """The failure seen on MI355X (tools/inv_repro.py): the batched call returns some wrong blocks
-    without an error.  Simulated by corrupting one block of every slice."""
+    without an error.  Simulated by corrupting, in every slice, a sampled block (which triggers the
+    full check of the slice) and another one (found by that full check)."""
     A = _blocks(300, 20, 5)
     calls = []
 
     def corrupt(a):
         x = torch.linalg.inv(a)
         calls.append(a.shape[0])
-        x[len(calls) % a.shape[0]] *= 3.0
+        x[0] *= 3.0
+        x[len(calls) % a.shape[0] + 1] *= 3.0
         return x
 
     monkeypatch.setattr(VS, "_inverse", corrupt)

@@ -77,22 +77,33 @@ def test_cfg4_state_is_converged(cfg4):
 
 def test_cfg4_ns_update_solves_the_oracle_linearisation(cfg4):
     """One NS block-Jacobi solve (solve_linear, NavierStokes_Component.py:52-60 -> _get_update) at the
-    state's linearisation: the oracle's _get_dresiduals (NavierStokes_Solver.py:138-160) of the device
-    update reproduces the seeded right-hand side.  The device stops the Schur Krylov solve at the
-    reference's rule ||r||_2 <= mtol sqrt(N) with the couplers' mtol_internal = 1e-13; the velocity rows
-    are solved directly (residual ~1e-14 relative)."""
+    state's linearisation, for the right-hand side the oracle's _get_dresiduals (NavierStokes_Solver.py:
+    138-160) makes of a smooth seeded step (du, dv vanish on the walls): the device update reproduces
+    the step's velocities (unique; the pressure is unique up to the spurious modes of the equal-order
+    discretisation) and the oracle's _get_dresiduals of the update reproduces the
+    right-hand side.  The device stops the Schur Krylov solve at the reference's rule
+    ||r||_2 <= mtol sqrt(N) with the couplers' mtol_internal = 1e-13; the velocity rows are solved
+    directly (residual ~1e-14 relative)."""
     c, x, N = cfg4["c"], cfg4["x"], cfg4["N"]
     o = cfg4["ns"]
     c.residuals(x)
     c.linearize(x)
-    _, (bu, bv, bp) = _rhs(N)
-    z = np.zeros(N)
-    du, dv, dp = c.ns._get_update(bu, bv, bp, du0=z, dv0=z, dp0=z)
+    X, Y = o.points
+    du = 1e-3 * np.sin(np.pi * X) * np.sin(2 * np.pi * Y)
+    dv = -2e-3 * np.sin(2 * np.pi * X) * np.sin(np.pi * Y)
+    dp = 1e-2 * np.cos(np.pi * X) * np.cos(np.pi * Y)
     o.residuals(cfg4["u"], cfg4["v"], cfg4["p"], cfg4["T"])
     o.calc_jacobians(cfg4["u"], cfg4["v"])
-    lin = o.dresiduals(np.asarray(du), np.asarray(dv), np.asarray(dp))
+    bu, bv, bp = o.dresiduals(du, dv, dp)
+    z = np.zeros(N)
+    c.ns._progress = 500
+    gu, gv, gp = c.ns._get_update(bu, bv, bp, du0=z, dv0=z, dp0=z)
+    lin = o.dresiduals(np.asarray(gu), np.asarray(gv), np.asarray(gp))
     err = np.sqrt(sum(np.sum((a - b) ** 2) for a, b in zip(lin, (bu, bv, bp))))
-    assert err <= 1e3 * 1e-13 * np.sqrt(N), err
+    assert err <= 1e2 * 1e-13 * np.sqrt(N), err
+    # velocities: to the accuracy the Schur stopping rule implies (measured 3.6e-6 relative)
+    for a, b in ((gu, du), (gv, dv)):
+        assert np.abs(np.asarray(a) - b).max() <= 2e-5 * np.abs(b).max()
     assert 0 < c.ns.schur_matvecs < 3000
 
 

@@ -111,9 +111,10 @@ def _worker_solver(rank, world, port, q, kind, overlap):
                                                 (2, "allreduce", False)])
 def test_partitioned_cd_solver(gpu, world, kind, overlap):
     from sem_amd.solvers import ConvectionDiffusionSolver
-    # the whole-mesh solver with the partitioned solver's Krylov method (plain device GMRES: a strip
-    # has no whole-mesh condensed factor), so the matvec counts are comparable
-    cd = ConvectionDiffusionSolver(1.0, 1.0, PE, P, NEX, NEY, T_W=0.5, T_E=-0.5, mtol=1e-10, precond=None)
+    # the whole-mesh solver with its condensed direct preconditioner; the partitioned solver's GMRES is
+    # preconditioned by the element-partitioned condensation of the same Jacobian (strip_solve.py), so
+    # both take one or two matvecs
+    cd = ConvectionDiffusionSolver(1.0, 1.0, PE, P, NEX, NEY, T_W=0.5, T_E=-0.5, mtol=1e-10)
     r = np.random.default_rng(23)
     T, u, v, dT, du, dv = (r.uniform(-1, 1, cd.N) for _ in range(6))
     res = cd._get_residuals(T, u, v)
@@ -135,7 +136,7 @@ def test_partitioned_cd_solver(gpu, world, kind, overlap):
         assert np.abs(pres - res).max() <= 1e-13 * np.abs(res).max(), rank
         assert np.abs(pdres - dres).max() <= 1e-13 * np.abs(dres).max(), rank
         assert np.abs(psol - sol).max() < 1e-8, rank
-        assert abs(mv - cd.matvecs) <= 2, (rank, mv, cd.matvecs)
+        assert mv <= cd.matvecs + 2 <= 5, (rank, mv, cd.matvecs)
 
 
 NS_CASE = dict(P=4, nex=6, ney=4, Re=100.0, Gr=50.0)
@@ -160,7 +161,8 @@ def _ns_run(ns):
 
 def _worker_ns(rank, world, port, q, kind):
     """NavierStokesSolver(partition=...) on real strip meshes (the fused strip sem_ns_apply, interface
-    assembly of the three outputs in one collective); updates by rank 0's whole-mesh counterpart."""
+    assembly of the three outputs in one collective); Newton updates by the element-partitioned velocity
+    condensation (sem_condensed_blocks on strip handles, StripLineSolver) inside the strip Schur GMRES."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -257,3 +259,108 @@ def test_cfg5_element_partitioned_coupled_maps(gpu):
         assert p.exitcode == 0
     assert np.abs(PR - R).max() <= 1e-13 * np.abs(R).max()
     assert np.abs(PJR - JR).max() <= 1e-13 * np.abs(JR).max()
+
+
+def _worker_strip_velocity(rank, world, port, q, case):
+    """StripLineSolver on real strip handles: sem_condensed_blocks writes the strip's partial pieces, each
+    rank condenses its own columns, the reduced system over the strip-boundary lines is shared."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.dirname(here), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from velocity_blocks import oracle_velocity_jacobian
+        import scipy.sparse.linalg as spla
+        from sem_amd import _lib
+        from sem_amd.device import get_mesh
+        from sem_amd.parallel import StripPartition
+        from sem_amd.solvers.strip_solve import StripLineSolver
+        P, nex, ney, Re = case
+        ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+        part = StripPartition(nex, world)
+        eb, ee = part.local_range(rank)
+        mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.0 / ney, eb, ee, 0)
+        sl = slice(mesh.dof_begin, mesh.dof_begin + mesh.n_local)
+        d = lambda a: mesh.to_device(np.asarray(a)[sl])  # noqa: E731
+        kw = dict(c_stiff=1.0, c_gradx=Re, cu=d(u), c_grady=Re, cv=d(v), juu=d(Re * (ref.Gx @ u)),
+                  jvv=d(Re * (ref.Gy @ v)), juv=d(Re * (ref.Gy @ u)), jvu=d(Re * (ref.Gx @ v)),
+                  dir_sides=_lib.SIDE_W | _lib.SIDE_E | _lib.SIDE_S | _lib.SIDE_N)
+        vs = StripLineSolver(P, nex, ney, mesh.device, part.bounds, rank, dist, gather_device="cpu")
+        vs.factor_mesh(mesh, budget_bytes=1, **kw)     # one column per chunk
+        r = np.random.default_rng(3)
+        bu, bv = r.uniform(-1, 1, ref.N), r.uniform(-1, 1, ref.N)
+        want = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
+        xu, xv = vs.solve(d(bu), d(bv))
+        err = max(np.abs(xu.cpu().numpy() - want[:ref.N][sl]).max(), np.abs(xv.cpu().numpy() - want[ref.N:][sl]).max())
+        q.put((rank, err / np.abs(want).max()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,case", [(2, (4, 4, 3, 300.0)), (3, (6, 7, 2, 1000.0)), (2, (12, 2, 3, 500.0))])
+def test_strip_velocity_solve_real_kernels(gpu, world, case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_strip_velocity, args=(r, world, port, q, case)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err in out:
+        assert err <= 1e-9, (rank, err)
+
+
+def _worker_cfg5_update(rank, world, port, q):
+    """cfg5's NS block solve element-partitioned (128^2, P=12 over `world` ranks): the velocity Jacobian
+    factored by the strips' condensations + the reduced boundary-line system, the Schur GMRES over the
+    strips; linearised at the coupled solve's start (fluid at rest, T = 1/2 - x, Ra = 1e6)."""
+    import sys
+    import time as _t
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sem_amd.parallel import Partition
+        from sem_amd.solvers import NavierStokesSolver
+        c5 = CFG5
+        ns = NavierStokesSolver(1.0, 1.0, c5["Re"], c5["Ra"] / c5["Pr"], c5["P"], c5["ne"], c5["ne"], mtol=1e-10,
+                                mtol_newton=1e-10, iprint=[], partition=Partition(dist))
+        m = ns._mesh
+        z = torch.zeros(m.n_local, dtype=torch.float64, device=m.device)
+        T = ns._dev(0.5 - ns.points[0])
+        ns._get_residuals(z, z, z, T)
+        ns._calc_jacobians(z, z)
+        r = np.random.default_rng(77)
+        rhs = [ns._dev(r.uniform(-1, 1, ns.N)) for _ in range(3)]
+        t0 = _t.perf_counter()
+        du, dv, dp = ns._get_update(*rhs)
+        secs = _t.perf_counter() - t0
+        lin = ns._get_dresiduals(du, dv, dp)
+        err = ns._norm(*(a - b for a, b in zip(lin, rhs)))
+        if rank == 0:
+            q.put((err, 1e-10 * np.sqrt(ns.N), ns.schur_matvecs, secs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cfg5_element_partitioned_ns_update(gpu):
+    """One cfg5 NS Newton update (_get_update) element-partitioned over 4 ranks on one GPU: it solves the
+    partitioned Jacobian (the coupled maps above pin that to the whole-mesh device maps) to the reference's
+    Schur tolerance mtol sqrt(N) (NavierStokes_Solver.py:222-224)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_worker_cfg5_update, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    err, tol, nmv, secs = q.get(timeout=280)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    print(f"cfg5 partitioned NS update: {nmv} Schur matvecs, {secs:.1f} s, residual {err:.3e} (tol {tol:.3e})")
+    assert err <= 10 * tol and 0 < nmv < 1000

@@ -1,10 +1,12 @@
-"""BASELINE cfg5 end to end: the element-partitioned Boussinesq coupler (both solvers strip-partitioned
-over the ranks, sem_amd.solvers.boussinesq.partitioned_coupler), 128 x 128 elements, P = 12, JNK from
-rest at the given Ra.  Rank 0 also holds the whole-mesh counterparts that solve the Newton updates.
+"""BASELINE cfg5 end to end: the Boussinesq coupler at 128 x 128 elements, P = 12, JNK from rest at the
+given Ra (Ra continuation through --continuation).  One rank: the whole-mesh device coupler
+(BoussinesqCoupler, the coupled vector on the device).  Several ranks: the element-partitioned coupler
+(partitioned_coupler: both solvers strip-partitioned, the Newton updates element-partitioned too).
 
+  python tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 [--ckpt DIR]          # one MI355X
   torchrun --nproc-per-node N tools/bous_cfg5_solve.py [--Ra 1e3]                  # RCCL, one GPU per rank
   torchrun --nproc-per-node N tools/bous_cfg5_solve.py --backend gloo              # N ranks on one GPU
-Prints the Newton history and one JSON line (rank 0).
+Prints the Newton history and one JSON line per stage (rank 0).
 """
 import argparse
 import json
@@ -28,6 +30,8 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--continuation", default="", help="Ra stages before --Ra (each starts from the last)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--ckpt", default="", help="directory for each finished stage's state (rank 0)")
+    ap.add_argument("--x0", default="", help="start from a saved state (.npy of [T, u, v, p])")
     args = ap.parse_args()
     if "RANK" not in os.environ:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29534")
@@ -38,30 +42,27 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     import gc
 
-    from sem_amd.solvers.boussinesq import partitioned_coupler
+    from sem_amd.solvers.boussinesq import BoussinesqCoupler, partitioned_coupler
     Re, Pr = 1e3, 0.71
-    x, stages = None, []
+    x, stages = (np.load(args.x0) if args.x0 else None), []
     for Ra in [float(r) for r in args.continuation.split(",") if r] + [args.Ra]:
-        c = partitioned_coupler(dist, 1.0, 1.0, Re, Ra, Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
-                                mode=args.mode, iprint=2 if rank == 0 else 0)
-        make_ns, make_cd = c.ns._central_solver, c.cd._central_solver
-
-        def central_ns(make_ns=make_ns):   # progress lines from rank 0's whole-mesh solves
-            t = make_ns()
-            t._progress, t._iprint = 250, ["LU_suc"]
-            return t
-
-        def central_cd(make_cd=make_cd):
-            t = make_cd()
-            t._progress = 250
-            return t
-
-        c.ns._central_solver, c.cd._central_solver = central_ns, central_cd
+        if world == 1:
+            c = BoussinesqCoupler(1.0, 1.0, Re, Ra, Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
+                                  mode=args.mode, iprint=2)
+        else:
+            c = partitioned_coupler(dist, 1.0, 1.0, Re, Ra, Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
+                                    mode=args.mode, iprint=2 if rank == 0 else 0)
+        if rank == 0:   # progress lines from the Schur / CD Krylov solves, and the factorisation times
+            c.ns._progress, c.cd._progress = 250, 250
+            c.ns._iprint = ["LU_suc"]
         t0 = time.perf_counter()
         T, u, v, p = c.solve(x)
         dt = time.perf_counter() - t0
         x = np.concatenate([T, u, v, p])
         res = float(np.linalg.norm(c.residuals(x)))   # collective
+        if rank == 0 and args.ckpt:
+            os.makedirs(args.ckpt, exist_ok=True)
+            np.save(os.path.join(args.ckpt, f"cfg5_{Ra:g}.npy"), x)
         if rank == 0:
             s = np.linspace(0.0, 1.0, 1001)
             um = np.asarray(c.ns._get_interpol(u, np.meshgrid([0.5], s, indexing="ij")))[0] * Re * Pr
@@ -76,7 +77,8 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
     if rank == 0:
-        out = {"config": f"cfg5 element-partitioned Boussinesq {args.mode} Ra={args.Ra:g}, {args.ne}x{args.ne} P={args.P}",
+        out = {"config": f"cfg5 Boussinesq {args.mode} Ra={args.Ra:g}, {args.ne}x{args.ne} P={args.P}"
+                         + (", element-partitioned" if world > 1 else ", whole mesh on one GPU"),
                "ranks": world, "backend": args.backend, "DOF": int(x.size), "stages": stages,
                "device": torch.cuda.get_device_name(dev)}
         print(json.dumps(out), flush=True)

@@ -18,12 +18,14 @@ step() {  # name limit cmd...
 for s in "$@"; do
   case $s in
     gpu)        step gputests 1100 $PYT -q -m gpu tests ;;
-    cfg4)       step cfg4 300 $PYT tests/test_gpu_cfg4.py ;;
+    cfg4)       step cfg4 300 $PYT -s tests/test_gpu_cfg4.py ;;
     nsapply)    step nsapply 300 $PYT tests/test_gpu_ns_apply.py ;;
     velocity)   step velocity 600 $PYT tests/test_gpu_ns_velocity.py ;;
     smoke)      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)      step bench 600 python bench.py ;;
     inv)        step inv 300 python tools/inv_repro.py ;;
+    nsbench)    step nsbench 300 python tools/nsbench.py ;;
+    dist)       step dist 900 $PYT -s tests/test_gpu_dist.py ;;
     cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5ns)     SEM_PROFILE_FACTOR=1 step cfg5ns 900 python tools/cfg5_ns_probe.py ;;
     pmcbench)
