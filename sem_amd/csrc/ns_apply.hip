@@ -78,11 +78,14 @@ __device__ __forceinline__ double wsum1(int g, int P, int e_lo, int e_hi, const 
 template <int P>
 struct NsTile {
   static constexpr int TXE = 1;
+  // ~32 owned columns: measured faster than one 64-wide line per wavefront (tools/nsbench.py, r03:
+  // 14.7 vs 19.6 us for the 48^2 residual -- twice the workgroups to fill the chip)
   static constexpr int TYE = (32 / P) > 0 ? 32 / P : 1;
   static constexpr int BX = TXE * P, BY = TYE * P;
   static constexpr int SX = BX + P + 1, SY = BY + P + 1;
   static constexpr int PITCH = SY | 1;  // odd: lanes striding across staged lines hit distinct banks
   static constexpr int THREADS = 256;
+  static_assert((3 * SX * PITCH + 2 * (P + 1) * (P + 1) + P + 1) * 8 <= 64 * 1024, "LDS staging above 64 KB");
 };
 
 // One workgroup per tile (XCD-aware order: the 8 XCDs take contiguous runs of tiles, so neighbouring

@@ -48,7 +48,7 @@ class NavierStokesSolver:
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
                  max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
-                 recycle_bytes: float = 0.0, velocity_sweep: str = "cr", schur_precond: str = "mass",
+                 recycle_bytes: float = 0.0, velocity_sweep: str = "auto", schur_precond: str = "mass",
                  partition=None, partition_update: str = "distributed"):
         """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip per
         rank: _get_residuals / _calc_jacobians / _get_dresiduals run the fused strip launch and sum the

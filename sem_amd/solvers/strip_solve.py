@@ -33,7 +33,7 @@ class StripLineSolver(VelocityJacobianSolver):
         """bounds: the StripPartition bounds (rank r holds element columns [bounds[r], bounds[r+1]));
         gather_device: where the all-gathered blocks travel (the GPU under RCCL, the host under gloo)."""
         eb, ee = bounds[rank], bounds[rank + 1]
-        super().__init__(P, ee - eb, ney, device, interior="nested", sweep="cr", ncomp=ncomp)
+        super().__init__(P, ee - eb, ney, device, interior="nested", sweep="auto", ncomp=ncomp)
         self.nex_global, self.eb, self.ee = nex, eb, ee
         self.bounds, self.rank, self.G = list(bounds), rank, len(bounds) - 1
         self.dist, self.group = dist, group

@@ -33,8 +33,24 @@ from ..device import no_gc
 GEMV_LDS_DOUBLES = 8192   # sem_block_gemv stages S m operand doubles in LDS (include/sem_ops.h)
 
 
+# rocSOLVER's strided-batched getrf/getri (sem_amd/linalg.py) in place of torch's pointer-array batched
+# path (hipblasDgetrfBatched, faulty on this stack); SEM_STRIDED_INV=0 selects torch's for A/B runs
+_STRIDED = os.environ.get("SEM_STRIDED_INV", "1") != "0"
+
+
 def _inverse(A):
-    """torch.linalg.inv of a batch; on a getrf workspace-allocation failure the batch is halved."""
+    """Inverse of a batch: rocSOLVER strided-batched on the GPU, else torch.linalg.inv; on a getrf
+    workspace-allocation failure the batch is halved."""
+    if _STRIDED and A.is_cuda and A.dim() == 3:
+        from .. import linalg
+        if linalg.available():
+            try:
+                return linalg.strided_inverse(A)[0]
+            except RuntimeError:
+                if A.shape[0] == 1:
+                    raise
+                h = A.shape[0] // 2
+                return torch.cat((_inverse(A[:h]), _inverse(A[h:])))
     try:
         return torch.linalg.inv(A)
     except RuntimeError as e:
@@ -98,19 +114,22 @@ def batched_inverse(A, max_batch=128, sample=8):
 class VelocityJacobianSolver:
     """x = J^-1 b for the velocity Jacobian J of one linearisation, J given by its condensation pieces."""
 
-    def __init__(self, P, nex, ney, device, interior="nested", sweep="cr", ncomp=2):
+    def __init__(self, P, nex, ney, device, interior="nested", sweep="auto", ncomp=2):
         """ncomp: unknowns per node -- 2 for the velocity pair [u | v], 1 for a scalar operator
         (the convection-diffusion Jacobian, or the pressure stiffness of the Schur preconditioner).
         interior: elimination of the element-column interiors ("nested" static condensation, or
         one dense block per column: "lu" factors, "inverse" explicit inverses).  sweep: solve of the
         block-tridiagonal interface system ("cr": block cyclic reduction, about 2 log2(N_ex) batched
-        launches; "thomas": block Thomas, 2 N_ex sequential steps)."""
+        launches; "thomas": block Thomas, 2 N_ex sequential steps, a third of CR's factorisation flops and
+        fewer bytes per solve; "auto": CR up to m = 2048 interface unknowns per line, Thomas above --
+        measured: CR's solve is faster at cfg3/cfg4 (m = 514 / 770), its factorisation dominates cfg5's
+        (m = 3074: 4.6 s of 8.3 s, profiles/r03/cfg5/))."""
         if P < 1 or nex < 1 or ney < 1:
             raise ValueError("bad mesh")
         if interior not in ("nested", "lu", "inverse"):
             raise ValueError("interior must be 'nested', 'lu' or 'inverse'")
-        if sweep not in ("cr", "thomas"):
-            raise ValueError("sweep must be 'cr' or 'thomas'")
+        if sweep not in ("cr", "thomas", "auto"):
+            raise ValueError("sweep must be 'cr', 'thomas' or 'auto'")
         if ncomp not in (1, 2):
             raise ValueError("ncomp must be 1 or 2")
         self.sweep, self.ncomp = sweep, ncomp
@@ -118,6 +137,8 @@ class VelocityJacobianSolver:
         self.NY, self.NX = ney * P + 1, nex * P + 1
         self.m = ncomp * self.NY
         self.nI = (P - 1) * self.m
+        if sweep == "auto":
+            sweep = self.sweep = "cr" if self.m <= 2048 else "thomas"
         self.device = torch.device(device)
         self.interior = interior
         self.factored = False
@@ -670,7 +691,16 @@ class VelocityJacobianSolver:
 
     def _iface_solve(self, g):
         """The interface system S xB = g (overwrites g)."""
-        return self._cr_solve(g)
+        if self.sweep == "cr":
+            return self._cr_solve(g)
+        # block Thomas with the pivot blocks' explicit inverses: 2 GEMVs per line forward, 1 back
+        z = g
+        z[0] = self.Dinv[0] @ g[0]
+        for L in range(1, self.nex + 1):
+            z[L] = self.Dinv[L] @ (g[L] - self.S_lo[L - 1] @ z[L - 1])
+        for L in range(self.nex - 1, -1, -1):
+            z[L] -= self.Uh[L] @ z[L + 1]
+        return z
 
     def _solve_lines_hip(self, B):
         """_solve_lines on the GPU with the nested interior solves and the interface right-hand side
@@ -700,7 +730,7 @@ class VelocityJacobianSolver:
     def _solve_lines(self, B):
         """x = J^-1 b with b, x as (NX, 2 NY) line arrays (every line: u then v)."""
         P, nex, m, NX = self.P, self.nex, self.m, self.NX
-        if (self.device.type == "cuda" and P > 1 and self.interior == "nested" and self.sweep == "cr"
+        if (self.device.type == "cuda" and P > 1 and self.interior == "nested"
                 and getattr(self, "hip_nested", True)):
             return self._solve_lines_hip(B)
         g = B[0::P].clone()                                    # interface lines (nex+1, m)
@@ -716,16 +746,7 @@ class VelocityJacobianSolver:
             g[:-1] -= (self.aBI[:, 0] * yIr).sum(1)
             g[1:] -= (self.aBI[:, 1] * yIr).sum(1)
         self._own_rhs(g, B)
-        if self.sweep == "cr":
-            xB = self._iface_solve(g)
-        else:   # block Thomas with the pivot blocks' explicit inverses
-            z = torch.empty_like(g)
-            z[0] = self.Dinv[0] @ g[0]
-            for L in range(1, nex + 1):
-                z[L] = self.Dinv[L] @ (g[L] - self.S_lo[L - 1] @ z[L - 1])
-            xB = z
-            for L in range(nex - 1, -1, -1):
-                xB[L] = z[L] - self.Uh[L] @ xB[L + 1]
+        xB = self._iface_solve(g)
         out = torch.empty((NX, m), dtype=torch.float64, device=self.device)
         out[0::P] = xB
         if P > 1:

@@ -12,8 +12,13 @@ python tools/inv_repro.py [--n 121,242] [--batches 64,128,256,384,512,1024,4096]
 """
 import argparse
 import json
+import os
+import sys
+import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def rel_residual(A, X):
@@ -26,11 +31,12 @@ def rel_residual(A, X):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", default="121,242")
-    ap.add_argument("--batches", default="64,128,256,384,512,1024,4096")
+    ap.add_argument("--batches", default="64,128,256,384,512,1024,4096,16384")
     ap.add_argument("--seed", type=int, default=2024)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(args.seed)
+    from sem_amd import linalg
     for n in (int(s) for s in args.n.split(",")):
         eye = torch.eye(n, dtype=torch.float64, device=dev)
         for nb in (int(s) for s in args.batches.split(",")):
@@ -40,16 +46,21 @@ def main():
                             ("inv_ex", lambda a: torch.linalg.inv_ex(a)[0]),
                             ("lu_solve", lambda a: torch.linalg.lu_solve(*torch.linalg.lu_factor(a),
                                                                          eye.expand_as(a))),
-                            ("solve", lambda a: torch.linalg.solve(a, eye.expand_as(a)))):
+                            ("solve", lambda a: torch.linalg.solve(a, eye.expand_as(a))),
+                            ("rocsolver_strided", lambda a: linalg.strided_inverse(a)[0])):
                 try:
+                    torch.cuda.synchronize(dev)
+                    t0 = time.perf_counter()
                     X = f(A)
                     torch.cuda.synchronize(dev)
+                    ms = (time.perf_counter() - t0) * 1e3
                 except RuntimeError as e:      # e.g. HIPBLAS_STATUS_ALLOC_FAILED in getrfBatched
                     out[name] = {"error": str(e).splitlines()[0][:160]}
                     continue
                 r = rel_residual(A, X)
                 bad = int((r > 1e-10).sum())
-                out[name] = {"max_rel_residual": float(r.max()), "bad_blocks": bad,
+                out[name] = {"max_rel_residual": float(r.max()), "bad_blocks": bad, "ms": round(ms, 2),
+                             "gflops": round(2.0 * nb * n ** 3 / (ms * 1e-3) / 1e9, 1),
                              "first_bad": int(torch.nonzero(r > 1e-10)[0, 0]) if bad else -1}
             # a strided view of twice the batch (every other block): the caller-side layout question
             A2 = torch.empty((2 * nb, n, n), dtype=torch.float64, device=dev)
