@@ -77,21 +77,26 @@ def _bad_blocks(A, X):
     return torch.nonzero(~(E.abs().amax(dim=(-2, -1)) <= tol)).flatten()
 
 
-def batched_inverse(A, max_batch=128, sample=8):
-    """Inverses of a batch of blocks (rocSOLVER getrf/getri through torch), sliced and spot-checked.
+def batched_inverse(A, max_batch=None, sample=8):
+    """Inverses of a batch of blocks, sliced and spot-checked.
 
-    The batched LU of this ROCm stack is faulty (tools/inv_repro.py on MI355X,
+    torch's batched LU on this ROCm stack is faulty (tools/inv_repro.py on MI355X,
     profiles/r03/inv/inv_repro_mi355x.txt): on seeded, well-conditioned, contiguous 121^2 blocks
     (U(-1, 1) + n I) torch.linalg.inv, inv_ex, lu_factor + lu_solve and solve -- every route goes through
-    hipblasDgetrfBatched -- return correct inverses (residual 2e-15) in batches up to 512 and wrong ones
-    without an error at 1024 (16 of 1024 blocks) and 4096 (950 of 4096); 242^2 blocks fail their workspace
-    allocation at batch 256.  The caller is not involved (fresh contiguous tensors, no views).  So the
-    batch is inverted in slices of max_batch (128, inside the measured safe range), and each slice is
-    spot-checked through the residual A X - I of `sample` blocks (its first, its last and evenly spaced
-    ones); a slice whose sample misses is checked in full, and a block that misses is inverted again on
-    its own (then by a solve against the identity) before giving up."""
+    hipblasDgetrfBatched (pointer-array batched) -- return correct inverses (residual 2e-15) in batches up
+    to 512 and wrong ones without an error at 1024 (16 of 1024 blocks) and 4096 (950 of 4096); 242^2
+    blocks fail their workspace allocation from batch 256 on.  The caller is not involved (fresh
+    contiguous tensors, no views).  rocSOLVER's strided-batched getrf + getri on the same blocks
+    (sem_amd/linalg.py) is correct at every batch measured (up to 16384 blocks of 242^2, residual 5e-15)
+    and runs at 5.2 TFLOP/s there against 0.17 for the sliced torch route, so it is the GPU path
+    (_inverse).  Either way the batch is inverted in slices of max_batch (4096 strided, 128 through torch)
+    and each slice is spot-checked through the residual A X - I of `sample` blocks (its first, its last
+    and evenly spaced ones); a slice whose sample misses is checked in full, and a block that misses is
+    inverted again on its own (then by a solve against the identity) before giving up."""
     if A.dim() < 3:
-        return torch.linalg.inv(A)
+        return batched_inverse(A[None], max_batch, sample)[0]
+    if max_batch is None:   # rocSOLVER's strided path measured correct up to 16384 blocks; torch's to 512
+        max_batch = 4096 if (_STRIDED and A.is_cuda) else 128
     out = torch.empty_like(A)
     for i in range(0, A.shape[0], max_batch):
         a = A[i:i + max_batch]
@@ -503,7 +508,7 @@ class VelocityJacobianSolver:
         for L in range(nex + 1):
             if L > 0:
                 Dt = S_diag[L] - S_lo[L - 1] @ Uh[L - 1]
-            Dinv[L] = torch.linalg.inv(Dt)
+            Dinv[L] = batched_inverse(Dt)
             if L < nex:
                 Uh[L] = Dinv[L] @ S_up[L]
         self.Dinv, self.Uh, self.S_lo = Dinv, Uh, S_lo

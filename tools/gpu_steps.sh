@@ -34,6 +34,13 @@ for s in "$@"; do
       tools/pmc_run.sh "$O/pmc_cd1024" -- python tools/kbench.py --meshes 8:1024 --reps 20 || exit 1
       tools/pmc_run.sh "$O/pmc_mfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1
       tools/pmc_run.sh "$O/pmc_dot2" -- python tools/sweep_bench.py || exit 1 ;;
+    pmcns)
+      tools/pmc_run.sh "$O/pmc_ns48" -- python tools/nsbench.py --meshes 8:48 --reps 200 || exit 1
+      tools/pmc_run.sh "$O/pmc_ns128" -- python tools/nsbench.py --meshes 12:128 --reps 20 || exit 1
+      tools/pmc_run.sh "$O/pmc_vel48" -- python tools/velocity_bench.py --ne 48 --P 8 --configs nested:cr --reps 20 \
+        || exit 1 ;;
+    cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 --ckpt "$O/ckpt" \
+                  --out "$O/cfg5_ra1e4.json" ;;
     benchtrace)
       step bench 600 python bench.py
       step benchtrace 600 rocprofv3 --kernel-trace --stats -d "$O/benchtrace" -o trace --output-format csv -- \
