@@ -27,6 +27,7 @@ for s in "$@"; do
     nsbench)    step nsbench 300 python tools/nsbench.py ;;
     dist)       step dist 900 $PYT -s tests/test_gpu_dist.py ;;
     cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
+    cfg5factor_inv) SEM_PIVOT_INV=inv SEM_PROFILE_FACTOR=1 step cfg5factor_inv 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5ns)     SEM_PROFILE_FACTOR=1 step cfg5ns 900 python tools/cfg5_ns_probe.py ;;
     pmcbench)
       tools/pmc_run.sh "$O/pmc_cal" -- python tools/kbench.py --dss 1024 || exit 1
@@ -39,7 +40,7 @@ for s in "$@"; do
       tools/pmc_run.sh "$O/pmc_ns128" -- python tools/nsbench.py --meshes 12:128 --reps 20 || exit 1
       tools/pmc_run.sh "$O/pmc_vel48" -- python tools/velocity_bench.py --ne 48 --P 8 --configs nested:cr --reps 20 \
         || exit 1 ;;
-    cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 --ckpt "$O/ckpt" \
+    cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
     benchtrace)
       step bench 600 python bench.py
