@@ -137,36 +137,49 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
                             : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
                                ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
     const double u0 = a.u ? su[sidx] : 0.0, v0 = a.v ? sv[sidx] : 0.0;
+    // one pass per direction over the node's element row(s): every operand value and table entry is read
+    // from LDS once and feeds all the sums that use it (Sys u, Sys v; G p; G u, G v; K p)
+    const bool hu = a.u != nullptr, hv = a.v != nullptr, hp = a.p != nullptr;
+    const double cu = a.cu ? a.cu[q] : 1.0, cv = a.cv ? a.cv[q] : 1.0;
+    const double fx = a.fKx * my, gxc = a.fX * cu * my;  // x rows of Sys: fx K + gxc G
+    const double fy = a.fKy * mx, gyc = a.fY * cv * mx;  // y rows of Sys: fy K + gyc G
+    double Su = 0.0, Sv = 0.0, gxu = 0.0, gyv = 0.0, gxp = 0.0, gyp = 0.0, kxp = 0.0, kyp = 0.0;
+    const bool sys = want_uv && (hu || hv);
+    dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
+      const double K = Ks[row * n + c], G = Gs[row * n + c];
+      const double co = sys ? fma(gxc, G, fx * K) : 0.0;
+      if (hu) {
+        const double uq = su[sidx + off];
+        if (sys) Su = fma(co, uq, Su);
+        gxu = fma(G, uq, gxu);
+      }
+      if (hv && sys) Sv = fma(co, sv[sidx + off], Sv);
+      if (hp) {
+        const double pq = sp[sidx + off];
+        gxp = fma(G, pq, gxp);
+        kxp = fma(K, pq, kxp);
+      }
+    });
+    dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
+      const double K = Ks[row * n + c], G = Gs[row * n + c];
+      const double co = sys ? fma(gyc, G, fy * K) : 0.0;
+      if (hu && sys) Su = fma(co, su[sidx + off], Su);
+      if (hv) {
+        const double vq = sv[sidx + off];
+        if (sys) Sv = fma(co, vq, Sv);
+        gyv = fma(G, vq, gyv);
+      }
+      if (hp) {
+        const double pq = sp[sidx + off];
+        gyp = fma(G, pq, gyp);
+        kyp = fma(K, pq, kyp);
+      }
+    });
     if (want_uv) {
       if (dir) {
         if (a.ru) a.ru[qv] = own ? u0 - (a.gu ? a.gu[q] : 0.0) : 0.0;
         if (a.rv) a.rv[qv] = own ? v0 - (a.gv ? a.gv[q] : 0.0) : 0.0;
       } else {
-        const double cu = a.cu ? a.cu[q] : 1.0, cv = a.cv ? a.cv[q] : 1.0;
-        const double fx = a.fKx * my, gxc = a.fX * cu * my;  // x rows of Sys: fx K + gxc G
-        const double fy = a.fKy * mx, gyc = a.fY * cv * mx;  // y rows of Sys: fy K + gyc G
-        double Su = 0.0, Sv = 0.0, gxp = 0.0, gyp = 0.0;
-        const bool hu = a.u != nullptr, hv = a.v != nullptr, hp = a.p != nullptr;
-        if (hu || hv) {
-          dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
-            const double co = fma(gxc, Gs[row * n + c], fx * Ks[row * n + c]);
-            if (hu) Su = fma(co, su[sidx + off], Su);
-            if (hv) Sv = fma(co, sv[sidx + off], Sv);
-          });
-          dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
-            const double co = fma(gyc, Gs[row * n + c], fy * Ks[row * n + c]);
-            if (hu) Su = fma(co, su[sidx + off], Su);
-            if (hv) Sv = fma(co, sv[sidx + off], Sv);
-          });
-        }
-        if (hp) {
-          if (a.ru) dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
-            gxp = fma(Gs[row * n + c], sp[sidx + off], gxp);
-          });
-          if (a.rv) dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
-            gyp = fma(Gs[row * n + c], sp[sidx + off], gyp);
-          });
-        }
         const double fm = a.fM * mx * my;
         if (a.ru) {
           double z = fma(fm, u0, Su);
@@ -188,32 +201,14 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
       const bool pinned = static_cast<int64_t>(gx) * NY + gy == a.pin;
       const double pinrow = own ? (a.p ? sp[sidx] : 0.0) - a.pin_val : 0.0;
       double z;
-      if (pinned && !a.pin_first) {
+      if (pinned && !a.pin_first)
         z = pinrow;
-      } else if (dir) {  // the (K p) row: sx my Kx p + sy mx Ky p, coefficients combined on the diagonal
-        double kp = 0.0;
-        if (a.p) {
-          const double fx = a.sx * my, fy = a.sy * mx;
-          dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
-            kp = fma(fx * Ks[row * n + c], sp[sidx + off], kp);
-          });
-          dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
-            kp = fma(fy * Ks[row * n + c], sp[sidx + off], kp);
-          });
-        }
-        z = kp;
-      } else if (pinned) {
+      else if (dir)  // the (K p) row
+        z = a.sx * my * kxp + a.sy * mx * kyp;
+      else if (pinned)
         z = pinrow;
-      } else {
-        double gxu = 0.0, gyv = 0.0;
-        if (a.u) dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
-          gxu = fma(Gs[row * n + c], su[sidx + off], gxu);
-        });
-        if (a.v) dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
-          gyv = fma(Gs[row * n + c], sv[sidx + off], gyv);
-        });
+      else
         z = a.c_div * (a.hy * my * gxu + a.hx * mx * gyv);
-      }
       a.rc[q] = z;
     }
   }

@@ -25,6 +25,7 @@ for s in "$@"; do
     bench)      step bench 600 python bench.py ;;
     inv)        step inv 300 python tools/inv_repro.py ;;
     nsbench)    step nsbench 300 python tools/nsbench.py ;;
+    pivot)      step pivot 300 python tools/pivot_probe.py ;;
     dist)       step dist 900 $PYT -s tests/test_gpu_dist.py ;;
     cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5factor_inv) SEM_PIVOT_INV=inv SEM_PROFILE_FACTOR=1 step cfg5factor_inv 900 python tools/cfg5_ns_probe.py --update 0 ;;
