@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 7
+#define SEM_ABI_VERSION 8
 
 enum sem_status {
   SEM_OK = 0,
@@ -314,6 +314,15 @@ int sem_interface_rhs(int P, int nex, int m, const double* B, int64_t ld_b, cons
  * rows, y, xrow and yrow are device memory.  Stream-ordered. */
 int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* src, const int64_t* ld_src,
                    const int64_t* xrow, double* y, int64_t ld_y, const int64_t* yrow, int accumulate, void* stream);
+
+/* ---- small dense inverse (leaves of the sweep's pivot inverses) --------- */
+/* X = A^-1 for one n x n row-major block, n <= 64 (row r of A at A + r lda, of X at X + r ldx; device
+ * memory; X must not overlap A): Gauss-Jordan elimination with partial pivoting in one workgroup (ABI 8).
+ * The leaves of the GEMM-recursive inverse of the interface sweep's pivot blocks
+ * (sem_amd/linalg.py block_inverse), which replace the reference's SuperLU factorisation of the
+ * velocity Jacobian (NavierStokes_Solver.py:176-236).  A singular block yields non-finite entries, not
+ * an error: callers check A X - I.  Stream-ordered. */
+int sem_dense_inverse_small(const double* A, int64_t lda, double* X, int64_t ldx, int n, void* stream);
 
 /* ---- Navier-Stokes residuals (fused) ------------------------------------ */
 /* All three outputs of NavierStokes_Solver._get_residuals (NavierStokes_Solver.py:93-121) or

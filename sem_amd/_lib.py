@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE = range(6)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
@@ -102,6 +102,7 @@ _SIGS = {
                                     C.c_int64, C.c_void_p, C.c_void_p]),
     "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,
                                  C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p]),
+    "sem_dense_inverse_small": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_void_p]),
 }
 
 _lib = None

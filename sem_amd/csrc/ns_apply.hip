@@ -93,7 +93,12 @@ struct NsTile {
 // in LDS with loads coalesced along the lines; phase 2 forms every owned node's outputs from LDS only.
 // The Sys rows use the assembled 1-D coefficients (cK K + Re c G of the node's row combined before the
 // dot product, as the reference's CSR row of Sys = K + Re (diag(u) G_x + diag(v) G_y) holds them).
-template <int P>
+// Form flags: which operands are present and which outputs are written, fixed at compile time for the
+// forms the solvers launch so that a form does none of the sums it does not use (the residual: all; the
+// Schur gradient: G p into ru, rv; the Schur divergence: G u + G v, and K p on Dirichlet rows, into rc).
+enum : int { NS_U = 1, NS_P = 2, NS_UV_OUT = 4, NS_C_OUT = 8, NS_ALL = 15 };
+
+template <int P, int F>
 __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y, int ntiles, int per_xcd) {
   using T = NsTile<P>;
   constexpr int n = P + 1, BX = T::BX, BY = T::BY, SX = T::SX, SY = T::SY, PIT = T::PITCH;
@@ -114,15 +119,17 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
     const int gx = sx0 + r, gy = sy0 + c;
     if (gx < lb0 || gx > lb1 || gy < 0 || gy >= NY) continue;
     const int64_t lx = gx - lb0;
-    if (a.u) su[r * PIT + c] = a.u[lx * pitch + gy];
-    if (a.v) sv[r * PIT + c] = a.v[lx * pitch + gy];
-    if (a.p) sp[r * PIT + c] = a.p[lx * NY + gy];
+    if ((F & NS_U) && a.u) su[r * PIT + c] = a.u[lx * pitch + gy];
+    if ((F & NS_U) && a.v) sv[r * PIT + c] = a.v[lx * pitch + gy];
+    if ((F & NS_P) && a.p) sp[r * PIT + c] = a.p[lx * NY + gy];
   }
   __syncthreads();
   const double* Ks = tab;
   const double* Gs = tab + n * n;
   const double* w = tab + 2 * n * n;
-  const bool want_uv = a.ru || a.rv;
+  constexpr bool out_uv = (F & NS_UV_OUT) != 0, out_c = (F & NS_C_OUT) != 0;
+  const bool want_uv = out_uv && (a.ru || a.rv);
+  const bool want_c = out_c && a.rc;
   for (int k = threadIdx.x; k < BX * BY; k += T::THREADS) {
     const int ox = k / BY, oy = k - ox * BY;
     const int gx = gx0 + ox, gy = gy0 + oy;
@@ -136,28 +143,30 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
     const bool dir = a.mask ? a.mask[q] != 0
                             : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
                                ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
-    const double u0 = a.u ? su[sidx] : 0.0, v0 = a.v ? sv[sidx] : 0.0;
+    const bool hu = (F & NS_U) && a.u != nullptr, hv = (F & NS_U) && a.v != nullptr;
+    const bool hp = (F & NS_P) && a.p != nullptr;
+    const double u0 = hu ? su[sidx] : 0.0, v0 = hv ? sv[sidx] : 0.0;
     // one pass per direction over the node's element row(s): every operand value and table entry is read
     // from LDS once and feeds all the sums that use it (Sys u, Sys v; G p; G u, G v; K p)
-    const bool hu = a.u != nullptr, hv = a.v != nullptr, hp = a.p != nullptr;
     const double cu = a.cu ? a.cu[q] : 1.0, cv = a.cv ? a.cv[q] : 1.0;
     const double fx = a.fKx * my, gxc = a.fX * cu * my;  // x rows of Sys: fx K + gxc G
     const double fy = a.fKy * mx, gyc = a.fY * cv * mx;  // y rows of Sys: fy K + gyc G
     double Su = 0.0, Sv = 0.0, gxu = 0.0, gyv = 0.0, gxp = 0.0, gyp = 0.0, kxp = 0.0, kyp = 0.0;
     const bool sys = want_uv && (hu || hv);
+    const bool kp = want_c && hp && dir;  // K p: the artificial Neumann rows only
     dir_rows<P>(PIT, ex, ix, eb, ee, [&](int row, int c, int off) {
       const double K = Ks[row * n + c], G = Gs[row * n + c];
       const double co = sys ? fma(gxc, G, fx * K) : 0.0;
       if (hu) {
         const double uq = su[sidx + off];
         if (sys) Su = fma(co, uq, Su);
-        gxu = fma(G, uq, gxu);
+        if (want_c) gxu = fma(G, uq, gxu);
       }
       if (hv && sys) Sv = fma(co, sv[sidx + off], Sv);
-      if (hp) {
+      if (hp && (want_uv || kp)) {
         const double pq = sp[sidx + off];
-        gxp = fma(G, pq, gxp);
-        kxp = fma(K, pq, kxp);
+        if (want_uv) gxp = fma(G, pq, gxp);
+        if (kp) kxp = fma(K, pq, kxp);
       }
     });
     dir_rows<P>(1, ey, iy, 0, a.ney, [&](int row, int c, int off) {
@@ -167,12 +176,12 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
       if (hv) {
         const double vq = sv[sidx + off];
         if (sys) Sv = fma(co, vq, Sv);
-        gyv = fma(G, vq, gyv);
+        if (want_c) gyv = fma(G, vq, gyv);
       }
-      if (hp) {
+      if (hp && (want_uv || kp)) {
         const double pq = sp[sidx + off];
-        gyp = fma(G, pq, gyp);
-        kyp = fma(K, pq, kyp);
+        if (want_uv) gyp = fma(G, pq, gyp);
+        if (kp) kyp = fma(K, pq, kyp);
       }
     });
     if (want_uv) {
@@ -197,9 +206,9 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
         }
       }
     }
-    if (a.rc) {
+    if (want_c) {
       const bool pinned = static_cast<int64_t>(gx) * NY + gy == a.pin;
-      const double pinrow = own ? (a.p ? sp[sidx] : 0.0) - a.pin_val : 0.0;
+      const double pinrow = own ? (hp ? sp[sidx] : 0.0) - a.pin_val : 0.0;
       double z;
       if (pinned && !a.pin_first)
         z = pinrow;
@@ -214,7 +223,7 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
   }
 }
 
-template <int P>
+template <int P, int F>
 static void launch_ns_tile(const NsArgs& a, hipStream_t s) {
   using T = NsTile<P>;
   const int ncols = a.ex_end - a.ex_begin;
@@ -222,7 +231,7 @@ static void launch_ns_tile(const NsArgs& a, hipStream_t s) {
   const int tiles_y = (a.ney + T::TYE) / T::TYE;
   const int ntiles = tiles_x * tiles_y;
   const int per_xcd = (ntiles + 7) / 8;
-  hipLaunchKernelGGL(ns_apply_tile<P>, dim3(static_cast<unsigned>(8 * per_xcd)), dim3(T::THREADS), 0, s, a, tiles_y,
+  hipLaunchKernelGGL((ns_apply_tile<P, F>), dim3(static_cast<unsigned>(8 * per_xcd)), dim3(T::THREADS), 0, s, a, tiles_y,
                      ntiles, per_xcd);
 }
 
@@ -291,10 +300,18 @@ int sem_ns_apply(sem_handle* h, const sem_ns_desc* d, const double* u, const dou
   a.lb1 = static_cast<int>(h->line_end);
   a.n_local = h->n_local;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // the Schur gradient (p in; ru, rv out) and divergence (u, v, p in; rc out) run specialised kernels
+  const int form = ((u || v) ? sem::NS_U : 0) | (p ? sem::NS_P : 0) | ((ru || rv) ? sem::NS_UV_OUT : 0) |
+                   (rc ? sem::NS_C_OUT : 0);
   switch (h->P) {
-#define SEM_NSCASE(PP)                 \
-  case PP:                             \
-    sem::launch_ns_tile<PP>(a, s);     \
+#define SEM_NSCASE(PP)                                                        \
+  case PP:                                                                    \
+    if (form == (sem::NS_P | sem::NS_UV_OUT))                                 \
+      sem::launch_ns_tile<PP, sem::NS_P | sem::NS_UV_OUT>(a, s);              \
+    else if (form == (sem::NS_U | sem::NS_P | sem::NS_C_OUT))                 \
+      sem::launch_ns_tile<PP, sem::NS_U | sem::NS_P | sem::NS_C_OUT>(a, s);   \
+    else                                                                      \
+      sem::launch_ns_tile<PP, sem::NS_ALL>(a, s);                             \
     break;
     SEM_NSCASE(1) SEM_NSCASE(2) SEM_NSCASE(3) SEM_NSCASE(4) SEM_NSCASE(5) SEM_NSCASE(6) SEM_NSCASE(7) SEM_NSCASE(8)
     SEM_NSCASE(9) SEM_NSCASE(10) SEM_NSCASE(11) SEM_NSCASE(12) SEM_NSCASE(13) SEM_NSCASE(14) SEM_NSCASE(15)

@@ -71,3 +71,60 @@ def strided_inverse(A):
     if st != 0:
         raise RuntimeError(f"rocsolver_dgetri_strided_batched: status {st}")
     return X, info
+
+
+def _split(n):
+    """Leading block size of a 2 x 2 split: half of n, rounded up to a multiple of 64 (GEMM tiles)."""
+    h = (n // 2 + 63) // 64 * 64
+    return h if h < n else n // 2
+
+
+def block_inverse(A, base=64, out=None):
+    """Inverse of one square float64 matrix by 2 x 2 block recursion, all but the leaves in GEMMs:
+        A = [[A11, A12], [A21, A22]],  X11 = A11^-1,  T = X11 A12,  U = A21 X11,
+        S = A22 - A21 T  (the Schur complement),  Y = S^-1,
+        A^-1 = [[X11 + T Y U, -T Y], [-Y U, Y]].
+    Six GEMMs of half size per level (2 n^3 flops in all, the flops of getrf + getri), written straight
+    into the quadrants of the result (views with a leading dimension, no copies); leaves of at most
+    `base` rows inverted in one launch each by the Gauss-Jordan kernel of this library on the GPU
+    (sem_dense_inverse_small, partial pivoting within the leaf; rocSOLVER took ~130 us per 64^2 leaf,
+    tools/pivot_probe.py --profile), by torch's pivoted LU on the host.  No pivoting across the split: every leading block
+    must be regular, which holds for the diagonally dominated pivot blocks of the interface sweep and is
+    not assumed -- the caller checks A X - I (velocity_solve.pivot_inverse) and falls back to a pivoted
+    LU when it misses.  A singular leaf gives non-finite entries, never an exception."""
+    return _block_inv(A, base, torch.empty_like(A) if out is None else out)
+
+
+def small_inverse_into(A, X):
+    """X = A^-1 for one n x n float64 CUDA block, n <= 64, through the library's one-workgroup
+    Gauss-Jordan kernel (sem_dense_inverse_small); A and X may be row-major views with a leading
+    dimension.  Non-finite entries for a singular block."""
+    from . import _lib
+    n = A.shape[-1]
+    if A.stride(1) != 1 or X.stride(1) != 1:
+        raise ValueError("small_inverse_into needs unit column stride")
+    lib = _lib.load()
+    _lib.check(lib.sem_dense_inverse_small(C.c_void_p(A.data_ptr()), A.stride(0), C.c_void_p(X.data_ptr()),
+                                           X.stride(0), n,
+                                           C.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)))
+    return X
+
+
+def _block_inv(A, base, X):
+    n = A.shape[-1]
+    if A.is_cuda and n <= 64:   # the one-launch Gauss-Jordan leaf
+        return small_inverse_into(A, X)
+    if n <= base:
+        X.copy_(torch.linalg.inv_ex(A)[0])
+        return X
+    h = _split(n)
+    A11, A12, A21, A22 = A[:h, :h], A[:h, h:], A[h:, :h], A[h:, h:]
+    X11, X12, X21, X22 = X[:h, :h], X[:h, h:], X[h:, :h], X[h:, h:]
+    _block_inv(A11, base, X11)
+    T = X11 @ A12
+    U = A21 @ X11
+    _block_inv(torch.addmm(A22, A21, T, alpha=-1.0), base, X22)
+    torch.addmm(X12, T, X22, beta=0.0, alpha=-1.0, out=X12)
+    torch.addmm(X21, X22, U, beta=0.0, alpha=-1.0, out=X21)
+    X11.addmm_(X12, U, alpha=-1.0)
+    return X

@@ -23,7 +23,7 @@ on shared lines.
 """
 import torch
 
-from .velocity_solve import VelocityJacobianSolver, batched_inverse
+from .velocity_solve import VelocityJacobianSolver, pivot_inverse
 
 
 class StripLineSolver(VelocityJacobianSolver):
@@ -69,7 +69,7 @@ class StripLineSolver(VelocityJacobianSolver):
             return super()._sweep_factor(S_diag, S_up, S_lo)
         n, m = self.nex, self.m
         dev, f64 = self.device, torch.float64
-        inv = lambda A: batched_inverse(A[None])[0]  # noqa: E731
+        inv = pivot_inverse
         if n == 1:
             R = torch.stack((torch.stack((S_diag[0], S_up[0])), torch.stack((S_lo[0], S_diag[1]))))
             self._T = None

@@ -116,27 +116,52 @@ def batched_inverse(A, max_batch=None, sample=8):
     return out
 
 
-_PIVOT_INV = os.environ.get("SEM_PIVOT_INV", "lu")   # "lu" | "inv" | "strided" (A/B of the sweep pivots)
+_PIVOT_INV = os.environ.get("SEM_PIVOT_INV", "block")  # "block" | "lu" | "inv" | "strided" (sweep pivots)
+
+
+def _pivot_ok(A, X, r):
+    """|A (X r) - r| within 8 n^2 eps |A| |X| |r| (the relative bound of _bad_blocks, on one probe)."""
+    n = A.shape[-1]
+    res = (A @ (X @ r) - r).abs().max()
+    tol = 8.0 * n * n * torch.finfo(A.dtype).eps * A.abs().max() * X.abs().max() * r.abs().max()
+    return bool(res <= tol)
 
 
 def pivot_inverse(A):
-    """Inverse of one large pivot block of the interface sweep (m x m, m up to 3,074 at cfg5): an LU
-    factorisation and a triangular solve against the identity (getrf + getrs: TRSM-rich, faster than
-    getri's inversion of U on this stack), checked on a random probe vector: |A (X r) - r| against
-    n eps |A| |X| |r|; a miss falls back to the checked batched path."""
+    """Inverse of one large pivot block of the interface sweep (m x m, m up to 3,074 at cfg5).
+
+    Default ("block"): the GEMM-recursive inverse (sem_amd/linalg.py block_inverse) -- rocSOLVER's
+    getrf runs at 2.4 TFLOP/s on one 3,074^2 block against 55 for a GEMM of that size on MI355X
+    (tools/pivot_probe.py, profiles/r03/cfg5/pivot_probe.jsonl), and the 129 sequential pivots of the cfg5
+    block-Thomas sweep spent ~3.5 s there.  The recursion does not pivot across its splits, so the result
+    is checked on a random probe vector (|A (X r) - r| within 8 n^2 eps |A| |X| |r|); on a miss
+    E = A X - I is formed (one GEMM) and the inverse refined by one Newton step X <- X - X E when E is a
+    contraction (row sums below 1/2: the error squares), checked again; otherwise -- a leading block
+    singular or badly conditioned -- it is replaced by the pivoted route.
+    "lu": LU factorisation and a triangular solve against the identity (getrf + getrs), checked on a
+    random probe vector; a miss falls back to the checked batched path (batched_inverse)."""
+    n = A.shape[-1]
+    g = torch.Generator(device=A.device).manual_seed(7)
+    r = torch.rand(n, dtype=A.dtype, device=A.device, generator=g) - 0.5
+    if _PIVOT_INV == "block" and n > 64:
+        from ..linalg import block_inverse
+        X = block_inverse(A)
+        if _pivot_ok(A, X, r):
+            return X
+        E = A @ X
+        E.diagonal().sub_(1.0)
+        if bool(E.abs().sum(dim=1).max() < 0.5):
+            X = X - X @ E
+            if _pivot_ok(A, X, r):
+                return X
     if _PIVOT_INV == "strided":
         return batched_inverse(A)
     if _PIVOT_INV == "inv":
         X = torch.linalg.inv(A)
     else:
         LU, piv = torch.linalg.lu_factor(A)
-        X = torch.linalg.lu_solve(LU, piv, torch.eye(A.shape[-1], dtype=A.dtype, device=A.device))
-    g = torch.Generator(device=A.device).manual_seed(7)
-    r = torch.rand(A.shape[-1], dtype=A.dtype, device=A.device, generator=g) - 0.5
-    res = (A @ (X @ r) - r).abs().max()
-    n = A.shape[-1]
-    tol = 8.0 * n * torch.finfo(A.dtype).eps * A.abs().max() * X.abs().max() * r.abs().max() * n
-    if not bool(res <= tol):
+        X = torch.linalg.lu_solve(LU, piv, torch.eye(n, dtype=A.dtype, device=A.device))
+    if not _pivot_ok(A, X, r):
         return batched_inverse(A)
     return X
 

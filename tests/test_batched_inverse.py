@@ -75,3 +75,43 @@ def test_raises_when_no_route_inverts(monkeypatch):
     monkeypatch.setattr(torch.linalg, "solve", lambda a, b: torch.zeros_like(b))
     with pytest.raises(RuntimeError, match="could not be inverted"):
         VS.batched_inverse(A, max_batch=4)
+
+
+def test_block_inverse_matches_lu():
+    """The GEMM-recursive inverse of the sweep pivots (sem_amd/linalg.py) against the pivoted LU."""
+    from sem_amd.linalg import block_inverse
+    r = np.random.default_rng(11)
+    n = 700                                  # splits 384 | 316, then leaves of <= 256 rows
+    A = torch.as_tensor(r.uniform(-1, 1, (n, n)) + 4 * np.sqrt(n) * np.eye(n))
+    X = block_inverse(A, base=128)
+    want = torch.linalg.inv(A)
+    assert (X - want).abs().max() <= 1e-12 * want.abs().max()
+
+
+def test_pivot_inverse_routes(monkeypatch):
+    """pivot_inverse: the block route accepts an accurate inverse, refines a slightly wrong one by one
+    Newton step, and falls back to the pivoted LU when a leading block is singular (no pivoting across
+    the recursion's split)."""
+    from sem_amd import linalg
+    monkeypatch.setattr(VS, "_PIVOT_INV", "block")
+    r = np.random.default_rng(12)
+    n = 600
+    A = torch.as_tensor(r.uniform(-1, 1, (n, n)) + 4 * np.sqrt(n) * np.eye(n))
+    want = torch.linalg.inv(A)
+    X = VS.pivot_inverse(A)
+    assert (X - want).abs().max() <= 1e-12 * want.abs().max()
+    # a perturbed block inverse: E = A X - I is a contraction, one Newton step squares it
+    real = linalg.block_inverse
+    monkeypatch.setattr(linalg, "block_inverse", lambda a, base=256, out=None: real(a) * (1 + 1e-7))
+    X = VS.pivot_inverse(A)
+    assert (X - want).abs().max() <= 1e-11 * want.abs().max()
+    monkeypatch.setattr(linalg, "block_inverse", real)
+    # leading block exactly singular: the recursion yields non-finite entries, the LU route takes over
+    Z = torch.zeros((n, n), dtype=torch.float64)
+    Z[: n // 2, n // 2:] = torch.eye(n - n // 2, dtype=torch.float64)[: n // 2]
+    Z[n // 2:, : n // 2] = torch.eye(n // 2, dtype=torch.float64)[: n - n // 2]
+    Z += torch.as_tensor(r.uniform(-1e-3, 1e-3, (n, n))) * torch.as_tensor(np.kron(
+        np.array([[0.0, 1.0], [1.0, 1.0]]), np.ones((n // 2, n // 2))))
+    X = VS.pivot_inverse(Z)
+    E = Z @ X - torch.eye(n, dtype=torch.float64)
+    assert E.abs().max() <= 1e-10
