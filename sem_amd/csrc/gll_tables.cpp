@@ -45,6 +45,7 @@ Tuning& tuning() {
     r.v[SEM_TUNE_MARCH_WG] = env_int("SEM_MARCH_WG");
     r.v[SEM_TUNE_MFMA_TILE] = env_int("SEM_MFMA_TILE");
     r.v[SEM_TUNE_COL_TILE] = env_int("SEM_COL_TILE");
+    r.v[SEM_TUNE_NS_APPLY] = env_int("SEM_NS_APPLY");
     return r;
   }();
   return t;

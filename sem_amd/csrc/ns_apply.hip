@@ -22,6 +22,8 @@
 
 #include <string>
 
+#include "apply_common.h"
+#include "gll_consts.h"
 #include "sem_internal.h"
 
 namespace sem {
@@ -223,6 +225,364 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
   }
 }
 
+// ---- Band form (round 3, the default): the assembled 1-D rows of the operators with compile-time
+// coefficients, every lane on a wave-uniform row (the structure of apply_band.hip's band kernel).
+//
+// Tile = one element-column position (P lines; the closing line of the strip is a ghost position of one
+// line) x TYE element rows (BY = TYE P <= 64 columns; the closing column is a ghost position of one
+// column).  Staged in LDS: u, v, p over lines gx0-P .. gx0+P and columns gy0-P .. gy0+BY (absent nodes 0),
+// and cv of the owned block when the Sys rows need it and cv is not v itself.  Two phases, 4 waves, wave
+// w takes the element rows w, w+4, ... in both:
+//   Y  lane = (line r, element b): the y-direction rows of element b on line r from a register window
+//      along the line -> LDS (Sys u, Sys v + G_y p, G_y v, K p of the y direction)
+//   X  lane = column c: the x-direction rows of its column from a register window across the lines,
+//      added onto the Y sums, then the pointwise terms, the row replacements and the (coalesced) stores.
+// Every coefficient is an immediate, each staged value is read from LDS once per window, and no lane of
+// a wave waits on another lane's row type (row 0 -- the shared node -- is a whole wave's row).
+template <int P>
+struct NsBand {
+  static constexpr int n = P + 1;
+  static constexpr int NW = 4, THREADS = 64 * NW;
+  static constexpr int TYE = 64 / P > 0 ? 64 / P : 1;
+  static constexpr int BY = TYE * P;          // owned columns of a full tile
+  static constexpr int SX = 2 * P + 1;        // staged lines gx0-P .. gx0+P
+  static constexpr int SY = BY + P + 1;       // staged columns gy0-P .. gy0+BY
+  static constexpr int PIT = SY | 1;          // odd pitch
+  static constexpr int NST = (SX * SY + THREADS - 1) / THREADS;   // staging loads per thread and field
+  static constexpr int NCV = (P * BY + THREADS - 1) / THREADS;    // cv staging loads per thread
+};
+
+// GLL weight w_J of order P for a runtime J (compile-time constants, no memory access)
+template <int P>
+__device__ __forceinline__ double ns_gll_w(int J) {
+  double r = 0.0;
+  for_rows(std::make_integer_sequence<int, P + 1>{}, [&](auto K) {
+    constexpr int k = decltype(K)::value;
+    if (J == k) r = GllConst<P>::w[k];
+  });
+  return r;
+}
+
+template <int B, int E, int S, class Fn>
+__device__ __forceinline__ void ns_sfor(Fn&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    ns_sfor<B + S, E, S>(f);
+  }
+}
+
+struct NsTileCtx {
+  int gx0, gy0, n0, nlx, ncy;  // first line / column, first element row, lines, columns of the tile
+  bool hasLx, hasRx;           // the tile's element column has a left neighbour / is not the ghost
+};
+
+// Y phase of wave W: rows W, W+4, ... of element b on line r (lane = (r, b)); sums -> yu, yv, yg, yk.
+template <int P, int F, int W>
+__device__ __forceinline__ void ns_y_rows(const NsArgs& a, const NsTileCtx& t, const double* su, const double* sv,
+                                          const double* sp, const double* scv, bool cv_is_v, const double* ws,
+                                          double* yu, double* yv, double* yg, double* yk) {
+  using C = NsBand<P>;
+  using G = GllConst<P>;
+  constexpr int n = C::n, BY = C::BY, PIT = C::PIT;
+  constexpr bool HU = (F & NS_U) != 0, HP = (F & NS_P) != 0, OUV = (F & NS_UV_OUT) != 0, OC = (F & NS_C_OUT) != 0;
+  constexpr bool SYS = HU && OUV;
+  if constexpr (W < P) {
+    const int l = threadIdx.x & 63;
+    if (l >= P * C::TYE) return;
+    const int r = l / C::TYE, b = l - r * C::TYE;
+    const int pos = t.n0 + b;
+    if (r >= t.nlx || pos > a.ney) return;
+    const bool ghost = pos == a.ney, hasL = pos > 0;
+    const double mx = wsum1(t.gx0 + r, P, a.ex_begin, a.ex_end, ws);
+    constexpr int q0 = W == 0 ? 0 : P;  // only row 0 reads the lower neighbour element
+    const int base = (P + r) * PIT + b * P;
+    double tu[2 * P + 1], tv[2 * P + 1], tp[2 * P + 1];
+#pragma unroll
+    for (int q = q0; q <= 2 * P; ++q) {
+      if constexpr (HU) {
+        tu[q] = su[base + q];
+        tv[q] = sv[base + q];
+      }
+      if constexpr (HP) tp[q] = sp[base + q];
+    }
+    const double fy = a.fKy * mx, hxm = a.hx * mx, sym = a.sy * mx;
+    ns_sfor<W, P, C::NW>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      if (ghost && j != 0) return;  // the ghost position holds its row 0 only
+      const int c = b * P + j;      // tile column of the node
+      double gyc = 0.0;
+      if constexpr (SYS) {
+        const double cvn = a.cv ? (cv_is_v ? tv[P + j] : scv[r * BY + c]) : 1.0;
+        gyc = a.fY * cvn * mx;
+      }
+      double Su = 0.0, Sv = 0.0, gp = 0.0, gv = 0.0, kp = 0.0;
+      auto term = [&](double K, double Gc, int q) {
+        if constexpr (SYS) {
+          const double co = fma(gyc, Gc, fy * K);
+          Su = fma(co, tu[q], Su);
+          Sv = fma(co, tv[q], Sv);
+        }
+        if constexpr (HU && OC) gv = fma(Gc, tv[q], gv);
+        if constexpr (HP && OUV) gp = fma(Gc, tp[q], gp);
+        if constexpr (HP && OC) kp = fma(K, tp[q], kp);
+      };
+      if constexpr (j == 0) {
+        if (hasL) ns_sfor<0, n, 1>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            term(G::K[P * n + q], G::G[P * n + q], q);
+          });
+        if (!ghost) ns_sfor<0, n, 1>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            term(G::K[q], G::G[q], P + q);
+          });
+      } else {
+        ns_sfor<0, n, 1>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          term(G::K[j * n + q], G::G[j * n + q], P + q);
+        });
+      }
+      const int o = r * BY + c;
+      if constexpr (SYS) yu[o] = Su;
+      if constexpr (OUV) yv[o] = SYS ? fma(hxm, gp, Sv) : hxm * gp;
+      if constexpr (HU && OC) yg[o] = hxm * gv;
+      if constexpr (HP && OC) yk[o] = sym * kp;
+    });
+  }
+}
+
+// X phase of wave W: rows (lines) W, W+4, ... of column c (lane = c): the x sums onto the Y sums, then the
+// node's pointwise terms, row replacements and stores (the arithmetic of ns_apply_tile's epilogue).
+template <int P, int F, int W>
+__device__ __forceinline__ void ns_x_rows(const NsArgs& a, const NsTileCtx& t, const double* su, const double* sv,
+                                          const double* sp, bool cu_is_u, const double* ws, const double* yu,
+                                          const double* yv, const double* yg, const double* yk) {
+  using C = NsBand<P>;
+  using G = GllConst<P>;
+  constexpr int n = C::n, BY = C::BY, PIT = C::PIT;
+  constexpr bool HU = (F & NS_U) != 0, HP = (F & NS_P) != 0, OUV = (F & NS_UV_OUT) != 0, OC = (F & NS_C_OUT) != 0;
+  constexpr bool SYS = HU && OUV;
+  if constexpr (W < P) {
+    const int c = threadIdx.x & 63;
+    if (c >= t.ncy) return;
+    const int gy = t.gy0 + c, NY = a.NY;
+    const double my = wsum1(gy, P, 0, a.ney, ws);
+    constexpr int q0 = W == 0 ? 0 : P;  // only row 0 reads the left neighbour element
+    double tu[2 * P + 1], tv[2 * P + 1], tp[2 * P + 1];
+#pragma unroll
+    for (int q = q0; q <= 2 * P; ++q) {
+      if constexpr (HU) {
+        tu[q] = su[q * PIT + P + c];
+        tv[q] = sv[q * PIT + P + c];
+      }
+      if constexpr (HP) tp[q] = sp[q * PIT + P + c];
+    }
+    const bool want_uv = OUV && (a.ru || a.rv), want_c = OC && a.rc;
+    const double fx = a.fKx * my, hym = a.hy * my, sxm = a.sx * my;
+    ns_sfor<W, P, C::NW>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if (i >= t.nlx) return;  // the ghost position holds its line 0 only
+      const int gx = t.gx0 + i;
+      const int64_t q = static_cast<int64_t>(gx - a.lb0) * NY + gy;
+      const int64_t qv = static_cast<int64_t>(gx - a.lb0) * a.pitch + gy;
+      const double mx = wsum1(gx, P, a.ex_begin, a.ex_end, ws);
+      const int o = i * BY + c;
+      double gxc = 0.0;
+      if constexpr (SYS) {
+        const double cun = a.cu ? (cu_is_u ? tu[P + i] : a.cu[q]) : 1.0;
+        gxc = a.fX * cun * my;
+      }
+      double Su = 0.0, Sv = 0.0, gp = 0.0, gu = 0.0, kp = 0.0;
+      if constexpr (SYS) {
+        Su = yu[o];
+        Sv = yv[o];
+      }
+      auto term = [&](double K, double Gc, int qq) {
+        if constexpr (SYS) {
+          const double co = fma(gxc, Gc, fx * K);
+          Su = fma(co, tu[qq], Su);
+          Sv = fma(co, tv[qq], Sv);
+        }
+        if constexpr (HU && OC) gu = fma(Gc, tu[qq], gu);
+        if constexpr (HP && OUV) gp = fma(Gc, tp[qq], gp);
+        if constexpr (HP && OC) kp = fma(K, tp[qq], kp);
+      };
+      if constexpr (i == 0) {
+        if (t.hasLx) ns_sfor<0, n, 1>([&](auto Q) {
+            constexpr int qq = decltype(Q)::value;
+            term(G::K[P * n + qq], G::G[P * n + qq], qq);
+          });
+        if (t.hasRx) ns_sfor<0, n, 1>([&](auto Q) {
+            constexpr int qq = decltype(Q)::value;
+            term(G::K[qq], G::G[qq], P + qq);
+          });
+      } else {
+        ns_sfor<0, n, 1>([&](auto Q) {
+          constexpr int qq = decltype(Q)::value;
+          term(G::K[i * n + qq], G::G[i * n + qq], P + qq);
+        });
+      }
+      const bool own = !(gx == a.lb1 && a.ex_end < a.nex);  // a strip's right interface line: its right owner's
+      const bool dir = a.mask ? a.mask[q] != 0
+                              : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
+                                 ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
+      const double u0 = HU ? tu[P + i] : 0.0, v0 = HU ? tv[P + i] : 0.0;
+      if constexpr (OUV) {
+        if (want_uv) {
+          if (dir) {
+            if (a.ru) a.ru[qv] = own ? u0 - (a.gu ? a.gu[q] : 0.0) : 0.0;
+            if (a.rv) a.rv[qv] = own ? v0 - (a.gv ? a.gv[q] : 0.0) : 0.0;
+          } else {
+            const double fm = a.fM * mx * my;
+            if (a.ru) {
+              double z = fma(fm, u0, Su);
+              if (a.juu && own) z = fma(a.juu[q], u0, z);
+              if (a.juv && own) z = fma(a.juv[q], v0, z);
+              a.ru[qv] = fma(hym, gp, z);
+            }
+            if (a.rv) {
+              double z = fma(fm, v0, SYS ? Sv : yv[o]);  // Sv started from yv (Sys v + G_y p, y rows)
+              if (a.jvu && own) z = fma(a.jvu[q], u0, z);
+              if (a.jvv && own) z = fma(a.jvv[q], v0, z);
+              if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
+              a.rv[qv] = z;
+            }
+          }
+        }
+      }
+      if constexpr (OC) {
+        if (want_c) {
+          const bool pinned = static_cast<int64_t>(gx) * NY + gy == a.pin;
+          const double pinrow = own ? (HP ? tp[P + i] : 0.0) - a.pin_val : 0.0;
+          double z;
+          if (pinned && !a.pin_first)
+            z = pinrow;
+          else if (dir)  // the (K p) row
+            z = HP ? fma(sxm, kp, yk[o]) : 0.0;
+          else if (pinned)
+            z = pinrow;
+          else
+            z = HU ? a.c_div * fma(hym, gu, yg[o]) : 0.0;
+          a.rc[q] = z;
+        }
+      }
+    });
+  }
+}
+
+template <int P, int F>
+__global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y, int ntiles, int per_xcd, int ubytes,
+                                                    int pbytes) {
+  using C = NsBand<P>;
+  constexpr int n = P + 1, BY = C::BY, SX = C::SX, SY = C::SY, PIT = C::PIT;
+  constexpr bool HU = (F & NS_U) != 0, HP = (F & NS_P) != 0, OUV = (F & NS_UV_OUT) != 0, OC = (F & NS_C_OUT) != 0;
+  constexpr bool SYS = HU && OUV;
+  __shared__ double ws[n];
+  __shared__ double su[HU ? SX * PIT : 1], sv[HU ? SX * PIT : 1], sp[HP ? SX * PIT : 1];
+  __shared__ double scv[SYS ? P * BY : 1];
+  __shared__ double yu[SYS ? P * BY : 1], yv[OUV ? P * BY : 1], yg[(HU && OC) ? P * BY : 1];
+  __shared__ double yk[(HP && OC) ? P * BY : 1];
+  const int bid = blockIdx.x;
+  const int tile = (bid & 7) * per_xcd + (bid >> 3);
+  if (tile >= ntiles) return;
+  const int tx = tile / tiles_y, ty = tile - tx * tiles_y;
+  const int tid = threadIdx.x;
+  NsTileCtx t;
+  t.gx0 = (a.ex_begin + tx) * P;
+  t.n0 = ty * C::TYE;
+  t.gy0 = t.n0 * P;
+  t.hasLx = tx > 0;
+  t.hasRx = a.ex_begin + tx < a.ex_end;
+  t.nlx = t.hasRx ? P : 1;
+  t.ncy = min(BY, a.NY - t.gy0);
+  const bool cv_is_v = a.cv == a.v, cu_is_u = a.cu == a.u;
+  // ---- staging: every load issued before the first LDS write (buffer loads outside [0, bytes) read 0;
+  // columns outside the mesh would wrap into neighbouring lines and are zeroed explicitly)
+  const int64_t pitch = a.pitch;
+  const auto ru_ = brsrc(HU ? a.u : nullptr, HU && a.u ? ubytes : 0);
+  const auto rv_ = brsrc(HU ? a.v : nullptr, HU && a.v ? ubytes : 0);
+  const auto rp_ = brsrc(HP ? a.p : nullptr, HP && a.p ? pbytes : 0);
+  double st_u[C::NST], st_v[C::NST], st_p[C::NST];
+#pragma unroll
+  for (int s = 0; s < C::NST; ++s) {
+    const int k = min(tid + s * C::THREADS, SX * SY - 1);
+    const int r = k / SY, cc = k - r * SY;
+    const int lx = t.gx0 - P + r - a.lb0;  // local line (out of range -> out-of-bounds offset)
+    const int gy = t.gy0 - P + cc;
+    const bool ok = lx >= 0 && t.gx0 - P + r <= a.lb1;
+    if constexpr (HU) {
+      st_u[s] = bload(ru_, ok ? static_cast<int>((lx * pitch + gy) * 8) : -1);
+      st_v[s] = bload(rv_, ok ? static_cast<int>((lx * pitch + gy) * 8) : -1);
+    }
+    if constexpr (HP) st_p[s] = bload(rp_, ok ? (lx * a.NY + gy) * 8 : -1);
+  }
+  double st_c[SYS ? C::NCV : 1];
+  if constexpr (SYS) {
+    const bool stage_cv = a.cv && !cv_is_v;
+#pragma unroll
+    for (int s = 0; s < C::NCV; ++s) {
+      const int k = tid + s * C::THREADS;
+      const int r = k / BY, cc = k - r * BY;
+      st_c[s] = (stage_cv && k < P * BY && r < t.nlx && cc < t.ncy)
+                    ? a.cv[static_cast<int64_t>(t.gx0 + r - a.lb0) * a.NY + t.gy0 + cc]
+                    : 0.0;
+    }
+  }
+  if (tid < n) ws[tid] = ns_gll_w<P>(tid);
+#pragma unroll
+  for (int s = 0; s < C::NST; ++s) {
+    const int k = tid + s * C::THREADS;
+    if (k < SX * SY) {
+      const int r = k / SY, cc = k - r * SY;
+      const int gy = t.gy0 - P + cc;
+      const bool inside = gy >= 0 && gy < a.NY;
+      if constexpr (HU) {
+        su[r * PIT + cc] = inside ? st_u[s] : 0.0;
+        sv[r * PIT + cc] = inside ? st_v[s] : 0.0;
+      }
+      if constexpr (HP) sp[r * PIT + cc] = inside ? st_p[s] : 0.0;
+    }
+  }
+  if constexpr (SYS) {
+#pragma unroll
+    for (int s = 0; s < C::NCV; ++s) {
+      const int k = tid + s * C::THREADS;
+      if (k < P * BY) scv[k] = st_c[s];
+    }
+  }
+  __syncthreads();
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  switch (w) {
+    case 0: ns_y_rows<P, F, 0>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
+    case 1: ns_y_rows<P, F, 1>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
+    case 2: ns_y_rows<P, F, 2>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
+    default: ns_y_rows<P, F, 3>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
+  }
+  __syncthreads();
+  switch (w) {
+    case 0: ns_x_rows<P, F, 0>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
+    case 1: ns_x_rows<P, F, 1>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
+    case 2: ns_x_rows<P, F, 2>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
+    default: ns_x_rows<P, F, 3>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
+  }
+}
+
+template <int P, int F>
+static bool launch_ns_band(const NsArgs& a, hipStream_t s) {
+  using C = NsBand<P>;
+  // buffer-resource offsets are 32-bit: the band form covers strips below 2 GB per operand
+  const int64_t nl = a.lb1 - a.lb0;
+  const int64_t ub = (nl * a.pitch + a.NY) * 8, pb = (nl * a.NY + a.NY) * 8;
+  if (ub >= (int64_t{1} << 31) || pb >= (int64_t{1} << 31)) return false;
+  const int ncols = a.ex_end - a.ex_begin;
+  const int tiles_x = ncols + 1;  // positions 0..ncols (ncols: the closing line)
+  const int tiles_y = (a.ney + C::TYE) / C::TYE;
+  const int ntiles = tiles_x * tiles_y;
+  const int per_xcd = (ntiles + 7) / 8;
+  hipLaunchKernelGGL((ns_apply_band<P, F>), dim3(static_cast<unsigned>(8 * per_xcd)), dim3(C::THREADS), 0, s, a,
+                     tiles_y, ntiles, per_xcd, static_cast<int>(ub), static_cast<int>(pb));
+  return true;
+}
+
 template <int P, int F>
 static void launch_ns_tile(const NsArgs& a, hipStream_t s) {
   using T = NsTile<P>;
@@ -303,15 +663,21 @@ int sem_ns_apply(sem_handle* h, const sem_ns_desc* d, const double* u, const dou
   // the Schur gradient (p in; ru, rv out) and divergence (u, v, p in; rc out) run specialised kernels
   const int form = ((u || v) ? sem::NS_U : 0) | (p ? sem::NS_P : 0) | ((ru || rv) ? sem::NS_UV_OUT : 0) |
                    (rc ? sem::NS_C_OUT : 0);
+  // the band form by default; the tile form on request (SEM_NS_APPLY=1, in-process A/B: results agree to
+  // rounding, not bitwise) and for strips beyond the band form's 32-bit buffer offsets
+  const bool tile = sem::tune(SEM_TUNE_NS_APPLY) == 1;
   switch (h->P) {
-#define SEM_NSCASE(PP)                                                        \
-  case PP:                                                                    \
-    if (form == (sem::NS_P | sem::NS_UV_OUT))                                 \
-      sem::launch_ns_tile<PP, sem::NS_P | sem::NS_UV_OUT>(a, s);              \
-    else if (form == (sem::NS_U | sem::NS_P | sem::NS_C_OUT))                 \
-      sem::launch_ns_tile<PP, sem::NS_U | sem::NS_P | sem::NS_C_OUT>(a, s);   \
-    else                                                                      \
-      sem::launch_ns_tile<PP, sem::NS_ALL>(a, s);                             \
+#define SEM_NSCASE(PP)                                                                              \
+  case PP:                                                                                          \
+    if (form == (sem::NS_P | sem::NS_UV_OUT)) {                                                     \
+      if (tile || !sem::launch_ns_band<PP, sem::NS_P | sem::NS_UV_OUT>(a, s))                       \
+        sem::launch_ns_tile<PP, sem::NS_P | sem::NS_UV_OUT>(a, s);                                  \
+    } else if (form == (sem::NS_U | sem::NS_P | sem::NS_C_OUT)) {                                   \
+      if (tile || !sem::launch_ns_band<PP, sem::NS_U | sem::NS_P | sem::NS_C_OUT>(a, s))            \
+        sem::launch_ns_tile<PP, sem::NS_U | sem::NS_P | sem::NS_C_OUT>(a, s);                       \
+    } else {                                                                                        \
+      if (tile || !sem::launch_ns_band<PP, sem::NS_ALL>(a, s)) sem::launch_ns_tile<PP, sem::NS_ALL>(a, s); \
+    }                                                                                               \
     break;
     SEM_NSCASE(1) SEM_NSCASE(2) SEM_NSCASE(3) SEM_NSCASE(4) SEM_NSCASE(5) SEM_NSCASE(6) SEM_NSCASE(7) SEM_NSCASE(8)
     SEM_NSCASE(9) SEM_NSCASE(10) SEM_NSCASE(11) SEM_NSCASE(12) SEM_NSCASE(13) SEM_NSCASE(14) SEM_NSCASE(15)

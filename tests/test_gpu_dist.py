@@ -332,6 +332,9 @@ def _worker_cfg5_update(rank, world, port, q):
         m = ns._mesh
         z = torch.zeros(m.n_local, dtype=torch.float64, device=m.device)
         T = ns._dev(0.5 - ns.points[0])
+        say = (lambda msg: print(f"[cfg5 update rank 0] {msg}", file=sys.stderr, flush=True)) if rank == 0 \
+            else (lambda msg: None)
+        say("solver built")
         ns._get_residuals(z, z, z, T)
         ns._calc_jacobians(z, z)
         r = np.random.default_rng(77)
@@ -339,6 +342,7 @@ def _worker_cfg5_update(rank, world, port, q):
         t0 = _t.perf_counter()
         du, dv, dp = ns._get_update(*rhs)
         secs = _t.perf_counter() - t0
+        say(f"update {secs:.1f} s, {ns.schur_matvecs} Schur matvecs")
         lin = ns._get_dresiduals(du, dv, dp)
         err = ns._norm(*(a - b for a, b in zip(lin, rhs)))
         if rank == 0:

@@ -23,8 +23,18 @@ def _rel(a, b):
     return np.abs(np.asarray(a) - b).max() / max(np.abs(b).max(), 1e-300)
 
 
-@pytest.mark.parametrize("P,nex,ney,Re,Gr", CASES)
-def test_fused_residuals_match_oracle(gpu, P, nex, ney, Re, Gr):
+@pytest.fixture(params=["band", "tile"])
+def ns_kernel(request):
+    """sem_ns_apply's two forms (SEM_TUNE_NS_APPLY): the band form (default) and the LDS-tile form."""
+    from sem_amd import _lib
+    lib = _lib.load()
+    _lib.check(lib.sem_set_tuning(_lib.TUNE_NS_APPLY, 1 if request.param == "tile" else 0))
+    yield request.param
+    _lib.check(lib.sem_set_tuning(_lib.TUNE_NS_APPLY, 0))
+
+
+@pytest.mark.parametrize("P,nex,ney,Re,Gr", CASES + [(12, 3, 5, 1000.0, 40.0), (16, 2, 2, 300.0, 5.0)])
+def test_fused_residuals_match_oracle(gpu, ns_kernel, P, nex, ney, Re, Gr):
     from oracle import sem_oracle as O
     from sem_amd.solvers import NavierStokesSolver
     ref = O.NSOracle(1.0, 1.3, Re, Gr, P, nex, ney, u_N=1.0, v_W=0.25)

@@ -17,7 +17,10 @@ step() {  # name limit cmd...
 }
 for s in "$@"; do
   case $s in
-    gpu)        step gputests 1100 $PYT -q -m gpu tests ;;
+    gpu)        step gputests 1100 $PYT -m gpu tests ;;
+    gpurest)    step gpurest 900 $PYT -m gpu tests/test_gpu_krylov.py tests/test_gpu_ns_velocity.py \
+                  tests/test_gpu_partition.py tests/test_gpu_solvers.py tests/test_gpu_boussinesq.py tests/test_gpu_cfg4.py ;;
+    nsbenchab)  step nsbenchab 300 python tools/nsbench.py --kernels band,tile ;;
     cfg4)       step cfg4 300 $PYT -s tests/test_gpu_cfg4.py ;;
     nsapply)    step nsapply 300 $PYT tests/test_gpu_ns_apply.py ;;
     velocity)   step velocity 600 $PYT tests/test_gpu_ns_velocity.py ;;
@@ -37,7 +40,7 @@ for s in "$@"; do
       tools/pmc_run.sh "$O/pmc_mfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1
       tools/pmc_run.sh "$O/pmc_dot2" -- python tools/sweep_bench.py || exit 1 ;;
     pmcns)
-      tools/pmc_run.sh "$O/pmc_ns48" -- python tools/nsbench.py --meshes 8:48 --reps 200 || exit 1
+      tools/pmc_run.sh "$O/pmc_ns48" -- python tools/nsbench.py --meshes 8:48 --reps 100 || exit 1
       tools/pmc_run.sh "$O/pmc_ns128" -- python tools/nsbench.py --meshes 12:128 --reps 20 || exit 1
       tools/pmc_run.sh "$O/pmc_vel48" -- python tools/velocity_bench.py --ne 48 --P 8 --configs nested:cr --reps 20 \
         || exit 1 ;;
