@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 8
+#define SEM_ABI_VERSION 9
 
 enum sem_status {
   SEM_OK = 0,
@@ -293,6 +293,14 @@ typedef struct sem_nested_desc {
   double* T;
   double* C;
   double* Ye;
+  /* ABI 9: the edge Schur complement as its block-Thomas factors instead of the dense inverse Se (Se = NULL):
+   * per column Ed[k] = inverse pivot block k (N_ey+1 of ne1 x ne1), El[k] = lower block (edge k+1 <- k) and
+   * Eu[k] = Ed[k] A_up[k] (edge k <- k+1), N_ey each, column-major; the edge solve is then a forward and a
+   * back sweep over the column's N_ey+1 edges (one wavefront per column) reading O(N_ey ne1^2) doubles
+   * instead of the n_e^2 of the dense inverse (cfg5: 1.5 MB instead of 64 MB per column).  ne1 <= 32. */
+  const double* Ed;
+  const double* El;
+  const double* Eu;
 } sem_nested_desc;
 /* Column e's right-hand side at R + e ld_r (interior offsets o = (l-1) m + c N_y + gy), minus
  * aIB[e][l-1][s][.] xB[e+s][.] when aIB and xB are given (the back substitution r = b - A_IB x_B);

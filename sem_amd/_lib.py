@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE, TUNE_NS_APPLY = range(7)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
@@ -48,7 +48,8 @@ class SemVelocityDesc(C.Structure):
 class SemNestedDesc(C.Structure):
     _fields_ = [("P", C.c_int), ("nex", C.c_int), ("ney", C.c_int), ("nc", C.c_int), ("NY", C.c_int64),
                 ("Xi", C.c_void_p), ("Aei", C.c_void_p), ("Yie", C.c_void_p), ("Se", C.c_void_p),
-                ("pi", C.c_void_p), ("pe", C.c_void_p), ("T", C.c_void_p), ("C", C.c_void_p), ("Ye", C.c_void_p)]
+                ("pi", C.c_void_p), ("pe", C.c_void_p), ("T", C.c_void_p), ("C", C.c_void_p), ("Ye", C.c_void_p),
+                ("Ed", C.c_void_p), ("El", C.c_void_p), ("Eu", C.c_void_p)]
 
 
 class SemNsDesc(C.Structure):

@@ -231,14 +231,17 @@ __global__ __launch_bounds__(256) void ns_apply_tile(const NsArgs a, int tiles_y
 // Tile = one element-column position (P lines; the closing line of the strip is a ghost position of one
 // line) x TYE element rows (BY = TYE P <= 64 columns; the closing column is a ghost position of one
 // column).  Staged in LDS: u, v, p over lines gx0-P .. gx0+P and columns gy0-P .. gy0+BY (absent nodes 0),
-// and cv of the owned block when the Sys rows need it and cv is not v itself.  Two phases, 4 waves, wave
-// w takes the element rows w, w+4, ... in both:
-//   Y  lane = (line r, element b): the y-direction rows of element b on line r from a register window
-//      along the line -> LDS (Sys u, Sys v + G_y p, G_y v, K p of the y direction)
-//   X  lane = column c: the x-direction rows of its column from a register window across the lines,
-//      added onto the Y sums, then the pointwise terms, the row replacements and the (coalesced) stores.
-// Every coefficient is an immediate, each staged value is read from LDS once per window, and no lane of
-// a wave waits on another lane's row type (row 0 -- the shared node -- is a whole wave's row).
+// and cv of the owned block when the Sys rows need it and cv is not v itself (CVS).  4 waves; wave w takes
+// the element rows w, w+4, ... in both directions:
+//   Y   lane = (line r, element b): the y-direction rows of element b on line r (Sys u, Sys v + G_y p, and
+//       G_y v or K p for the continuity row) -> registers; wave 3 (the fewest y rows) also forms the x rows
+//       of the tile's first line over the LEFT element (the only use of the P halo lines gx0-P .. gx0-1)
+//   --- barrier: the halo lines are dead; the Y sums and the left-element sums go to LDS over them
+//   X   lane = column c: the x-direction rows of its column onto the Y sums, then the node's pointwise
+//       terms, the row replacements and the (coalesced) stores.
+// Every coefficient is an immediate; each staged value of the element is read from LDS once per window;
+// no lane waits on another lane's row type (row 0 -- the shared node -- is a whole wave's row).  Reusing
+// the halo lines for the Y sums keeps the LDS to the staged window, 3 workgroups per CU at P = 12.
 template <int P>
 struct NsBand {
   static constexpr int n = P + 1;
@@ -248,8 +251,11 @@ struct NsBand {
   static constexpr int SX = 2 * P + 1;        // staged lines gx0-P .. gx0+P
   static constexpr int SY = BY + P + 1;       // staged columns gy0-P .. gy0+BY
   static constexpr int PIT = SY | 1;          // odd pitch
+  static constexpr int FLD = SX * PIT;        // one staged field
   static constexpr int NST = (SX * SY + THREADS - 1) / THREADS;   // staging loads per thread and field
   static constexpr int NCV = (P * BY + THREADS - 1) / THREADS;    // cv staging loads per thread
+  static constexpr int XLW = 3;               // the wave with the fewest y rows (rows 3, 7, ...)
+  static constexpr int rows(int w) { return w < P ? (P - 1 - w) / NW + 1 : 0; }
 };
 
 // GLL weight w_J of order P for a runtime J (compile-time constants, no memory access)
@@ -271,221 +277,72 @@ __device__ __forceinline__ void ns_sfor(Fn&& f) {
   }
 }
 
+// Which sums a form needs (compile time): the staged fields and the Y / left-element sum arrays.
+template <int F>
+struct NsForm {
+  static constexpr bool HU = (F & NS_U) != 0, HP = (F & NS_P) != 0;
+  static constexpr bool OUV = (F & NS_UV_OUT) != 0, OC = (F & NS_C_OUT) != 0;
+  static constexpr bool SYS = HU && OUV;
+  static constexpr int NF = (HU ? 2 : 0) + (HP ? 1 : 0);               // staged fields u, v | p
+  static constexpr int IU = 0, IV = 1, IP = HU ? 2 : 0;                // their order in the staging
+  static constexpr int YU = 0, YV = SYS ? 1 : 0, YC = (SYS ? 1 : 0) + (OUV ? 1 : 0);  // Y sums
+  static constexpr int NY = YC + (OC ? 1 : 0);
+  static constexpr int NXL = (SYS ? 2 : 0) + (HP && OUV ? 1 : 0) + (HU && OC ? 1 : 0) + (HP && OC ? 1 : 0);
+  static constexpr int LU = 0, LV = 1, LGP = SYS ? 2 : 0, LGU = LGP + (HP && OUV ? 1 : 0), LKP = LGU + (HU && OC ? 1 : 0);
+  static_assert(NY <= NF, "the Y sums live in the staged fields' halo lines");
+};
+
 struct NsTileCtx {
   int gx0, gy0, n0, nlx, ncy;  // first line / column, first element row, lines, columns of the tile
   bool hasLx, hasRx;           // the tile's element column has a left neighbour / is not the ghost
 };
 
-// Y phase of wave W: rows W, W+4, ... of element b on line r (lane = (r, b)); sums -> yu, yv, yg, yk.
-template <int P, int F, int W>
-__device__ __forceinline__ void ns_y_rows(const NsArgs& a, const NsTileCtx& t, const double* su, const double* sv,
-                                          const double* sp, const double* scv, bool cv_is_v, const double* ws,
-                                          double* yu, double* yv, double* yg, double* yk) {
-  using C = NsBand<P>;
-  using G = GllConst<P>;
-  constexpr int n = C::n, BY = C::BY, PIT = C::PIT;
-  constexpr bool HU = (F & NS_U) != 0, HP = (F & NS_P) != 0, OUV = (F & NS_UV_OUT) != 0, OC = (F & NS_C_OUT) != 0;
-  constexpr bool SYS = HU && OUV;
-  if constexpr (W < P) {
-    const int l = threadIdx.x & 63;
-    if (l >= P * C::TYE) return;
-    const int r = l / C::TYE, b = l - r * C::TYE;
-    const int pos = t.n0 + b;
-    if (r >= t.nlx || pos > a.ney) return;
-    const bool ghost = pos == a.ney, hasL = pos > 0;
-    const double mx = wsum1(t.gx0 + r, P, a.ex_begin, a.ex_end, ws);
-    constexpr int q0 = W == 0 ? 0 : P;  // only row 0 reads the lower neighbour element
-    const int base = (P + r) * PIT + b * P;
-    double tu[2 * P + 1], tv[2 * P + 1], tp[2 * P + 1];
-#pragma unroll
-    for (int q = q0; q <= 2 * P; ++q) {
-      if constexpr (HU) {
-        tu[q] = su[base + q];
-        tv[q] = sv[base + q];
-      }
-      if constexpr (HP) tp[q] = sp[base + q];
-    }
-    const double fy = a.fKy * mx, hxm = a.hx * mx, sym = a.sy * mx;
-    ns_sfor<W, P, C::NW>([&](auto J) {
-      constexpr int j = decltype(J)::value;
-      if (ghost && j != 0) return;  // the ghost position holds its row 0 only
-      const int c = b * P + j;      // tile column of the node
-      double gyc = 0.0;
-      if constexpr (SYS) {
-        const double cvn = a.cv ? (cv_is_v ? tv[P + j] : scv[r * BY + c]) : 1.0;
-        gyc = a.fY * cvn * mx;
-      }
-      double Su = 0.0, Sv = 0.0, gp = 0.0, gv = 0.0, kp = 0.0;
-      auto term = [&](double K, double Gc, int q) {
-        if constexpr (SYS) {
-          const double co = fma(gyc, Gc, fy * K);
-          Su = fma(co, tu[q], Su);
-          Sv = fma(co, tv[q], Sv);
-        }
-        if constexpr (HU && OC) gv = fma(Gc, tv[q], gv);
-        if constexpr (HP && OUV) gp = fma(Gc, tp[q], gp);
-        if constexpr (HP && OC) kp = fma(K, tp[q], kp);
-      };
-      if constexpr (j == 0) {
-        if (hasL) ns_sfor<0, n, 1>([&](auto Q) {
-            constexpr int q = decltype(Q)::value;
-            term(G::K[P * n + q], G::G[P * n + q], q);
-          });
-        if (!ghost) ns_sfor<0, n, 1>([&](auto Q) {
-            constexpr int q = decltype(Q)::value;
-            term(G::K[q], G::G[q], P + q);
-          });
-      } else {
-        ns_sfor<0, n, 1>([&](auto Q) {
-          constexpr int q = decltype(Q)::value;
-          term(G::K[j * n + q], G::G[j * n + q], P + q);
-        });
-      }
-      const int o = r * BY + c;
-      if constexpr (SYS) yu[o] = Su;
-      if constexpr (OUV) yv[o] = SYS ? fma(hxm, gp, Sv) : hxm * gp;
-      if constexpr (HU && OC) yg[o] = hxm * gv;
-      if constexpr (HP && OC) yk[o] = sym * kp;
-    });
-  }
+__device__ __forceinline__ bool ns_dir(const NsArgs& a, int64_t q, int gx, int gy) {
+  return a.mask ? a.mask[q] != 0
+                : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
+                   ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1));
 }
 
-// X phase of wave W: rows (lines) W, W+4, ... of column c (lane = c): the x sums onto the Y sums, then the
-// node's pointwise terms, row replacements and stores (the arithmetic of ns_apply_tile's epilogue).
-template <int P, int F, int W>
-__device__ __forceinline__ void ns_x_rows(const NsArgs& a, const NsTileCtx& t, const double* su, const double* sv,
-                                          const double* sp, bool cu_is_u, const double* ws, const double* yu,
-                                          const double* yv, const double* yg, const double* yk) {
-  using C = NsBand<P>;
-  using G = GllConst<P>;
-  constexpr int n = C::n, BY = C::BY, PIT = C::PIT;
-  constexpr bool HU = (F & NS_U) != 0, HP = (F & NS_P) != 0, OUV = (F & NS_UV_OUT) != 0, OC = (F & NS_C_OUT) != 0;
-  constexpr bool SYS = HU && OUV;
-  if constexpr (W < P) {
-    const int c = threadIdx.x & 63;
-    if (c >= t.ncy) return;
-    const int gy = t.gy0 + c, NY = a.NY;
-    const double my = wsum1(gy, P, 0, a.ney, ws);
-    constexpr int q0 = W == 0 ? 0 : P;  // only row 0 reads the left neighbour element
-    double tu[2 * P + 1], tv[2 * P + 1], tp[2 * P + 1];
-#pragma unroll
-    for (int q = q0; q <= 2 * P; ++q) {
-      if constexpr (HU) {
-        tu[q] = su[q * PIT + P + c];
-        tv[q] = sv[q * PIT + P + c];
-      }
-      if constexpr (HP) tp[q] = sp[q * PIT + P + c];
+// One term of a row: the Sys coefficient of the row formed from the 1-D K and G entries (cK K + Re c G, as
+// the reference's CSR row holds it) and every sum that uses the operand values.
+template <int F>
+struct NsAcc {
+  double su = 0.0, sv = 0.0, gp = 0.0, gw = 0.0, kp = 0.0;  // Sys u, Sys v, G p, G (u | v), K p
+  // d: the divergence operand of the direction (u along x, v along y)
+  __device__ __forceinline__ void term(double K, double Gc, double f, double gc, double u, double v, double p,
+                                       double d) {
+    using M = NsForm<F>;
+    if constexpr (M::SYS) {
+      const double co = fma(gc, Gc, f * K);
+      su = fma(co, u, su);
+      sv = fma(co, v, sv);
     }
-    const bool want_uv = OUV && (a.ru || a.rv), want_c = OC && a.rc;
-    const double fx = a.fKx * my, hym = a.hy * my, sxm = a.sx * my;
-    ns_sfor<W, P, C::NW>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      if (i >= t.nlx) return;  // the ghost position holds its line 0 only
-      const int gx = t.gx0 + i;
-      const int64_t q = static_cast<int64_t>(gx - a.lb0) * NY + gy;
-      const int64_t qv = static_cast<int64_t>(gx - a.lb0) * a.pitch + gy;
-      const double mx = wsum1(gx, P, a.ex_begin, a.ex_end, ws);
-      const int o = i * BY + c;
-      double gxc = 0.0;
-      if constexpr (SYS) {
-        const double cun = a.cu ? (cu_is_u ? tu[P + i] : a.cu[q]) : 1.0;
-        gxc = a.fX * cun * my;
-      }
-      double Su = 0.0, Sv = 0.0, gp = 0.0, gu = 0.0, kp = 0.0;
-      if constexpr (SYS) {
-        Su = yu[o];
-        Sv = yv[o];
-      }
-      auto term = [&](double K, double Gc, int qq) {
-        if constexpr (SYS) {
-          const double co = fma(gxc, Gc, fx * K);
-          Su = fma(co, tu[qq], Su);
-          Sv = fma(co, tv[qq], Sv);
-        }
-        if constexpr (HU && OC) gu = fma(Gc, tu[qq], gu);
-        if constexpr (HP && OUV) gp = fma(Gc, tp[qq], gp);
-        if constexpr (HP && OC) kp = fma(K, tp[qq], kp);
-      };
-      if constexpr (i == 0) {
-        if (t.hasLx) ns_sfor<0, n, 1>([&](auto Q) {
-            constexpr int qq = decltype(Q)::value;
-            term(G::K[P * n + qq], G::G[P * n + qq], qq);
-          });
-        if (t.hasRx) ns_sfor<0, n, 1>([&](auto Q) {
-            constexpr int qq = decltype(Q)::value;
-            term(G::K[qq], G::G[qq], P + qq);
-          });
-      } else {
-        ns_sfor<0, n, 1>([&](auto Q) {
-          constexpr int qq = decltype(Q)::value;
-          term(G::K[i * n + qq], G::G[i * n + qq], P + qq);
-        });
-      }
-      const bool own = !(gx == a.lb1 && a.ex_end < a.nex);  // a strip's right interface line: its right owner's
-      const bool dir = a.mask ? a.mask[q] != 0
-                              : (((a.sides & SEM_SIDE_W) && gx == 0) || ((a.sides & SEM_SIDE_E) && gx == a.NX - 1) ||
-                                 ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == NY - 1));
-      const double u0 = HU ? tu[P + i] : 0.0, v0 = HU ? tv[P + i] : 0.0;
-      if constexpr (OUV) {
-        if (want_uv) {
-          if (dir) {
-            if (a.ru) a.ru[qv] = own ? u0 - (a.gu ? a.gu[q] : 0.0) : 0.0;
-            if (a.rv) a.rv[qv] = own ? v0 - (a.gv ? a.gv[q] : 0.0) : 0.0;
-          } else {
-            const double fm = a.fM * mx * my;
-            if (a.ru) {
-              double z = fma(fm, u0, Su);
-              if (a.juu && own) z = fma(a.juu[q], u0, z);
-              if (a.juv && own) z = fma(a.juv[q], v0, z);
-              a.ru[qv] = fma(hym, gp, z);
-            }
-            if (a.rv) {
-              double z = fma(fm, v0, SYS ? Sv : yv[o]);  // Sv started from yv (Sys v + G_y p, y rows)
-              if (a.jvu && own) z = fma(a.jvu[q], u0, z);
-              if (a.jvv && own) z = fma(a.jvv[q], v0, z);
-              if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
-              a.rv[qv] = z;
-            }
-          }
-        }
-      }
-      if constexpr (OC) {
-        if (want_c) {
-          const bool pinned = static_cast<int64_t>(gx) * NY + gy == a.pin;
-          const double pinrow = own ? (HP ? tp[P + i] : 0.0) - a.pin_val : 0.0;
-          double z;
-          if (pinned && !a.pin_first)
-            z = pinrow;
-          else if (dir)  // the (K p) row
-            z = HP ? fma(sxm, kp, yk[o]) : 0.0;
-          else if (pinned)
-            z = pinrow;
-          else
-            z = HU ? a.c_div * fma(hym, gu, yg[o]) : 0.0;
-          a.rc[q] = z;
-        }
-      }
-    });
+    if constexpr (M::HU && M::OC) gw = fma(Gc, d, gw);
+    if constexpr (M::HP && M::OUV) gp = fma(Gc, p, gp);
+    if constexpr (M::HP && M::OC) kp = fma(K, p, kp);
   }
-}
+};
 
-template <int P, int F>
+template <int P, int F, bool CVS>
 __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y, int ntiles, int per_xcd, int ubytes,
                                                     int pbytes) {
   using C = NsBand<P>;
-  constexpr int n = P + 1, BY = C::BY, SX = C::SX, SY = C::SY, PIT = C::PIT;
-  constexpr bool HU = (F & NS_U) != 0, HP = (F & NS_P) != 0, OUV = (F & NS_UV_OUT) != 0, OC = (F & NS_C_OUT) != 0;
-  constexpr bool SYS = HU && OUV;
+  using M = NsForm<F>;
+  using G = GllConst<P>;
+  constexpr int n = P + 1, BY = C::BY, SX = C::SX, SY = C::SY, PIT = C::PIT, FLD = C::FLD;
   __shared__ double ws[n];
-  __shared__ double su[HU ? SX * PIT : 1], sv[HU ? SX * PIT : 1], sp[HP ? SX * PIT : 1];
-  __shared__ double scv[SYS ? P * BY : 1];
-  __shared__ double yu[SYS ? P * BY : 1], yv[OUV ? P * BY : 1], yg[(HU && OC) ? P * BY : 1];
-  __shared__ double yk[(HP && OC) ? P * BY : 1];
+  __shared__ double stg[M::NF * FLD];
+  __shared__ double scv[CVS ? P * BY : 1];
+  __shared__ double xl[M::NXL > 0 ? M::NXL * 64 : 1];
+  double* const su = stg + M::IU * FLD;
+  double* const sv = stg + M::IV * FLD;
+  double* const sp = stg + M::IP * FLD;
   const int bid = blockIdx.x;
   const int tile = (bid & 7) * per_xcd + (bid >> 3);
   if (tile >= ntiles) return;
   const int tx = tile / tiles_y, ty = tile - tx * tiles_y;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   NsTileCtx t;
   t.gx0 = (a.ex_begin + tx) * P;
   t.n0 = ty * C::TYE;
@@ -494,36 +351,37 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
   t.hasRx = a.ex_begin + tx < a.ex_end;
   t.nlx = t.hasRx ? P : 1;
   t.ncy = min(BY, a.NY - t.gy0);
-  const bool cv_is_v = a.cv == a.v, cu_is_u = a.cu == a.u;
+  const int NY = a.NY;
+
   // ---- staging: every load issued before the first LDS write (buffer loads outside [0, bytes) read 0;
   // columns outside the mesh would wrap into neighbouring lines and are zeroed explicitly)
   const int64_t pitch = a.pitch;
-  const auto ru_ = brsrc(HU ? a.u : nullptr, HU && a.u ? ubytes : 0);
-  const auto rv_ = brsrc(HU ? a.v : nullptr, HU && a.v ? ubytes : 0);
-  const auto rp_ = brsrc(HP ? a.p : nullptr, HP && a.p ? pbytes : 0);
+  const auto ru_ = brsrc(M::HU ? a.u : nullptr, M::HU && a.u ? ubytes : 0);
+  const auto rv_ = brsrc(M::HU ? a.v : nullptr, M::HU && a.v ? ubytes : 0);
+  const auto rp_ = brsrc(M::HP ? a.p : nullptr, M::HP && a.p ? pbytes : 0);
   double st_u[C::NST], st_v[C::NST], st_p[C::NST];
 #pragma unroll
   for (int s = 0; s < C::NST; ++s) {
     const int k = min(tid + s * C::THREADS, SX * SY - 1);
     const int r = k / SY, cc = k - r * SY;
-    const int lx = t.gx0 - P + r - a.lb0;  // local line (out of range -> out-of-bounds offset)
-    const int gy = t.gy0 - P + cc;
-    const bool ok = lx >= 0 && t.gx0 - P + r <= a.lb1;
-    if constexpr (HU) {
-      st_u[s] = bload(ru_, ok ? static_cast<int>((lx * pitch + gy) * 8) : -1);
-      st_v[s] = bload(rv_, ok ? static_cast<int>((lx * pitch + gy) * 8) : -1);
+    const int gx = t.gx0 - P + r, gy = t.gy0 - P + cc;
+    const bool ok = gx >= a.lb0 && gx <= a.lb1;
+    const int64_t lx = gx - a.lb0;
+    if constexpr (M::HU) {
+      const int off = ok ? static_cast<int>((lx * pitch + gy) * 8) : -8;
+      st_u[s] = bload(ru_, off);
+      st_v[s] = bload(rv_, off);
     }
-    if constexpr (HP) st_p[s] = bload(rp_, ok ? (lx * a.NY + gy) * 8 : -1);
+    if constexpr (M::HP) st_p[s] = bload(rp_, ok ? static_cast<int>((lx * NY + gy) * 8) : -8);
   }
-  double st_c[SYS ? C::NCV : 1];
-  if constexpr (SYS) {
-    const bool stage_cv = a.cv && !cv_is_v;
+  double st_c[CVS ? C::NCV : 1];
+  if constexpr (CVS) {
 #pragma unroll
     for (int s = 0; s < C::NCV; ++s) {
       const int k = tid + s * C::THREADS;
       const int r = k / BY, cc = k - r * BY;
-      st_c[s] = (stage_cv && k < P * BY && r < t.nlx && cc < t.ncy)
-                    ? a.cv[static_cast<int64_t>(t.gx0 + r - a.lb0) * a.NY + t.gy0 + cc]
+      st_c[s] = (k < P * BY && r < t.nlx && cc < t.ncy)
+                    ? a.cv[static_cast<int64_t>(t.gx0 + r - a.lb0) * NY + t.gy0 + cc]
                     : 0.0;
     }
   }
@@ -534,15 +392,15 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
     if (k < SX * SY) {
       const int r = k / SY, cc = k - r * SY;
       const int gy = t.gy0 - P + cc;
-      const bool inside = gy >= 0 && gy < a.NY;
-      if constexpr (HU) {
+      const bool inside = gy >= 0 && gy < NY;
+      if constexpr (M::HU) {
         su[r * PIT + cc] = inside ? st_u[s] : 0.0;
         sv[r * PIT + cc] = inside ? st_v[s] : 0.0;
       }
-      if constexpr (HP) sp[r * PIT + cc] = inside ? st_p[s] : 0.0;
+      if constexpr (M::HP) sp[r * PIT + cc] = inside ? st_p[s] : 0.0;
     }
   }
-  if constexpr (SYS) {
+  if constexpr (CVS) {
 #pragma unroll
     for (int s = 0; s < C::NCV; ++s) {
       const int k = tid + s * C::THREADS;
@@ -550,19 +408,245 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
     }
   }
   __syncthreads();
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // ---- Y phase (+ the left-element x rows of line gx0 on wave XLW): sums in registers
+  double yres[(P + C::NW - 1) / C::NW][M::NY > 0 ? M::NY : 1];
+  double xlres[M::NXL > 0 ? M::NXL : 1];
+  auto y_phase = [&](auto WW) {
+    constexpr int W = decltype(WW)::value;
+    if constexpr (C::rows(W) > 0) {
+      if (lane >= P * C::TYE) return;
+      const int r = lane / C::TYE, b = lane - r * C::TYE;
+      const int pos = t.n0 + b;
+      if (r >= t.nlx || pos > a.ney) return;
+      const bool ghost = pos == a.ney, hasL = pos > 0;
+      const int gx = t.gx0 + r;
+      const double mx = wsum1(gx, P, a.ex_begin, a.ex_end, ws);
+      const int base = (P + r) * PIT + b * P;  // staged column b P + q <-> gy = gy0 + b P - P + q
+      double tu[n], tv[n], tp[n];              // the element's own nodes (q = P .. 2P)
+#pragma unroll
+      for (int k = 0; k < n; ++k) {
+        if constexpr (M::HU) {
+          tu[k] = su[base + P + k];
+          tv[k] = sv[base + P + k];
+        }
+        if constexpr (M::HP) tp[k] = sp[base + P + k];
+      }
+      const double fy = a.fKy * mx, hxm = a.hx * mx, sym = a.sy * mx;
+      ns_sfor<W, P, C::NW>([&](auto J) {
+        constexpr int j = decltype(J)::value, slot = (j - W) / C::NW;
+        if (ghost && j != 0) return;  // the ghost position holds its row 0 only
+        const int c = b * P + j;      // tile column of the node
+        double gyc = 0.0;
+        if constexpr (M::SYS) {
+          const double cvn = CVS ? scv[r * BY + c] : (a.cv ? tv[j] : 1.0);  // !CVS: cv is v itself or absent
+          gyc = a.fY * cvn * mx;
+        }
+        NsAcc<F> acc;
+        if constexpr (j == 0) {
+          if (hasL) ns_sfor<0, n, 1>([&](auto Q) {
+              constexpr int q = decltype(Q)::value;
+              const double uq = M::HU ? (q == P ? tu[0] : su[base + q]) : 0.0;
+              const double vq = M::HU ? (q == P ? tv[0] : sv[base + q]) : 0.0;
+              const double pq = M::HP ? (q == P ? tp[0] : sp[base + q]) : 0.0;
+              acc.term(G::K[P * n + q], G::G[P * n + q], fy, gyc, uq, vq, pq, vq);
+            });
+          if (!ghost) ns_sfor<0, n, 1>([&](auto Q) {
+              constexpr int q = decltype(Q)::value;
+              acc.term(G::K[q], G::G[q], fy, gyc, M::HU ? tu[q] : 0.0, M::HU ? tv[q] : 0.0, M::HP ? tp[q] : 0.0,
+                       M::HU ? tv[q] : 0.0);
+            });
+        } else {
+          ns_sfor<0, n, 1>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            acc.term(G::K[j * n + q], G::G[j * n + q], fy, gyc, M::HU ? tu[q] : 0.0, M::HU ? tv[q] : 0.0,
+                     M::HP ? tp[q] : 0.0, M::HU ? tv[q] : 0.0);
+          });
+        }
+        if constexpr (M::SYS) yres[slot][M::YU] = acc.su;
+        if constexpr (M::OUV) yres[slot][M::YV] = M::SYS ? fma(hxm, acc.gp, acc.sv) : hxm * acc.gp;
+        if constexpr (M::OC) {
+          const int gy = t.gy0 + c;
+          const bool dir = ns_dir(a, static_cast<int64_t>(gx - a.lb0) * NY + gy, gx, gy);
+          yres[slot][M::YC] = dir ? (M::HP ? sym * acc.kp : 0.0) : (M::HU ? hxm * acc.gw : 0.0);
+        }
+      });
+    }
+  };
   switch (w) {
-    case 0: ns_y_rows<P, F, 0>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
-    case 1: ns_y_rows<P, F, 1>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
-    case 2: ns_y_rows<P, F, 2>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
-    default: ns_y_rows<P, F, 3>(a, t, su, sv, sp, scv, cv_is_v, ws, yu, yv, yg, yk); break;
+    case 0: y_phase(std::integral_constant<int, 0>{}); break;
+    case 1: y_phase(std::integral_constant<int, 1>{}); break;
+    case 2: y_phase(std::integral_constant<int, 2>{}); break;
+    default: y_phase(std::integral_constant<int, 3>{}); break;
+  }
+  if (w == C::XLW && t.hasLx && lane < t.ncy) {
+    // left-element x rows of line gx0 (row P of element ex_begin + tx - 1) at column `lane`
+    const int c = lane, gy = t.gy0 + c;
+    const double my = wsum1(gy, P, 0, a.ney, ws);
+    const double fx = a.fKx * my;
+    double gxc = 0.0;
+    if constexpr (M::SYS) {
+      const bool cu_is_u = a.cu == a.u;
+      const double cun = a.cu ? (cu_is_u ? su[P * PIT + P + c] : a.cu[static_cast<int64_t>(t.gx0 - a.lb0) * NY + gy])
+                              : 1.0;
+      gxc = a.fX * cun * my;
+    }
+    NsAcc<F> acc;
+    ns_sfor<0, n, 1>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      const int o = q * PIT + P + c;
+      acc.term(G::K[P * n + q], G::G[P * n + q], fx, gxc, M::HU ? su[o] : 0.0, M::HU ? sv[o] : 0.0,
+               M::HP ? sp[o] : 0.0, M::HU ? su[o] : 0.0);
+    });
+    if constexpr (M::SYS) {
+      xlres[M::LU] = acc.su;
+      xlres[M::LV] = acc.sv;
+    }
+    if constexpr (M::HP && M::OUV) xlres[M::LGP] = acc.gp;
+    if constexpr (M::HU && M::OC) xlres[M::LGU] = acc.gw;
+    if constexpr (M::HP && M::OC) xlres[M::LKP] = acc.kp;
+  }
+  __syncthreads();  // the halo lines are dead from here: they take the Y sums
+
+  // ---- Y sums and left-element sums -> LDS (Y sum k over the halo lines of staged field k)
+  auto y_store = [&](auto WW) {
+    constexpr int W = decltype(WW)::value;
+    if constexpr (C::rows(W) > 0 && M::NY > 0) {
+      if (lane >= P * C::TYE) return;
+      const int r = lane / C::TYE, b = lane - r * C::TYE;
+      const int pos = t.n0 + b;
+      if (r >= t.nlx || pos > a.ney) return;
+      const bool ghost = pos == a.ney;
+      ns_sfor<W, P, C::NW>([&](auto J) {
+        constexpr int j = decltype(J)::value, slot = (j - W) / C::NW;
+        if (ghost && j != 0) return;
+#pragma unroll
+        for (int k = 0; k < M::NY; ++k) stg[k * FLD + r * BY + b * P + j] = yres[slot][k];
+      });
+    }
+  };
+  switch (w) {
+    case 0: y_store(std::integral_constant<int, 0>{}); break;
+    case 1: y_store(std::integral_constant<int, 1>{}); break;
+    case 2: y_store(std::integral_constant<int, 2>{}); break;
+    default: y_store(std::integral_constant<int, 3>{}); break;
+  }
+  if constexpr (M::NXL > 0) {
+    if (w == C::XLW && t.hasLx && lane < t.ncy) {
+#pragma unroll
+      for (int k = 0; k < M::NXL; ++k) xl[k * 64 + lane] = xlres[k];
+    }
   }
   __syncthreads();
+
+  // ---- X phase: lane = column c, rows (lines) w, w+4, ...
+  auto x_phase = [&](auto WW) {
+    constexpr int W = decltype(WW)::value;
+    if constexpr (C::rows(W) > 0) {
+      const int c = lane;
+      if (c >= t.ncy) return;
+      const int gy = t.gy0 + c;
+      const double my = wsum1(gy, P, 0, a.ney, ws);
+      double tu[n], tv[n], tp[n];  // lines gx0 .. gx0 + P of column c
+#pragma unroll
+      for (int k = 0; k < n; ++k) {
+        const int o = (P + k) * PIT + P + c;
+        if constexpr (M::HU) {
+          tu[k] = su[o];
+          tv[k] = sv[o];
+        }
+        if constexpr (M::HP) tp[k] = sp[o];
+      }
+      const bool want_uv = M::OUV && (a.ru || a.rv), want_c = M::OC && a.rc;
+      const bool cu_is_u = a.cu == a.u;
+      const double fx = a.fKx * my, hym = a.hy * my, sxm = a.sx * my;
+      ns_sfor<W, P, C::NW>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if (i >= t.nlx) return;  // the ghost position holds its line 0 only
+        const int gx = t.gx0 + i;
+        const int64_t q = static_cast<int64_t>(gx - a.lb0) * NY + gy;
+        const int64_t qv = static_cast<int64_t>(gx - a.lb0) * pitch + gy;
+        const double mx = wsum1(gx, P, a.ex_begin, a.ex_end, ws);
+        const int o = i * BY + c;
+        double gxc = 0.0;
+        if constexpr (M::SYS) {
+          const double cun = a.cu ? (cu_is_u ? tu[i] : a.cu[q]) : 1.0;
+          gxc = a.fX * cun * my;
+        }
+        NsAcc<F> acc;
+        if constexpr (i == 0) {
+          if (t.hasLx) {
+            if constexpr (M::SYS) {
+              acc.su = xl[M::LU * 64 + c];
+              acc.sv = xl[M::LV * 64 + c];
+            }
+            if constexpr (M::HP && M::OUV) acc.gp = xl[M::LGP * 64 + c];
+            if constexpr (M::HU && M::OC) acc.gw = xl[M::LGU * 64 + c];
+            if constexpr (M::HP && M::OC) acc.kp = xl[M::LKP * 64 + c];
+          }
+          if (t.hasRx) ns_sfor<0, n, 1>([&](auto Q) {
+              constexpr int qq = decltype(Q)::value;
+              acc.term(G::K[qq], G::G[qq], fx, gxc, M::HU ? tu[qq] : 0.0, M::HU ? tv[qq] : 0.0,
+                       M::HP ? tp[qq] : 0.0, M::HU ? tu[qq] : 0.0);
+            });
+        } else {
+          ns_sfor<0, n, 1>([&](auto Q) {
+            constexpr int qq = decltype(Q)::value;
+            acc.term(G::K[i * n + qq], G::G[i * n + qq], fx, gxc, M::HU ? tu[qq] : 0.0, M::HU ? tv[qq] : 0.0,
+                     M::HP ? tp[qq] : 0.0, M::HU ? tu[qq] : 0.0);
+          });
+        }
+        const bool own = !(gx == a.lb1 && a.ex_end < a.nex);  // a strip's right interface line: its right owner's
+        const bool dir = ns_dir(a, q, gx, gy);
+        const double u0 = M::HU ? tu[i] : 0.0, v0 = M::HU ? tv[i] : 0.0;
+        if constexpr (M::OUV) {
+          if (want_uv) {
+            if (dir) {
+              if (a.ru) a.ru[qv] = own ? u0 - (a.gu ? a.gu[q] : 0.0) : 0.0;
+              if (a.rv) a.rv[qv] = own ? v0 - (a.gv ? a.gv[q] : 0.0) : 0.0;
+            } else {
+              const double fm = a.fM * mx * my;
+              if (a.ru) {
+                double z = fma(fm, u0, M::SYS ? stg[M::YU * FLD + o] + acc.su : 0.0);
+                if (a.juu && own) z = fma(a.juu[q], u0, z);
+                if (a.juv && own) z = fma(a.juv[q], v0, z);
+                a.ru[qv] = fma(hym, acc.gp, z);
+              }
+              if (a.rv) {
+                double z = fma(fm, v0, stg[M::YV * FLD + o] + (M::SYS ? acc.sv : 0.0));
+                if (a.jvu && own) z = fma(a.jvu[q], u0, z);
+                if (a.jvv && own) z = fma(a.jvv[q], v0, z);
+                if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
+                a.rv[qv] = z;
+              }
+            }
+          }
+        }
+        if constexpr (M::OC) {
+          if (want_c) {
+            const bool pinned = static_cast<int64_t>(gx) * NY + gy == a.pin;
+            const double pinrow = own ? (M::HP ? tp[i] : 0.0) - a.pin_val : 0.0;
+            const double yc = stg[M::YC * FLD + o];
+            double z;
+            if (pinned && !a.pin_first)
+              z = pinrow;
+            else if (dir)  // the (K p) row
+              z = M::HP ? fma(sxm, acc.kp, yc) : 0.0;
+            else if (pinned)
+              z = pinrow;
+            else
+              z = M::HU ? a.c_div * fma(hym, acc.gw, yc) : 0.0;
+            a.rc[q] = z;
+          }
+        }
+      });
+    }
+  };
   switch (w) {
-    case 0: ns_x_rows<P, F, 0>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
-    case 1: ns_x_rows<P, F, 1>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
-    case 2: ns_x_rows<P, F, 2>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
-    default: ns_x_rows<P, F, 3>(a, t, su, sv, sp, cu_is_u, ws, yu, yv, yg, yk); break;
+    case 0: x_phase(std::integral_constant<int, 0>{}); break;
+    case 1: x_phase(std::integral_constant<int, 1>{}); break;
+    case 2: x_phase(std::integral_constant<int, 2>{}); break;
+    default: x_phase(std::integral_constant<int, 3>{}); break;
   }
 }
 
@@ -578,8 +662,14 @@ static bool launch_ns_band(const NsArgs& a, hipStream_t s) {
   const int tiles_y = (a.ney + C::TYE) / C::TYE;
   const int ntiles = tiles_x * tiles_y;
   const int per_xcd = (ntiles + 7) / 8;
-  hipLaunchKernelGGL((ns_apply_band<P, F>), dim3(static_cast<unsigned>(8 * per_xcd)), dim3(C::THREADS), 0, s, a,
-                     tiles_y, ntiles, per_xcd, static_cast<int>(ub), static_cast<int>(pb));
+  const dim3 grid(static_cast<unsigned>(8 * per_xcd)), block(C::THREADS);
+  // cv staged in LDS when the Sys rows use a cv that is not v itself (the Jacobian forms)
+  if (NsForm<F>::SYS && a.cv && a.cv != a.v)
+    hipLaunchKernelGGL((ns_apply_band<P, F, NsForm<F>::SYS>), grid, block, 0, s, a, tiles_y, ntiles, per_xcd,
+                       static_cast<int>(ub), static_cast<int>(pb));
+  else
+    hipLaunchKernelGGL((ns_apply_band<P, F, false>), grid, block, 0, s, a, tiles_y, ntiles, per_xcd,
+                       static_cast<int>(ub), static_cast<int>(pb));
   return true;
 }
 

@@ -37,6 +37,7 @@ constexpr int kEdgeRows = 64;                         // edge-kernel rows per wo
 
 struct CondArgs {
   const double *Xi, *Aei, *Yie, *Se;
+  const double *Ed, *El, *Eu;  // block-Thomas factors of the edge Schur complement (Se == nullptr)
   const int64_t *pi, *pe;
   double *T, *C, *Ye;
   const double* R;     // column e interior at R + e ld_r (offset o)
@@ -171,6 +172,95 @@ __global__ __launch_bounds__(kCondThreads) void cond_edge_kernel(const CondArgs 
   }
 }
 
+// K2, block-Thomas form (ABI 9): one wavefront per column, lane i = row i of the ne1 x ne1 edge blocks.
+//   forward  z_k = Ed_k (r_k - El_{k-1} z_{k-1}),   back  y_k = z_k - Eu_k y_{k+1}
+// Each step is two (forward) or one (back) lane-per-row GEMVs on the previous step's vector, broadcast from
+// LDS; the next step's blocks are loaded into registers while the current step computes, so the sweep runs
+// at the latency of its dependent FMA chains, not of memory.  Columns are independent (grid = nex).
+constexpr int kThomasB = 32;  // largest ne1 (= nc (P-1)) of the block-Thomas form
+
+__device__ __forceinline__ void load_block_col(const double* __restrict__ M, int b, int i, double (&r)[kThomasB]) {
+#pragma unroll
+  for (int j = 0; j < kThomasB; ++j) r[j] = (j < b && i < b) ? M[j * b + i] : 0.0;
+}
+
+__global__ __launch_bounds__(64) void cond_edge_thomas_kernel(const CondArgs a) {
+  __shared__ double vb[2][kThomasB];
+  const int e = blockIdx.x, b = a.ne1, nb = a.ney + 1, i = threadIdx.x;
+  const int64_t bb = static_cast<int64_t>(b) * b;
+  const double* C = a.C + static_cast<int64_t>(e) * a.ney * 2 * b;
+  const double* Ed = a.Ed + static_cast<int64_t>(e) * nb * bb;
+  const double* El = a.El + static_cast<int64_t>(e) * a.ney * bb;
+  const double* Eu = a.Eu + static_cast<int64_t>(e) * a.ney * bb;
+  double* Ye = a.Ye + static_cast<int64_t>(e) * a.n_e;
+  auto redge = [&](int k) {  // reduced edge right-hand side of row i of edge k
+    if (i >= b) return 0.0;
+    const int r = k * b + i;
+    double v = rhs(a, e, a.pe[r]);
+    if (k < a.ney) v -= C[static_cast<int64_t>(k) * 2 * b + i];
+    if (k > 0) v -= C[static_cast<int64_t>(k - 1) * 2 * b + b + i];
+    return v;
+  };
+  double ml[kThomasB], md[kThomasB], nl[kThomasB], nd[kThomasB];
+  load_block_col(Ed, b, i, md);
+  double rk = redge(0);
+  // forward sweep
+  for (int k = 0; k < nb; ++k) {
+    if (k + 1 < nb) {  // prefetch step k+1: El_k, Ed_{k+1}, its right-hand side
+      load_block_col(El + k * bb, b, i, nl);
+      load_block_col(Ed + (k + 1) * bb, b, i, nd);
+    }
+    const double rn = k + 1 < nb ? redge(k + 1) : 0.0;
+    double t = rk;
+    if (k > 0) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < kThomasB; ++j)
+        if (j < b) acc = fma(ml[j], vb[0][j], acc);
+      t -= acc;
+    }
+    __syncthreads();
+    if (i < b) vb[1][i] = t;
+    __syncthreads();
+    double z = 0.0;
+#pragma unroll
+    for (int j = 0; j < kThomasB; ++j)
+      if (j < b) z = fma(md[j], vb[1][j], z);
+    if (i < b) {
+      vb[0][i] = z;
+      Ye[static_cast<int64_t>(k) * b + i] = z;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kThomasB; ++j) {
+      ml[j] = nl[j];
+      md[j] = nd[j];
+    }
+    rk = rn;
+  }
+  // back sweep: vb[0] holds y_{nb-1} = z_{nb-1}
+  if (i < b) a.Y[e * a.ld_y + a.pe[static_cast<int64_t>(nb - 1) * b + i]] = vb[0][i];
+  if (nb > 1) load_block_col(Eu + (nb - 2) * bb, b, i, md);
+  for (int k = nb - 2; k >= 0; --k) {
+    if (k > 0) load_block_col(Eu + (k - 1) * bb, b, i, nd);
+    const double zk = i < b ? Ye[static_cast<int64_t>(k) * b + i] : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kThomasB; ++j)
+      if (j < b) acc = fma(md[j], vb[0][j], acc);
+    const double y = zk - acc;
+    __syncthreads();
+    if (i < b) {
+      vb[0][i] = y;
+      Ye[static_cast<int64_t>(k) * b + i] = y;
+      a.Y[e * a.ld_y + a.pe[static_cast<int64_t>(k) * b + i]] = y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kThomasB; ++j) md[j] = nd[j];
+  }
+}
+
 // K3: y_i = T - Yie [y_e[n]; y_e[n+1]] for element (e, n), written to the element's interior nodes.
 __global__ __launch_bounds__(kCondThreads) void cond_back_kernel(const CondArgs a) {
   extern __shared__ double lds[];
@@ -232,7 +322,9 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
   if (!d || !R || !Y) return sem::set_error(SEM_EINVAL, "nested_solve: null argument");
   if (d->P < 2 || d->nex < 1 || d->ney < 1 || (d->nc != 1 && d->nc != 2) || d->NY != d->ney * d->P + 1)
     return sem::set_error(SEM_EINVAL, "nested_solve: bad sizes");
-  if (!d->Xi || !d->Aei || !d->Yie || !d->Se || !d->pi || !d->pe || !d->T || !d->C || !d->Ye)
+  const bool thomas = d->Se == nullptr;
+  if (!d->Xi || !d->Aei || !d->Yie || !d->pi || !d->pe || !d->T || !d->C || !d->Ye ||
+      (thomas && (!d->Ed || (d->ney > 0 && (!d->El || !d->Eu)))))
     return sem::set_error(SEM_EINVAL, "nested_solve: null factor or work array");
   if ((aIB == nullptr) != (xB == nullptr)) return sem::set_error(SEM_EINVAL, "nested_solve: aIB and xB go together");
   sem::CondArgs a{};
@@ -240,6 +332,9 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
   a.Aei = d->Aei;
   a.Yie = d->Yie;
   a.Se = d->Se;
+  a.Ed = d->Ed;
+  a.El = d->El;
+  a.Eu = d->Eu;
   a.pi = d->pi;
   a.pe = d->pe;
   a.T = d->T;
@@ -258,7 +353,9 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
   a.ne1 = d->nc * (d->P - 1);
   a.ni = a.ne1 * (d->P - 1);
   a.n_e = (d->ney + 1) * a.ne1;
-  if (static_cast<size_t>(a.n_e + sem::part_size()) * sizeof(double) > 64 * 1024)
+  if (thomas && a.ne1 > sem::kThomasB)
+    return sem::set_error(SEM_EUNSUPPORTED, "nested_solve: edge blocks wider than the block-Thomas form's 32");
+  if (!thomas && static_cast<size_t>(a.n_e + sem::part_size()) * sizeof(double) > 64 * 1024)
     return sem::set_error(SEM_EUNSUPPORTED, "nested_solve: too many edge unknowns per column");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const dim3 blk(sem::kCondThreads);
@@ -266,8 +363,11 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
   const size_t part = sem::part_size() * sizeof(double);
   hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(elems), blk, part + 2 * a.ni * sizeof(double), s, a);
   if (int st = sem::launch_check("nested_solve fwd")) return st;
-  hipLaunchKernelGGL(sem::cond_edge_kernel, dim3((a.n_e + sem::kEdgeRows - 1) / sem::kEdgeRows, d->nex), blk,
-                     part + a.n_e * sizeof(double), s, a);
+  if (thomas)
+    hipLaunchKernelGGL(sem::cond_edge_thomas_kernel, dim3(d->nex), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(sem::cond_edge_kernel, dim3((a.n_e + sem::kEdgeRows - 1) / sem::kEdgeRows, d->nex), blk,
+                       part + a.n_e * sizeof(double), s, a);
   if (int st = sem::launch_check("nested_solve edge")) return st;
   hipLaunchKernelGGL(sem::cond_back_kernel, dim3(elems), blk, part + 2 * a.ne1 * sizeof(double), s, a);
   return sem::launch_check("nested_solve back");

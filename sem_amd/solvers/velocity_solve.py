@@ -202,6 +202,11 @@ class VelocityJacobianSolver:
         self.timing = {}
         # edge Schur systems up to this size are inverted densely (pivoted); larger ones by block LU
         self.edge_dense_max = 1024
+        # edge solve of the block-LU path on the GPU: "auto" keeps the block-Thomas factors (sem_nested_solve's
+        # ABI-9 form: O(N_ey ne1^2) doubles per column read per solve instead of the n_e^2 of the dense
+        # inverse -- 1.5 MB instead of 64 MB per cfg5 column); "dense" keeps the dense inverse
+        self.edge_solve = "auto"
+        self._edge_thomas = False
 
     @contextlib.contextmanager
     def _phase(self, name):
@@ -297,14 +302,24 @@ class VelocityJacobianSolver:
         nex, ney, ne1 = self.nex, self.ney, self._ne1
         ni, n_e = self._pi.shape[1], self._pe.numel()
         z = dict(dtype=torch.float64, device=self.device)
+        self._edge_thomas = n_e > self.edge_dense_max and ne1 <= 32 and (
+            self.edge_solve == "thomas" or (self.edge_solve == "auto" and self.device.type == "cuda"))
         shapes = ((nex, ney, ni, ni), (nex, ney, 2 * ne1, ni), (nex, ney, ni, 2 * ne1), (nex, n_e, n_e))
+        if self._edge_thomas:   # block-Thomas factors of the edge Schur complement instead of its inverse
+            shapes = shapes[:3]
+            Et = [torch.empty(sh, **z) for sh in ((nex, ney + 1, ne1, ne1), (nex, ney, ne1, ne1), (nex, ney, ne1, ne1))]
+            self._EtT = tuple(Et)                                   # column-major blocks
+            self._Ed, self._El, self._Eu = (t.transpose(-1, -2) for t in Et)
         if self.device.type == "cuda":
             T = [torch.empty(s[:-2] + (s[-1], s[-2]), **z) for s in shapes]
+            if self._edge_thomas:
+                T.append(None)
             self._hipT = tuple(T)
-            self._Xi, self._Aei, self._Yie, self._Se_inv = (t.transpose(-1, -2) for t in T)
+            self._Xi, self._Aei, self._Yie, self._Se_inv = (None if t is None else t.transpose(-1, -2) for t in T)
         else:
             self._hipT = None
-            self._Xi, self._Aei, self._Yie, self._Se_inv = (torch.empty(s, **z) for s in shapes)
+            self._Xi, self._Aei, self._Yie, self._Se_inv = [torch.empty(s, **z) for s in shapes] + (
+                [None] if self._edge_thomas else [])
 
     def factor_condensed(self, fill, budget_bytes=24 << 30, pieces=None, line=None, chunk_cols=None):
         """Factor from condensed pieces: fill(blocks, cols) writes the pieces of element columns cols and the
@@ -392,8 +407,14 @@ class VelocityJacobianSolver:
             Sl = blk["Ael"].view(cc, ney, ne1, ne1) - Cee[:, :, ne1:, :ne1]
             del Cee
         with self._phase("inv_edge"):
-            Se_inv = self._blocktri_inverse(Sd, Su, Sl)
-        self._Xi[c0:c1], self._Yie[c0:c1], self._Aei[c0:c1], self._Se_inv[c0:c1] = Xi, Yie, Aei, Se_inv
+            Se_inv, fac = self._blocktri_inverse(Sd, Su, Sl, factors=True)
+        self._Xi[c0:c1], self._Yie[c0:c1], self._Aei[c0:c1] = Xi, Yie, Aei
+        if self._edge_thomas and fac is None:   # a column needed the pivoted dense inverse: dense edge solve
+            self._edge_to_dense(c0)
+        if self._edge_thomas:
+            self._Ed[c0:c1], self._El[c0:c1], self._Eu[c0:c1] = fac[0], Sl, fac[1]
+        else:
+            self._Se_inv[c0:c1] = Se_inv
         with self._phase("coupling_pieces"):
             eye_c = torch.eye(nc, dtype=f64, device=dev)
             eye_j = torch.eye(P - 1, dtype=f64, device=dev)
@@ -436,18 +457,21 @@ class VelocityJacobianSolver:
             inv = self._group_perm()
             return Cg[:, inv][:, :, inv]
 
-    def _blocktri_inverse(self, Sd, Su, Sl):
+    def _blocktri_inverse(self, Sd, Su, Sl, factors=False):
         """Dense inverse of block-tridiagonal matrices (batched over columns): diagonal blocks Sd (cc, nb, b, b),
         upper Su[k] (row block k, column block k+1), lower Sl[k] (row k+1, column k).  Block LU with pivoted
         inverses of the pivot blocks, then the block-Thomas solve against the identity; the result is
         checked through its residual S X - I (block-tridiagonal times dense: cheap) and a column whose
-        elimination without inter-block pivoting lost accuracy is inverted densely instead."""
+        elimination without inter-block pivoting lost accuracy is inverted densely instead.
+        factors=True: returns (X, (Dinv, Uh)) -- the block-Thomas factors (inverse pivot blocks and
+        Dinv_k Su_k) the checked inverse was built from, or None when they are absent (a dense inverse)
+        or when a column failed the check."""
         cc, nb, b = Sd.shape[0], Sd.shape[1], Sd.shape[2]
         n = nb * b
-        dev, f64 = Sd.device, Sd.dtype
         if n <= self.edge_dense_max:   # small edge systems: one pivoted dense inverse per column
             S = self._blocktri_dense(Sd, Su, Sl)
-            return batched_inverse(S)
+            X = batched_inverse(S)
+            return (X, None) if factors else X
         # pivot-block inverses without raising: a singular or ill-conditioned pivot shows in the final check
         inv = lambda A: torch.linalg.inv_ex(A)[0]  # noqa: E731
         Dinv = torch.empty_like(Sd)
@@ -456,6 +480,22 @@ class VelocityJacobianSolver:
         for k in range(1, nb):
             Uh[:, k - 1] = Dinv[:, k - 1] @ Su[:, k - 1]
             Dinv[:, k] = inv(Sd[:, k] - Sl[:, k - 1] @ Uh[:, k - 1])
+        X = self._blocktri_apply_identity(Dinv, Uh, Sl)
+        res = self._blocktri_residual(Sd, Su, Sl, X)
+        bad = torch.nonzero(~(res <= 8.0 * n * n * torch.finfo(Sd.dtype).eps)).flatten().tolist()
+        if bad:
+            S = self._blocktri_dense(Sd[bad], Su[bad], Sl[bad])
+            X[bad] = batched_inverse(S)
+        if factors:
+            return X, (None if bad else (Dinv, Uh))
+        return X
+
+    @staticmethod
+    def _blocktri_apply_identity(Dinv, Uh, Sl):
+        """S^-1 from the block-Thomas factors of S (batched over columns)."""
+        cc, nb, b = Dinv.shape[0], Dinv.shape[1], Dinv.shape[2]
+        n = nb * b
+        dev, f64 = Dinv.device, Dinv.dtype
         X = torch.zeros((cc, nb, b, n), dtype=f64, device=dev)
         # forward: Z_k = Dinv_k (I_k - Sl_{k-1} Z_{k-1}); Z_k is zero beyond column block k
         X[:, 0, :, :b] = Dinv[:, 0]
@@ -467,13 +507,21 @@ class VelocityJacobianSolver:
         # back: X_k = Z_k - Uh_k X_{k+1}
         for k in range(nb - 2, -1, -1):
             X[:, k] -= Uh[:, k] @ X[:, k + 1]
-        X = X.view(cc, n, n)
-        res = self._blocktri_residual(Sd, Su, Sl, X)
-        bad = torch.nonzero(~(res <= 8.0 * n * n * torch.finfo(f64).eps)).flatten().tolist()
-        if bad:
-            S = self._blocktri_dense(Sd[bad], Su[bad], Sl[bad])
-            X[bad] = batched_inverse(S)
-        return X
+        return X.view(cc, n, n)
+
+    def _edge_to_dense(self, c0):
+        """Leave the block-Thomas edge form (a column of chunk c0.. failed its check): dense inverses for the
+        columns factored so far, rebuilt from their checked factors, and the dense form from here on."""
+        nex, n_e = self.nex, self._pe.numel()
+        SeT = torch.empty((nex, n_e, n_e), dtype=torch.float64, device=self.device)
+        self._Se_inv = SeT.transpose(-1, -2)
+        for a in range(0, c0, 8):
+            b = min(c0, a + 8)
+            self._Se_inv[a:b] = self._blocktri_apply_identity(self._Ed[a:b], self._Eu[a:b], self._El[a:b])
+        if self._hipT is not None:
+            self._hipT = self._hipT[:3] + (SeT,)
+        self._edge_thomas = False
+        self._Ed = self._El = self._Eu = self._EtT = None
 
     @staticmethod
     def _blocktri_dense(Sd, Su, Sl):
@@ -699,7 +747,7 @@ class VelocityJacobianSolver:
     def _nested_finish(self):
         if self.device.type == "cuda":   # column-major blocks for sem_nested_solve (ns_condense.hip)
             if getattr(self, "_hipT", None) is None:
-                self._hipT = tuple(t.transpose(-1, -2).contiguous() for t in
+                self._hipT = tuple(None if t is None else t.transpose(-1, -2).contiguous() for t in
                                    (self._Xi, self._Aei, self._Yie, self._Se_inv))
             self._pi, self._pe = self._pi.contiguous(), self._pe.contiguous()
 
@@ -714,13 +762,26 @@ class VelocityJacobianSolver:
         Rv = Re.view(nex, ney + 1, ne1, k)
         Rv[:, :-1] -= Cn[:, :, :ne1]
         Rv[:, 1:] -= Cn[:, :, ne1:]
-        Ye = self._Se_inv[cols] @ Re                                    # (nex, n_e, k)
+        Ye = self._edge_thomas_solve(Re, cols) if self._edge_thomas else self._Se_inv[cols] @ Re  # (nex, n_e, k)
         Yv = Ye.view(nex, ney + 1, ne1, k)
         Yi = Ti - self._Yie[cols] @ torch.cat((Yv[:, :-1], Yv[:, 1:]), dim=2)
         Y = torch.empty_like(R)
         Y[:, self._pi] = Yi
         Y[:, self._pe] = Ye
         return Y
+
+    def _edge_thomas_solve(self, Re, cols=slice(None)):
+        """S_e^-1 Re from the block-Thomas factors (the torch form of cond_edge_thomas_kernel)."""
+        Ed, El, Eu = self._Ed[cols], self._El[cols], self._Eu[cols]
+        nex, nb, b = Ed.shape[0], Ed.shape[1], Ed.shape[2]
+        R = Re.view(nex, nb, b, -1)
+        Z = torch.empty_like(R)
+        Z[:, 0] = Ed[:, 0] @ R[:, 0]
+        for k in range(1, nb):
+            Z[:, k] = Ed[:, k] @ (R[:, k] - El[:, k - 1] @ Z[:, k - 1])
+        for k in range(nb - 2, -1, -1):
+            Z[:, k] -= Eu[:, k] @ Z[:, k + 1]
+        return Z.view(Re.shape)
 
     # ------------------------------------------------------------------ solve
     def _hip_nested(self):
@@ -736,8 +797,10 @@ class VelocityJacobianSolver:
             T, Cw, Ye, _, _ = self._work
             p = lambda t: t.data_ptr()  # noqa: E731
             XiT, AeiT, YieT, SeT = self._hipT
-            self._nd = _lib.SemNestedDesc(P, nex, ney, self.ncomp, self.NY, p(XiT), p(AeiT), p(YieT), p(SeT),
-                                          p(self._pi), p(self._pe), p(T), p(Cw), p(Ye))
+            Et = self._EtT if self._edge_thomas else (None, None, None)   # ABI 9: Se = NULL -> block Thomas
+            q = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+            self._nd = _lib.SemNestedDesc(P, nex, ney, self.ncomp, self.NY, p(XiT), p(AeiT), p(YieT), q(SeT),
+                                          p(self._pi), p(self._pe), p(T), p(Cw), p(Ye), *(q(t) for t in Et))
         return self._nd
 
     def _own_rhs(self, g, B):

@@ -201,13 +201,23 @@ def test_condensed_blocks_and_chunked_factor(gpu, P, nex, ney, Re):
     r = np.random.default_rng(3)
     bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
     sol = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
-    for edge_dense_max in (1024, 0):
+    sols = {}
+    for edge_dense_max, edge_solve in ((1024, "auto"), (0, "dense"), (0, "auto")):
+        # dense pivoted edge inverses; block LU -> dense inverse; block LU -> block-Thomas sweeps (ABI 9 kernel)
         ch = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
-        ch.edge_dense_max = edge_dense_max
+        ch.edge_dense_max, ch.edge_solve = edge_dense_max, edge_solve
         ch.factor_mesh(ns._mesh, budget_bytes=1, **kw)
-        xu, xv = ch.solve(ns._dev(bu), ns._dev(bv))
-        got = np.hstack((xu.cpu().numpy(), xv.cpu().numpy()))
-        assert np.abs(got - sol).max() <= 1e-9 * np.abs(sol).max()
+        assert ch._edge_thomas == (edge_dense_max == 0 and edge_solve == "auto")
+        for graph in (False, True):
+            if graph:
+                assert ch.capture()
+            xu, xv = ch.solve(ns._dev(bu), ns._dev(bv))
+            got = np.hstack((xu.cpu().numpy(), xv.cpu().numpy()))
+            assert np.abs(got - sol).max() <= 1e-9 * np.abs(sol).max()
+            sols[(edge_dense_max, edge_solve, graph)] = got
+    # the block-Thomas sweeps apply the same factors the dense inverse was built from
+    a, b = sols[(0, "dense", False)], sols[(0, "auto", False)]
+    assert np.abs(a - b).max() <= 1e-10 * np.abs(a).max()   # Re = 1000: the solves agree to the conditioning
 
 
 def test_interface_sweep_batched_gemv_fallback(gpu, monkeypatch):

@@ -62,11 +62,12 @@ def test_scalar_condensation_solves_the_cd_jacobian(P, nex, ney, Pe, sweep):
 
 @pytest.mark.parametrize("P,nex,ney,Re", [(4, 5, 2, 100.0), (3, 6, 2, 50.0), (6, 3, 2, 1000.0), (5, 4, 7, 400.0)])
 @pytest.mark.parametrize("chunk_cols", [1, 2])
-@pytest.mark.parametrize("edge", ["dense", "blocklu"])
+@pytest.mark.parametrize("edge", ["dense", "blocklu", "thomas"])
 def test_condensed_chunked_factor_matches_sparse_lu(P, nex, ney, Re, chunk_cols, edge):
     """factor_condensed (the ABI-7 path: the condensed pieces of chunk_cols element columns at a time,
     sem_condensed_blocks' col_begin/col_end contract) solves the Jacobian; the edge Schur blocks inverted
-    densely or by the checked block LU of their block-tridiagonal form."""
+    densely or by the checked block LU of their block-tridiagonal form, or (ABI 9) kept as the block-Thomas
+    factors that block LU produced and solved by forward / back sweeps."""
     ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
     pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
     ch = VelocityJacobianSolver(P, nex, ney, "cpu")
@@ -79,9 +80,11 @@ def test_condensed_chunked_factor_matches_sparse_lu(P, nex, ney, Re, chunk_cols,
         for k, v in cond.items():
             blocks[k].copy_(v[c0:c1])
 
-    if edge == "blocklu":
+    if edge in ("blocklu", "thomas"):
         ch.edge_dense_max = 0
+    ch.edge_solve = "thomas" if edge == "thomas" else "dense"
     ch.factor_condensed(fill, chunk_cols=chunk_cols)
+    assert ch._edge_thomas == (edge == "thomas")
     r = np.random.default_rng(9)
     bu, bv = (torch.as_tensor(r.uniform(-1, 1, ns.N)) for _ in range(2))
     want = spla.spsolve(ns.Jvelo.tocsc(), np.hstack((bu.numpy(), bv.numpy())))
@@ -109,3 +112,39 @@ def test_block_tridiagonal_inverse(nb, b, seed):
     S = VelocityJacobianSolver._blocktri_dense(Sd, Su, Sl)
     want = torch.linalg.inv(S)
     assert torch.allclose(X, want, rtol=0, atol=1e-10 * want.abs().max().item())
+
+
+def test_edge_thomas_falls_back_to_dense_inverses():
+    """A column whose block LU fails the residual check (zero leading pivot block) switches the block-Thomas
+    edge form to dense inverses: the columns factored before it get their inverses rebuilt from their
+    factors, and the solve still reproduces SciPy's."""
+    P, nex, ney, Re = 4, 4, 3, 100.0
+    ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=5)
+    pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
+    ch = VelocityJacobianSolver(P, nex, ney, "cpu")
+    ch.edge_dense_max, ch.edge_solve = 0, "thomas"
+    cond = ch.condense_dense(pcs["AII"])
+    orig = VelocityJacobianSolver._blocktri_inverse
+
+    def failing(self, Sd, Su, Sl, factors=False):   # pretend column 2's block LU failed its check
+        X, fac = orig(self, Sd, Su, Sl, factors=True)
+        return (X, None if self._c0 <= 2 < self._c0 + Sd.shape[0] else fac) if factors else X
+
+    def fill(blocks, cols):
+        ch._c0 = cols[0]
+        for k in ("D", "aIB", "aBI", "E", "F"):
+            blocks[k].copy_(pcs[k])
+        for k, v in cond.items():
+            blocks[k].copy_(v[cols[0]:cols[1]])
+
+    VelocityJacobianSolver._blocktri_inverse = failing
+    try:
+        ch.factor_condensed(fill, chunk_cols=1)
+    finally:
+        VelocityJacobianSolver._blocktri_inverse = orig
+    assert not ch._edge_thomas and ch._Se_inv is not None
+    r = np.random.default_rng(2)
+    bu, bv = (torch.as_tensor(r.uniform(-1, 1, ns.N)) for _ in range(2))
+    want = spla.spsolve(ns.Jvelo.tocsc(), np.hstack((bu.numpy(), bv.numpy())))
+    got = np.hstack([t.numpy() for t in ch.solve(bu, bv)])
+    assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()

@@ -18,4 +18,5 @@ for PMC in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL 120 rocprofv3 --pmc $PMC -d "$OUT/pmc$i" -o pmc --output-format csv -- "$@" > "$OUT/pmc$i.log" 2>&1 \
     || { echo "pmc pass $i failed: $OUT"; tail -3 "$OUT/pmc$i.log"; exit 1; }
 done
+python tools/pmc_compact.py "$OUT" && python tools/prof_summary.py "$OUT" > "$OUT/prof_summary.txt" 2>&1
 echo "pmc ok: $OUT"

@@ -23,8 +23,9 @@ def per_dispatch(d, counter, kfilter):
     for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter and kfilter in r["Kernel_Name"]:
-                acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+                # a tools/pmc_compact.py row is already a mean over `Dispatches` dispatches
+                acc[r["Kernel_Name"]].append((float(r["Counter_Value"]), int(r.get("Dispatches") or 1)))
+    return {k: (sum(x * n for x, n in v) / sum(n for _, n in v), sum(n for _, n in v)) for k, v in acc.items()}
 
 
 def short(name):

@@ -35,12 +35,14 @@ def main():
         for r in csv.DictReader(open(f)):
             if kfilter not in r["Kernel_Name"] and "dss_kernel" not in r["Kernel_Name"]:
                 continue
-            agg[(r["Kernel_Name"][:60], r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            n = int(r.get("Dispatches") or 1)   # tools/pmc_compact.py rows: a mean over n dispatches
+            agg[(r["Kernel_Name"][:60], r["Grid_Size"])][r["Counter_Name"]].append((float(r["Counter_Value"]), n))
     print("counters (per-dispatch means):")
     for (name, grid), cs in sorted(agg.items()):
         print(f"  {name}  grid={grid}")
         for c, v in sorted(cs.items()):
-            print(f"     {c:28s} {sum(v) / len(v):18.1f}   (n={len(v)})")
+            n = sum(k for _, k in v)
+            print(f"     {c:28s} {sum(x * k for x, k in v) / n:18.1f}   (n={n})")
 
 
 if __name__ == "__main__":
