@@ -324,7 +324,7 @@ struct NsAcc {
 };
 
 template <int P, int F, bool CVS>
-__global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y, int ntiles, int per_xcd, int ubytes,
+__global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tiles_y, int ntiles, int per_xcd, int ubytes,
                                                     int pbytes) {
   using C = NsBand<P>;
   using M = NsForm<F>;
@@ -560,8 +560,27 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
       const bool want_uv = M::OUV && (a.ru || a.rv), want_c = M::OC && a.rc;
       const bool cu_is_u = a.cu == a.u;
       const double fx = a.fKx * my, hym = a.hy * my, sxm = a.sx * my;
+      // the rows' pointwise operands, all loads issued before the first row's sums (buffer loads: an absent
+      // operand reads 0 without a branch)
+      constexpr int RW = C::rows(W);
+      double pcu[RW], pT[RW], pjuu[RW], pjuv[RW], pjvu[RW], pjvv[RW];
+      {
+        const auto rcu = brsrc(a.cu, M::SYS && a.cu && !cu_is_u ? pbytes : 0), rT = brsrc(a.T, M::OUV && a.T ? pbytes : 0);
+        const auto r1 = brsrc(a.juu, M::OUV && a.juu ? pbytes : 0), r2 = brsrc(a.juv, M::OUV && a.juv ? pbytes : 0);
+        const auto r3 = brsrc(a.jvu, M::OUV && a.jvu ? pbytes : 0), r4 = brsrc(a.jvv, M::OUV && a.jvv ? pbytes : 0);
+        ns_sfor<W, P, C::NW>([&](auto I) {
+          constexpr int i = decltype(I)::value, slot = (i - W) / C::NW;
+          const int off = i < t.nlx ? ((t.gx0 + i - a.lb0) * NY + gy) * 8 : -8;
+          pcu[slot] = bload(rcu, off);
+          pT[slot] = bload(rT, off);
+          pjuu[slot] = bload(r1, off);
+          pjuv[slot] = bload(r2, off);
+          pjvu[slot] = bload(r3, off);
+          pjvv[slot] = bload(r4, off);
+        });
+      }
       ns_sfor<W, P, C::NW>([&](auto I) {
-        constexpr int i = decltype(I)::value;
+        constexpr int i = decltype(I)::value, slot = (i - W) / C::NW;
         if (i >= t.nlx) return;  // the ghost position holds its line 0 only
         const int gx = t.gx0 + i;
         const int64_t q = static_cast<int64_t>(gx - a.lb0) * NY + gy;
@@ -570,7 +589,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
         const int o = i * BY + c;
         double gxc = 0.0;
         if constexpr (M::SYS) {
-          const double cun = a.cu ? (cu_is_u ? tu[i] : a.cu[q]) : 1.0;
+          const double cun = a.cu ? (cu_is_u ? tu[i] : pcu[slot]) : 1.0;
           gxc = a.fX * cun * my;
         }
         NsAcc<F> acc;
@@ -608,15 +627,15 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
               const double fm = a.fM * mx * my;
               if (a.ru) {
                 double z = fma(fm, u0, M::SYS ? stg[M::YU * FLD + o] + acc.su : 0.0);
-                if (a.juu && own) z = fma(a.juu[q], u0, z);
-                if (a.juv && own) z = fma(a.juv[q], v0, z);
+                if (a.juu && own) z = fma(pjuu[slot], u0, z);
+                if (a.juv && own) z = fma(pjuv[slot], v0, z);
                 a.ru[qv] = fma(hym, acc.gp, z);
               }
               if (a.rv) {
                 double z = fma(fm, v0, stg[M::YV * FLD + o] + (M::SYS ? acc.sv : 0.0));
-                if (a.jvu && own) z = fma(a.jvu[q], u0, z);
-                if (a.jvv && own) z = fma(a.jvv[q], v0, z);
-                if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
+                if (a.jvu && own) z = fma(pjvu[slot], u0, z);
+                if (a.jvv && own) z = fma(pjvv[slot], v0, z);
+                if (a.T) z = fma(a.fT * mx * my, pT[slot], z);
                 a.rv[qv] = z;
               }
             }

@@ -610,6 +610,21 @@ class VelocityJacobianSolver:
             if L < nex:
                 Uh[L] = Dinv[L] @ S_up[L]
         self.Dinv, self.Uh, self.S_lo = Dinv, Uh, S_lo
+        self._th = None
+        if (self.device.type == "cuda" and 2 * m <= GEMV_LDS_DOUBLES
+                and os.environ.get("SEM_THOMAS_HIP", "1") != "0"):
+            # sem_block_gemv form of the sweep: z_0 = D_0^-1 g_0, z_L = [D_L^-1 | -D_L^-1 S_lo[L-1]] [g_L; z_{L-1}],
+            # then z_L += (-Uh_L) z_{L+1}: one launch per line and direction, each operator read once
+            F = torch.empty((nex, m, 2 * m), dtype=torch.float64, device=self.device)
+            F[:, :, :m] = Dinv[1:]
+            for L in range(nex):
+                F[L, :, m:] = -(Dinv[L + 1] @ S_lo[L])
+            D0 = Dinv[:1].clone()
+            Uh.neg_()
+            Lr = torch.arange(nex + 1, dtype=torch.int64, device=self.device)
+            fx = torch.stack((Lr[1:], Lr[:-1]), dim=1)[:, :, None].contiguous()     # (nex, 2, 1): [L; L-1]
+            self._th = (D0, F, Uh, Lr[:, None].contiguous(), fx, Lr[1:, None, None].contiguous())
+            self.Dinv = self.Uh = self.S_lo = None
         self.factored = True
 
     # ------------------------------------------------------------------ interface sweep: cyclic reduction
@@ -683,34 +698,36 @@ class VelocityJacobianSolver:
             x[elim] = torch.bmm(back, rhs)[..., 0]
         return x
 
-    def _cr_solve_hip(self, g):
+    def _block_gemv(self, M, srcs, xrow, y, yrow, acc):
+        """y[yrow[b]] (+)= sum_s M[b][:, s m:(s+1) m] srcs[s][xrow[s][b]]: one sem_block_gemv launch (a batched
+        torch GEMV for operands beyond the kernel's LDS staging)."""
         import ctypes as C
         from .. import _lib
+        m, S = y.shape[1], len(srcs)
+        if not (M.is_contiguous() and xrow.is_contiguous() and yrow.is_contiguous()
+                and xrow.dtype == yrow.dtype == torch.int64 and tuple(M.shape) == (yrow.numel(), m, S * m)
+                and tuple(xrow.shape) == (S, yrow.numel())):
+            raise ValueError("sem_block_gemv: operator / index layout")
+        if S * m > GEMV_LDS_DOUBLES:   # operands beyond the kernel's LDS staging (cfg5's CR: m = 3074): batched GEMV
+            rhs = torch.cat([torch.where((r >= 0)[:, None], t[r.clamp(min=0)], 0.0) for t, r in zip(srcs, xrow)],
+                            dim=1)
+            out = torch.bmm(M, rhs[..., None])[..., 0]
+            if acc:
+                y[yrow] += out
+            else:
+                y[yrow] = out
+            return
         lib = _lib.load()
-        m = g.shape[1]
-        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        x = torch.zeros_like(g)
         P = C.c_void_p
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        src = (P * S)(*(P(t.data_ptr()) for t in srcs))
+        ld = (C.c_int64 * S)(*(t.stride(0) for t in srcs))
+        _lib.check(lib.sem_block_gemv(yrow.numel(), m, S, P(M.data_ptr()), src, ld, P(xrow.data_ptr()),
+                                      P(y.data_ptr()), y.stride(0), P(yrow.data_ptr()), int(acc), stream))
 
-        def gemv(M, srcs, xrow, y, yrow, acc):
-            S = len(srcs)
-            if not (M.is_contiguous() and xrow.is_contiguous() and yrow.is_contiguous()
-                    and xrow.dtype == yrow.dtype == torch.int64 and tuple(M.shape) == (yrow.numel(), m, S * m)
-                    and tuple(xrow.shape) == (S, yrow.numel())):
-                raise ValueError("sem_block_gemv: operator / index layout")
-            if S * m > GEMV_LDS_DOUBLES:   # operands beyond the kernel's LDS staging (cfg5: m = 3074): batched GEMV
-                rhs = torch.cat([torch.where((r >= 0)[:, None], t[r.clamp(min=0)], 0.0) for t, r in zip(srcs, xrow)],
-                                dim=1)
-                out = torch.bmm(M, rhs[..., None])[..., 0]
-                if acc:
-                    y[yrow] += out
-                else:
-                    y[yrow] = out
-                return
-            src = (P * S)(*(P(t.data_ptr()) for t in srcs))
-            ld = (C.c_int64 * S)(*(t.stride(0) for t in srcs))
-            _lib.check(lib.sem_block_gemv(yrow.numel(), m, S, P(M.data_ptr()), src, ld, P(xrow.data_ptr()),
-                                          P(y.data_ptr()), y.stride(0), P(yrow.data_ptr()), int(acc), stream))
+    def _cr_solve_hip(self, g):
+        x = torch.zeros_like(g)
+        gemv = self._block_gemv
         for keep, fwd, _, _, _, _, fx, _ in self._cr:
             gemv(fwd, (g, g), fx, g, keep, True)
         top, Tinv = self._cr_top
@@ -811,6 +828,15 @@ class VelocityJacobianSolver:
         """The interface system S xB = g (overwrites g)."""
         if self.sweep == "cr":
             return self._cr_solve(g)
+        if getattr(self, "_th", None) is not None:
+            D0, F, Bk, yr, fx, bx = self._th
+            z = torch.empty_like(g)
+            self._block_gemv(D0, (g,), yr[:1].reshape(1, 1), z, yr[0], False)
+            for L in range(1, self.nex + 1):
+                self._block_gemv(F[L - 1:L], (g, z), fx[L - 1], z, yr[L], False)
+            for L in range(self.nex - 1, -1, -1):
+                self._block_gemv(Bk[L:L + 1], (z,), bx[L], z, yr[L], True)
+            return z
         # block Thomas with the pivot blocks' explicit inverses: 2 GEMVs per line forward, 1 back
         z = g
         z[0] = self.Dinv[0] @ g[0]

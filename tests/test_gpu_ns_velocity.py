@@ -54,6 +54,31 @@ def test_device_velocity_solve_matches_sparse_lu(gpu, P, nex, ney, Re):
     assert np.abs(got - want).max() <= 1e-9 * np.abs(want).max()
 
 
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 8, 3, 700.0), (6, 2, 2, 1000.0), (2, 7, 2, 300.0), (3, 1, 2, 50.0)])
+def test_interface_sweeps_agree(gpu, P, nex, ney, Re):
+    """The two interface sweeps of the whole-mesh solve -- block cyclic reduction and block Thomas (cfg5's,
+    one sem_block_gemv launch per line and direction: [D^-1 | -D^-1 S_lo] [g; z] forward, -Uh z back) --
+    eager and graph-captured, reproduce SciPy's sparse solve."""
+    from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
+    ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex + 1)
+    ns = _device_solver(P, nex, ney, Re, u, v)
+    kw = dict(juu=ns._Jac_u_u._coeffs()[4], juv=ns._Jac_u_v._coeffs()[4], jvu=ns._Jac_v_u._coeffs()[4],
+              jvv=ns._Jac_v_v._coeffs()[4], dir_mask=ns._dir.mask, dir_sides=ns._dir.sides, **ns._sys_kw(ns._Sys))
+    r = np.random.default_rng(4)
+    bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
+    want = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
+    for sweep in ("cr", "thomas"):
+        vs = VelocityJacobianSolver(P, nex, ney, ns._mesh.device, sweep=sweep)
+        vs.factor_mesh(ns._mesh, **kw)
+        assert (getattr(vs, "_th", None) is not None) == (sweep == "thomas")
+        for graph in (False, True):
+            if graph:
+                assert vs.capture()
+            xu, xv = vs.solve(ns._dev(bu), ns._dev(bv))
+            got = np.hstack((xu.cpu().numpy(), xv.cpu().numpy()))
+            assert np.abs(got - want).max() <= 1e-9 * np.abs(want).max(), (sweep, graph)
+
+
 def test_ns_update_matches_oracle_update(gpu):
     """One Newton update (_get_update: velocity solves inside the Schur-complement Krylov solve)
     against the oracle's SuperLU + LGMRES update at the same linearisation.  The equal-order

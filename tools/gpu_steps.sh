@@ -33,8 +33,9 @@ for s in "$@"; do
     inv)        step inv 300 python tools/inv_repro.py ;;
     nsbench)    step nsbench 300 python tools/nsbench.py ;;
     pivot)      step pivot 300 python tools/pivot_probe.py ;;
+    gemvprobe)  step gemvprobe 300 python tools/gemv_probe.py ;;
     dist)       step dist 900 $PYT tests/test_gpu_dist.py -k "not cfg5_element_partitioned_ns_update" ;;
-    distcfg5)   step distcfg5 600 $PYT -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
+    distcfg5)   SEM_SLOW_GPU_TESTS=1 step distcfg5 900 $PYT -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
     cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5factor_inv) SEM_PIVOT_INV=inv SEM_PROFILE_FACTOR=1 step cfg5factor_inv 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5ns)     SEM_PROFILE_FACTOR=1 step cfg5ns 900 python tools/cfg5_ns_probe.py ;;
