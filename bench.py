@@ -211,8 +211,14 @@ def load_pmc(workload, kernel):
     except (OSError, ValueError):
         return None, None
     k = e.get("kernel", "")
-    fam = kernel[:-1] if kernel.endswith(">") else kernel
-    if not (k == kernel or k.startswith(fam + ",")):
+    # kernel_name() spells the coefficient mode as a suffix (", dpp" = CM 1, ", smem" = CM 2, none = CM 0); the
+    # PMC entry records the full instantiation <P, TXE, TYE, NS, FULL, CM, GRAD>: the families must match
+    cm, fam = "0", kernel[:-1] if kernel.endswith(">") else kernel
+    for suffix, mode in ((", dpp", "1"), (", smem", "2")):
+        if fam.endswith(suffix):
+            cm, fam = mode, fam[:-len(suffix)]
+    rest = k[len(fam) + 1:].rstrip(">").split(",") if k.startswith(fam + ",") else []
+    if not (k == kernel or (len(rest) >= 2 and rest[1].strip() == cm)):
         return None, None
     return e.get("hbm_bytes_per_launch"), k
 

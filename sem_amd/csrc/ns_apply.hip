@@ -324,11 +324,10 @@ struct NsAcc {
 };
 
 template <int P, int F, bool CVS>
-__global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tiles_y, int ntiles, int per_xcd, int ubytes,
+__global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y, int ntiles, int per_xcd, int ubytes,
                                                     int pbytes) {
   using C = NsBand<P>;
   using M = NsForm<F>;
-  using G = GllConst<P>;
   constexpr int n = P + 1, BY = C::BY, SX = C::SX, SY = C::SY, PIT = C::PIT, FLD = C::FLD;
   __shared__ double ws[n];
   __shared__ double stg[M::NF * FLD];
@@ -449,17 +448,17 @@ __global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tile
               const double uq = M::HU ? (q == P ? tu[0] : su[base + q]) : 0.0;
               const double vq = M::HU ? (q == P ? tv[0] : sv[base + q]) : 0.0;
               const double pq = M::HP ? (q == P ? tp[0] : sp[base + q]) : 0.0;
-              acc.term(G::K[P * n + q], G::G[P * n + q], fy, gyc, uq, vq, pq, vq);
+              acc.term(GllConst<P>::K[P * n + q], GllConst<P>::G[P * n + q], fy, gyc, uq, vq, pq, vq);
             });
           if (!ghost) ns_sfor<0, n, 1>([&](auto Q) {
               constexpr int q = decltype(Q)::value;
-              acc.term(G::K[q], G::G[q], fy, gyc, M::HU ? tu[q] : 0.0, M::HU ? tv[q] : 0.0, M::HP ? tp[q] : 0.0,
+              acc.term(GllConst<P>::K[q], GllConst<P>::G[q], fy, gyc, M::HU ? tu[q] : 0.0, M::HU ? tv[q] : 0.0, M::HP ? tp[q] : 0.0,
                        M::HU ? tv[q] : 0.0);
             });
         } else {
           ns_sfor<0, n, 1>([&](auto Q) {
             constexpr int q = decltype(Q)::value;
-            acc.term(G::K[j * n + q], G::G[j * n + q], fy, gyc, M::HU ? tu[q] : 0.0, M::HU ? tv[q] : 0.0,
+            acc.term(GllConst<P>::K[j * n + q], GllConst<P>::G[j * n + q], fy, gyc, M::HU ? tu[q] : 0.0, M::HU ? tv[q] : 0.0,
                      M::HP ? tp[q] : 0.0, M::HU ? tv[q] : 0.0);
           });
         }
@@ -495,7 +494,7 @@ __global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tile
     ns_sfor<0, n, 1>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       const int o = q * PIT + P + c;
-      acc.term(G::K[P * n + q], G::G[P * n + q], fx, gxc, M::HU ? su[o] : 0.0, M::HU ? sv[o] : 0.0,
+      acc.term(GllConst<P>::K[P * n + q], GllConst<P>::G[P * n + q], fx, gxc, M::HU ? su[o] : 0.0, M::HU ? sv[o] : 0.0,
                M::HP ? sp[o] : 0.0, M::HU ? su[o] : 0.0);
     });
     if constexpr (M::SYS) {
@@ -560,25 +559,6 @@ __global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tile
       const bool want_uv = M::OUV && (a.ru || a.rv), want_c = M::OC && a.rc;
       const bool cu_is_u = a.cu == a.u;
       const double fx = a.fKx * my, hym = a.hy * my, sxm = a.sx * my;
-      // the rows' pointwise operands, all loads issued before the first row's sums (buffer loads: an absent
-      // operand reads 0 without a branch)
-      constexpr int RW = C::rows(W);
-      double pcu[RW], pT[RW], pjuu[RW], pjuv[RW], pjvu[RW], pjvv[RW];
-      {
-        const auto rcu = brsrc(a.cu, M::SYS && a.cu && !cu_is_u ? pbytes : 0), rT = brsrc(a.T, M::OUV && a.T ? pbytes : 0);
-        const auto r1 = brsrc(a.juu, M::OUV && a.juu ? pbytes : 0), r2 = brsrc(a.juv, M::OUV && a.juv ? pbytes : 0);
-        const auto r3 = brsrc(a.jvu, M::OUV && a.jvu ? pbytes : 0), r4 = brsrc(a.jvv, M::OUV && a.jvv ? pbytes : 0);
-        ns_sfor<W, P, C::NW>([&](auto I) {
-          constexpr int i = decltype(I)::value, slot = (i - W) / C::NW;
-          const int off = i < t.nlx ? ((t.gx0 + i - a.lb0) * NY + gy) * 8 : -8;
-          pcu[slot] = bload(rcu, off);
-          pT[slot] = bload(rT, off);
-          pjuu[slot] = bload(r1, off);
-          pjuv[slot] = bload(r2, off);
-          pjvu[slot] = bload(r3, off);
-          pjvv[slot] = bload(r4, off);
-        });
-      }
       ns_sfor<W, P, C::NW>([&](auto I) {
         constexpr int i = decltype(I)::value, slot = (i - W) / C::NW;
         if (i >= t.nlx) return;  // the ghost position holds its line 0 only
@@ -589,7 +569,7 @@ __global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tile
         const int o = i * BY + c;
         double gxc = 0.0;
         if constexpr (M::SYS) {
-          const double cun = a.cu ? (cu_is_u ? tu[i] : pcu[slot]) : 1.0;
+          const double cun = a.cu ? (cu_is_u ? tu[i] : a.cu[q]) : 1.0;
           gxc = a.fX * cun * my;
         }
         NsAcc<F> acc;
@@ -605,13 +585,13 @@ __global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tile
           }
           if (t.hasRx) ns_sfor<0, n, 1>([&](auto Q) {
               constexpr int qq = decltype(Q)::value;
-              acc.term(G::K[qq], G::G[qq], fx, gxc, M::HU ? tu[qq] : 0.0, M::HU ? tv[qq] : 0.0,
+              acc.term(GllConst<P>::K[qq], GllConst<P>::G[qq], fx, gxc, M::HU ? tu[qq] : 0.0, M::HU ? tv[qq] : 0.0,
                        M::HP ? tp[qq] : 0.0, M::HU ? tu[qq] : 0.0);
             });
         } else {
           ns_sfor<0, n, 1>([&](auto Q) {
             constexpr int qq = decltype(Q)::value;
-            acc.term(G::K[i * n + qq], G::G[i * n + qq], fx, gxc, M::HU ? tu[qq] : 0.0, M::HU ? tv[qq] : 0.0,
+            acc.term(GllConst<P>::K[i * n + qq], GllConst<P>::G[i * n + qq], fx, gxc, M::HU ? tu[qq] : 0.0, M::HU ? tv[qq] : 0.0,
                      M::HP ? tp[qq] : 0.0, M::HU ? tu[qq] : 0.0);
           });
         }
@@ -627,15 +607,15 @@ __global__ __launch_bounds__(256, 3) void ns_apply_band(const NsArgs a, int tile
               const double fm = a.fM * mx * my;
               if (a.ru) {
                 double z = fma(fm, u0, M::SYS ? stg[M::YU * FLD + o] + acc.su : 0.0);
-                if (a.juu && own) z = fma(pjuu[slot], u0, z);
-                if (a.juv && own) z = fma(pjuv[slot], v0, z);
+                if (a.juu && own) z = fma(a.juu[q], u0, z);
+                if (a.juv && own) z = fma(a.juv[q], v0, z);
                 a.ru[qv] = fma(hym, acc.gp, z);
               }
               if (a.rv) {
                 double z = fma(fm, v0, stg[M::YV * FLD + o] + (M::SYS ? acc.sv : 0.0));
-                if (a.jvu && own) z = fma(pjvu[slot], u0, z);
-                if (a.jvv && own) z = fma(pjvv[slot], v0, z);
-                if (a.T) z = fma(a.fT * mx * my, pT[slot], z);
+                if (a.jvu && own) z = fma(a.jvu[q], u0, z);
+                if (a.jvv && own) z = fma(a.jvv[q], v0, z);
+                if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
                 a.rv[qv] = z;
               }
             }

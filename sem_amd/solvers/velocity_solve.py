@@ -200,8 +200,11 @@ class VelocityJacobianSolver:
         # SEM_PROFILE_FACTOR=1: per-phase wall times of the factorisation (device-synchronised)
         self.profile = os.environ.get("SEM_PROFILE_FACTOR", "") == "1"
         self.timing = {}
-        # edge Schur systems up to this size are inverted densely (pivoted); larger ones by block LU
-        self.edge_dense_max = 1024
+        # edge Schur systems up to this size are inverted densely (pivoted); larger ones by block LU.  On the
+        # GPU every size takes the checked block LU (its block-Thomas sweeps read (N_ey+1) 3 ne1^2 doubles per
+        # column instead of n_e^2: 48.5 -> ~15 us per edge step at cfg4, profiles/r03/vel48/); a column
+        # whose block LU fails the check still gets the pivoted dense inverse
+        self.edge_dense_max = 0 if self.device.type == "cuda" else 1024
         # edge solve of the block-LU path on the GPU: "auto" keeps the block-Thomas factors (sem_nested_solve's
         # ABI-9 form: O(N_ey ne1^2) doubles per column read per solve instead of the n_e^2 of the dense
         # inverse -- 1.5 MB instead of 64 MB per cfg5 column); "dense" keeps the dense inverse
@@ -611,20 +614,16 @@ class VelocityJacobianSolver:
                 Uh[L] = Dinv[L] @ S_up[L]
         self.Dinv, self.Uh, self.S_lo = Dinv, Uh, S_lo
         self._th = None
-        if (self.device.type == "cuda" and 2 * m <= GEMV_LDS_DOUBLES
-                and os.environ.get("SEM_THOMAS_HIP", "1") != "0"):
-            # sem_block_gemv form of the sweep: z_0 = D_0^-1 g_0, z_L = [D_L^-1 | -D_L^-1 S_lo[L-1]] [g_L; z_{L-1}],
-            # then z_L += (-Uh_L) z_{L+1}: one launch per line and direction, each operator read once
+        if self.device.type == "cuda" and os.environ.get("SEM_THOMAS_FUSED", "1") != "0":
+            # fused forward operators: z_0 = D_0^-1 g_0, z_L = [D_L^-1 | -D_L^-1 S_lo[L-1]] [g_L; z_{L-1}], then
+            # z_L -= Uh_L z_{L+1}: one GEMV per line and direction, each operator read once (the m x 2m GEMV runs
+            # at 5.7 TB/s at cfg5's m = 3,074, tools/gemv_probe.py); the subtraction of round 2's form is gone
             F = torch.empty((nex, m, 2 * m), dtype=torch.float64, device=self.device)
             F[:, :, :m] = Dinv[1:]
             for L in range(nex):
                 F[L, :, m:] = -(Dinv[L + 1] @ S_lo[L])
-            D0 = Dinv[:1].clone()
-            Uh.neg_()
-            Lr = torch.arange(nex + 1, dtype=torch.int64, device=self.device)
-            fx = torch.stack((Lr[1:], Lr[:-1]), dim=1)[:, :, None].contiguous()     # (nex, 2, 1): [L; L-1]
-            self._th = (D0, F, Uh, Lr[:, None].contiguous(), fx, Lr[1:, None, None].contiguous())
-            self.Dinv = self.Uh = self.S_lo = None
+            self._th = (Dinv[0].clone(), F, Uh)
+            self.Dinv = self.S_lo = None
         self.factored = True
 
     # ------------------------------------------------------------------ interface sweep: cyclic reduction
@@ -829,14 +828,19 @@ class VelocityJacobianSolver:
         if self.sweep == "cr":
             return self._cr_solve(g)
         if getattr(self, "_th", None) is not None:
-            D0, F, Bk, yr, fx, bx = self._th
-            z = torch.empty_like(g)
-            self._block_gemv(D0, (g,), yr[:1].reshape(1, 1), z, yr[0], False)
-            for L in range(1, self.nex + 1):
-                self._block_gemv(F[L - 1:L], (g, z), fx[L - 1], z, yr[L], False)
-            for L in range(self.nex - 1, -1, -1):
-                self._block_gemv(Bk[L:L + 1], (z,), bx[L], z, yr[L], True)
-            return z
+            # W[L] = [g_L | z_{L-1}]: the forward GEMV of line L reads one contiguous 2m vector and writes z_L
+            # straight into W[L+1]'s second half (z_nex into the last row's), so no copy sits in the chain
+            D0, F, Uh = self._th
+            nex, m = self.nex, self.m
+            W = torch.empty((nex + 2, 2 * m), dtype=g.dtype, device=g.device)
+            W[:nex + 1, :m] = g
+            torch.mv(D0, g[0], out=W[1, m:])
+            for L in range(1, nex + 1):
+                torch.mv(F[L - 1], W[L], out=W[L + 1, m:])
+            z = W[1:, m:]                       # z_L at row L
+            for L in range(nex - 1, -1, -1):
+                z[L].addmv_(Uh[L], z[L + 1], alpha=-1.0)
+            return z.contiguous()             # sem_nested_solve reads x_B as a packed (nex+1, m) array
         # block Thomas with the pivot blocks' explicit inverses: 2 GEMVs per line forward, 1 back
         z = g
         z[0] = self.Dinv[0] @ g[0]

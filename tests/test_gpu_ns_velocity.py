@@ -56,9 +56,9 @@ def test_device_velocity_solve_matches_sparse_lu(gpu, P, nex, ney, Re):
 
 @pytest.mark.parametrize("P,nex,ney,Re", [(4, 8, 3, 700.0), (6, 2, 2, 1000.0), (2, 7, 2, 300.0), (3, 1, 2, 50.0)])
 def test_interface_sweeps_agree(gpu, P, nex, ney, Re):
-    """The two interface sweeps of the whole-mesh solve -- block cyclic reduction and block Thomas (cfg5's,
-    one sem_block_gemv launch per line and direction: [D^-1 | -D^-1 S_lo] [g; z] forward, -Uh z back) --
-    eager and graph-captured, reproduce SciPy's sparse solve."""
+    """The two interface sweeps of the whole-mesh solve -- block cyclic reduction and block Thomas (cfg5's:
+    one GEMV per line and direction, [D^-1 | -D^-1 S_lo] [g; z] forward, -Uh z back) -- eager and
+    graph-captured, reproduce SciPy's sparse solve."""
     from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
     ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex + 1)
     ns = _device_solver(P, nex, ney, Re, u, v)
@@ -151,7 +151,10 @@ def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     vs.hip_nested = False
     x_torch = vs._solve_lines(B.clone())
     vs.hip_nested = True
-    assert (x_hip - x_torch).abs().max().item() <= 1e-12 * x_torch.abs().max().item()
+    # the two paths apply the same factors in different orders; the block-Thomas edge sweeps (ABI 9) carry
+    # the rounding through N_ey+1 dependent steps, so the bar is the solve's accuracy, not 1e-15
+    err = (x_hip - x_torch).abs().max().item() / x_torch.abs().max().item()
+    assert err <= 1e-10, err
     from sem_amd.solvers import ConvectionDiffusionSolver
     cd = ConvectionDiffusionSolver(1.0, 1.0, Re, P, nex, ney, T_W=0.5, T_E=-0.5)
     cd._get_residuals(np.zeros(cd.N), u, v)
@@ -160,7 +163,8 @@ def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     y_hip = vc._solve_lines(b.clone())
     vc.hip_nested = False
     y_torch = vc._solve_lines(b.clone())
-    assert (y_hip - y_torch).abs().max().item() <= 1e-12 * y_torch.abs().max().item()
+    err = (y_hip - y_torch).abs().max().item() / y_torch.abs().max().item()
+    assert err <= 1e-10, err
 
 
 @pytest.mark.parametrize("nb,m,S", [(1, 770, 3), (2, 385, 2), (40, 200, 3), (24, 770, 2), (3, 17, 1), (5, 1537, 3),

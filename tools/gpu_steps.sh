@@ -50,6 +50,10 @@ for s in "$@"; do
       tools/pmc_run.sh "$O/pmc_ns128" -- python tools/nsbench.py --meshes 12:128 --reps 20 || exit 1
       tools/pmc_run.sh "$O/pmc_vel48" -- python tools/velocity_bench.py --ne 48 --P 8 --configs nested:cr --reps 20 \
         || exit 1 ;;
+    cfg5trace)
+      step cfg5trace 900 rocprofv3 --kernel-trace --stats -d "$O/cfg5trace" -o trace --output-format csv -- \
+        python tools/cfg5_ns_probe.py --update 0
+      python tools/pmc_compact.py "$O/cfg5trace" && python tools/prof_summary.py "$O/cfg5trace" "" > "$O/cfg5trace/prof_summary.txt" ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
     benchtrace)

@@ -1,7 +1,7 @@
 """Shrink a tools/pmc_run.sh output directory in place, so that it travels back from the GPU box
 (gpurun copies at most 64 MiB of gpurun_out/): every *counter_collection.csv becomes one row per
 (kernel, grid, counter) holding the per-dispatch mean and the dispatch count, and every
-*kernel_trace.csv keeps only the sem:: dispatches and the columns tools/prof_summary.py reads.
+*kernel_trace.csv keeps only the columns tools/prof_summary.py reads.
 tools/prof_summary.py and tools/pmc_traffic.py read both forms.
 
 python tools/pmc_compact.py OUTDIR
@@ -31,9 +31,8 @@ def compact_trace(f):
     keep = []
     with open(f) as fh:
         for r in csv.DictReader(fh):
-            if "sem::" in r["Kernel_Name"]:
-                grid = r.get("Grid_Size") or r.get("Grid_Size_X") or "?"
-                keep.append((r["Kernel_Name"], grid, r["Start_Timestamp"], r["End_Timestamp"]))
+            grid = r.get("Grid_Size") or r.get("Grid_Size_X") or "?"
+            keep.append((r["Kernel_Name"], grid, r["Start_Timestamp"], r["End_Timestamp"]))
     with open(f, "w", newline="") as fh:
         w = csv.writer(fh)
         w.writerow(["Kernel_Name", "Grid_Size", "Start_Timestamp", "End_Timestamp"])
