@@ -255,6 +255,14 @@ struct NsBand {
   static constexpr int NST = (SX * SY + THREADS - 1) / THREADS;   // staging loads per thread and field
   static constexpr int NCV = (P * BY + THREADS - 1) / THREADS;    // cv staging loads per thread
   static constexpr int XLW = 3;               // the wave with the fewest y rows (rows 3, 7, ...)
+  // Y-phase lane -> (line r, element b): line fastest where that makes the staged-window reads
+  // ((P + r) PIT + b P + q, ds_read_b64 in two 32-lane groups) and the Y-sum stores (r PIT + b P + j,
+  // ds_write_b64 in four 16-lane groups) bank-conflict free (P = 4, 8, 12, 16 exactly; counted per order
+  // with the LDS banking of MI355X_MICROARCH.md); element fastest for the orders where it conflicts less.
+  static constexpr bool RF = !(P == 3 || P == 6 || P == 7 || P == 10);
+  static constexpr int SCP = BY | 1;          // odd pitch of the staged cv lines
+  static __device__ __forceinline__ int yline(int lane) { return RF ? lane % P : lane / TYE; }
+  static __device__ __forceinline__ int yelem(int lane) { return RF ? lane / P : lane % TYE; }
   static constexpr int rows(int w) { return w < P ? (P - 1 - w) / NW + 1 : 0; }
 };
 
@@ -331,7 +339,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
   constexpr int n = P + 1, BY = C::BY, SX = C::SX, SY = C::SY, PIT = C::PIT, FLD = C::FLD;
   __shared__ double ws[n];
   __shared__ double stg[M::NF * FLD];
-  __shared__ double scv[CVS ? P * BY : 1];
+  __shared__ double scv[CVS ? P * C::SCP : 1];
   __shared__ double xl[M::NXL > 0 ? M::NXL * 64 : 1];
   double* const su = stg + M::IU * FLD;
   double* const sv = stg + M::IV * FLD;
@@ -403,7 +411,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
 #pragma unroll
     for (int s = 0; s < C::NCV; ++s) {
       const int k = tid + s * C::THREADS;
-      if (k < P * BY) scv[k] = st_c[s];
+      if (k < P * BY) scv[(k / BY) * C::SCP + k % BY] = st_c[s];
     }
   }
   __syncthreads();
@@ -415,7 +423,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
     constexpr int W = decltype(WW)::value;
     if constexpr (C::rows(W) > 0) {
       if (lane >= P * C::TYE) return;
-      const int r = lane / C::TYE, b = lane - r * C::TYE;
+      const int r = C::yline(lane), b = C::yelem(lane);
       const int pos = t.n0 + b;
       if (r >= t.nlx || pos > a.ney) return;
       const bool ghost = pos == a.ney, hasL = pos > 0;
@@ -438,7 +446,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
         const int c = b * P + j;      // tile column of the node
         double gyc = 0.0;
         if constexpr (M::SYS) {
-          const double cvn = CVS ? scv[r * BY + c] : (a.cv ? tv[j] : 1.0);  // !CVS: cv is v itself or absent
+          const double cvn = CVS ? scv[r * C::SCP + c] : (a.cv ? tv[j] : 1.0);  // !CVS: cv is v itself or absent
           gyc = a.fY * cvn * mx;
         }
         NsAcc<F> acc;
@@ -512,7 +520,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
     constexpr int W = decltype(WW)::value;
     if constexpr (C::rows(W) > 0 && M::NY > 0) {
       if (lane >= P * C::TYE) return;
-      const int r = lane / C::TYE, b = lane - r * C::TYE;
+      const int r = C::yline(lane), b = C::yelem(lane);
       const int pos = t.n0 + b;
       if (r >= t.nlx || pos > a.ney) return;
       const bool ghost = pos == a.ney;
@@ -520,7 +528,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
         constexpr int j = decltype(J)::value, slot = (j - W) / C::NW;
         if (ghost && j != 0) return;
 #pragma unroll
-        for (int k = 0; k < M::NY; ++k) stg[k * FLD + r * BY + b * P + j] = yres[slot][k];
+        for (int k = 0; k < M::NY; ++k) stg[k * FLD + r * PIT + b * P + j] = yres[slot][k];
       });
     }
   };
@@ -566,7 +574,7 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
         const int64_t q = static_cast<int64_t>(gx - a.lb0) * NY + gy;
         const int64_t qv = static_cast<int64_t>(gx - a.lb0) * pitch + gy;
         const double mx = wsum1(gx, P, a.ex_begin, a.ex_end, ws);
-        const int o = i * BY + c;
+        const int o = i * PIT + c;  // Y sums: line pitch PIT (odd)
         double gxc = 0.0;
         if constexpr (M::SYS) {
           const double cun = a.cu ? (cu_is_u ? tu[i] : a.cu[q]) : 1.0;

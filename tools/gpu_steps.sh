@@ -60,6 +60,17 @@ for s in "$@"; do
       step bench 600 python bench.py
       step benchtrace 600 rocprofv3 --kernel-trace --stats -d "$O/benchtrace" -o trace --output-format csv -- \
         python bench.py --cpu-seconds 0 ;;
+    bandab)     # every band-kernel variant on the HBM mesh and cfg2 (one process per knob value: read once)
+      step bandab_floor 300 python tools/kbench.py --meshes 8:1024 --reps 100 --floor
+      for t in 0 1 2 3 4 5 6 7 8 9; do
+        SEM_BAND_TILE=$t step bandab_t$t 300 python tools/kbench.py --meshes 8:64,8:1024 --reps 200
+      done
+      for w in 512 2048 4096; do
+        SEM_BAND_TILE=8 SEM_MARCH_WG=$w step bandab_m$w 300 python tools/kbench.py --meshes 8:1024 --reps 200
+      done
+      for c in 5 1 4 257 260; do
+        SEM_BAND_CPOL=$c step bandab_c$c 300 python tools/kbench.py --meshes 8:1024 --reps 200
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
