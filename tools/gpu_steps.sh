@@ -50,6 +50,8 @@ for s in "$@"; do
       tools/pmc_run.sh "$O/pmc_ns128" -- python tools/nsbench.py --meshes 12:128 --reps 20 || exit 1
       tools/pmc_run.sh "$O/pmc_vel48" -- python tools/velocity_bench.py --ne 48 --P 8 --configs nested:cr --reps 20 \
         || exit 1 ;;
+    pmcns128)
+      tools/pmc_run.sh "$O/pmc_ns128" -- python tools/nsbench.py --meshes 12:128 --reps 20 || exit 1 ;;
     cfg5trace)
       step cfg5trace 900 rocprofv3 --kernel-trace --stats -d "$O/cfg5trace" -o trace --output-format csv -- \
         python tools/cfg5_ns_probe.py --update 0
