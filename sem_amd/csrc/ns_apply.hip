@@ -311,6 +311,29 @@ __device__ __forceinline__ bool ns_dir(const NsArgs& a, int64_t q, int gx, int g
                    ((a.sides & SEM_SIDE_S) && gy == 0) || ((a.sides & SEM_SIDE_N) && gy == a.NY - 1));
 }
 
+// Kernel arguments re-read at the point of use.  Taken from the kernel argument `a` by value, the
+// ~50 SGPRs of output / operand pointers and factors the epilogue needs are loaded once at kernel entry
+// and stay live through every unrolled row; with the fp64 coefficients' SGPR pairs on top, the residual
+// forms spilled 35-52 SGPRs into VGPR lanes and paid one v_readlane_b32 (a VALU instruction) per
+// reload: ~3,500 readlanes against ~2,600 fp64 FMAs in the P = 12 residual kernel's code.  Read through
+// a laundered kernarg-segment pointer instead, each row's fields are fresh scalar loads (s_load through
+// the constant cache) whose SGPRs die with the row.  `a` is the kernel's first argument: offset 0.
+using NsKArgs = const __attribute__((address_space(4))) NsArgs;
+// LAUNDER = false leaves the loads to the compiler (hoisted, as for a by-value argument): the forms without the
+// Sys sums (Schur gradient / divergence) never spilled, and per-row reloads cost them 3-10 %.
+template <bool LAUNDER>
+__device__ __forceinline__ NsKArgs* ns_kargs() {
+  auto p = (NsKArgs*)(__builtin_amdgcn_kernarg_segment_ptr());  // C cast: the builtin returns __constant__ void*
+  if constexpr (LAUNDER) asm volatile("" : "+s"(p));
+  return p;
+}
+
+__device__ __forceinline__ bool ns_dir_k(NsKArgs* a, int64_t q, int gx, int gy) {
+  return a->mask ? a->mask[q] != 0
+                : (((a->sides & SEM_SIDE_W) && gx == 0) || ((a->sides & SEM_SIDE_E) && gx == a->NX - 1) ||
+                   ((a->sides & SEM_SIDE_S) && gy == 0) || ((a->sides & SEM_SIDE_N) && gy == a->NY - 1));
+}
+
 // One term of a row: the Sys coefficient of the row formed from the 1-D K and G entries (cK K + Re c G, as
 // the reference's CSR row holds it) and every sum that uses the operand values.
 template <int F>
@@ -336,6 +359,12 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
                                                     int pbytes) {
   using C = NsBand<P>;
   using M = NsForm<F>;
+  // per-row kernel-argument reads (ns_kargs) for the residual form (Sys sums, cv = v: 52 SGPR spills and
+  // ~3,500 readlanes without them; VALU instructions per launch 22.7 M -> 13.5 M, 72 -> 63 us at cfg5); the
+  // Jacobian form (staged cv) measured 3 % slower with them and the Schur forms never spilled: they keep `a`
+  constexpr bool KR = M::SYS && !CVS;
+#define NSA(f) (KR ? A->f : a.f)
+#define NSDIR(...) (KR ? ns_dir_k(A, __VA_ARGS__) : ns_dir(a, __VA_ARGS__))
   constexpr int n = P + 1, BY = C::BY, SX = C::SX, SY = C::SY, PIT = C::PIT, FLD = C::FLD;
   __shared__ double ws[n];
   __shared__ double stg[M::NF * FLD];
@@ -474,7 +503,8 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
         if constexpr (M::OUV) yres[slot][M::YV] = M::SYS ? fma(hxm, acc.gp, acc.sv) : hxm * acc.gp;
         if constexpr (M::OC) {
           const int gy = t.gy0 + c;
-          const bool dir = ns_dir(a, static_cast<int64_t>(gx - a.lb0) * NY + gy, gx, gy);
+          NsKArgs* const A = ns_kargs<KR>();  // unused (no load) unless KR
+          const bool dir = NSDIR(static_cast<int64_t>(gx - NSA(lb0)) * NY + gy, gx, gy);
           yres[slot][M::YC] = dir ? (M::HP ? sym * acc.kp : 0.0) : (M::HU ? hxm * acc.gw : 0.0);
         }
       });
@@ -570,15 +600,16 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
       ns_sfor<W, P, C::NW>([&](auto I) {
         constexpr int i = decltype(I)::value, slot = (i - W) / C::NW;
         if (i >= t.nlx) return;  // the ghost position holds its line 0 only
+        NsKArgs* const A = ns_kargs<KR>();  // unused (no load) unless KR
         const int gx = t.gx0 + i;
-        const int64_t q = static_cast<int64_t>(gx - a.lb0) * NY + gy;
-        const int64_t qv = static_cast<int64_t>(gx - a.lb0) * pitch + gy;
-        const double mx = wsum1(gx, P, a.ex_begin, a.ex_end, ws);
+        const int64_t q = static_cast<int64_t>(gx - NSA(lb0)) * NY + gy;
+        const int64_t qv = static_cast<int64_t>(gx - NSA(lb0)) * pitch + gy;
+        const double mx = wsum1(gx, P, NSA(ex_begin), NSA(ex_end), ws);
         const int o = i * PIT + c;  // Y sums: line pitch PIT (odd)
         double gxc = 0.0;
         if constexpr (M::SYS) {
-          const double cun = a.cu ? (cu_is_u ? tu[i] : a.cu[q]) : 1.0;
-          gxc = a.fX * cun * my;
+          const double cun = NSA(cu) ? (cu_is_u ? tu[i] : NSA(cu)[q]) : 1.0;
+          gxc = NSA(fX) * cun * my;
         }
         NsAcc<F> acc;
         if constexpr (i == 0) {
@@ -603,47 +634,47 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
                      M::HP ? tp[qq] : 0.0, M::HU ? tu[qq] : 0.0);
           });
         }
-        const bool own = !(gx == a.lb1 && a.ex_end < a.nex);  // a strip's right interface line: its right owner's
-        const bool dir = ns_dir(a, q, gx, gy);
+        const bool own = !(gx == NSA(lb1) && NSA(ex_end) < NSA(nex));  // a strip's right interface line: its right owner's
+        const bool dir = NSDIR(q, gx, gy);
         const double u0 = M::HU ? tu[i] : 0.0, v0 = M::HU ? tv[i] : 0.0;
         if constexpr (M::OUV) {
           if (want_uv) {
             if (dir) {
-              if (a.ru) a.ru[qv] = own ? u0 - (a.gu ? a.gu[q] : 0.0) : 0.0;
-              if (a.rv) a.rv[qv] = own ? v0 - (a.gv ? a.gv[q] : 0.0) : 0.0;
+              if (NSA(ru)) NSA(ru)[qv] = own ? u0 - (NSA(gu) ? NSA(gu)[q] : 0.0) : 0.0;
+              if (NSA(rv)) NSA(rv)[qv] = own ? v0 - (NSA(gv) ? NSA(gv)[q] : 0.0) : 0.0;
             } else {
-              const double fm = a.fM * mx * my;
-              if (a.ru) {
+              const double fm = NSA(fM) * mx * my;
+              if (NSA(ru)) {
                 double z = fma(fm, u0, M::SYS ? stg[M::YU * FLD + o] + acc.su : 0.0);
-                if (a.juu && own) z = fma(a.juu[q], u0, z);
-                if (a.juv && own) z = fma(a.juv[q], v0, z);
-                a.ru[qv] = fma(hym, acc.gp, z);
+                if (NSA(juu) && own) z = fma(NSA(juu)[q], u0, z);
+                if (NSA(juv) && own) z = fma(NSA(juv)[q], v0, z);
+                NSA(ru)[qv] = fma(hym, acc.gp, z);
               }
-              if (a.rv) {
+              if (NSA(rv)) {
                 double z = fma(fm, v0, stg[M::YV * FLD + o] + (M::SYS ? acc.sv : 0.0));
-                if (a.jvu && own) z = fma(a.jvu[q], u0, z);
-                if (a.jvv && own) z = fma(a.jvv[q], v0, z);
-                if (a.T) z = fma(a.fT * mx * my, a.T[q], z);
-                a.rv[qv] = z;
+                if (NSA(jvu) && own) z = fma(NSA(jvu)[q], u0, z);
+                if (NSA(jvv) && own) z = fma(NSA(jvv)[q], v0, z);
+                if (NSA(T)) z = fma(NSA(fT) * mx * my, NSA(T)[q], z);
+                NSA(rv)[qv] = z;
               }
             }
           }
         }
         if constexpr (M::OC) {
           if (want_c) {
-            const bool pinned = static_cast<int64_t>(gx) * NY + gy == a.pin;
-            const double pinrow = own ? (M::HP ? tp[i] : 0.0) - a.pin_val : 0.0;
+            const bool pinned = static_cast<int64_t>(gx) * NY + gy == NSA(pin);
+            const double pinrow = own ? (M::HP ? tp[i] : 0.0) - NSA(pin_val) : 0.0;
             const double yc = stg[M::YC * FLD + o];
             double z;
-            if (pinned && !a.pin_first)
+            if (pinned && !NSA(pin_first))
               z = pinrow;
             else if (dir)  // the (K p) row
               z = M::HP ? fma(sxm, acc.kp, yc) : 0.0;
             else if (pinned)
               z = pinrow;
             else
-              z = M::HU ? a.c_div * fma(hym, acc.gw, yc) : 0.0;
-            a.rc[q] = z;
+              z = M::HU ? NSA(c_div) * fma(hym, acc.gw, yc) : 0.0;
+            NSA(rc)[q] = z;
           }
         }
       });
@@ -655,6 +686,8 @@ __global__ __launch_bounds__(256) void ns_apply_band(const NsArgs a, int tiles_y
     case 2: x_phase(std::integral_constant<int, 2>{}); break;
     default: x_phase(std::integral_constant<int, 3>{}); break;
   }
+#undef NSA
+#undef NSDIR
 }
 
 template <int P, int F>
