@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 9
+#define SEM_ABI_VERSION 10
 
 enum sem_status {
   SEM_OK = 0,
@@ -135,7 +135,9 @@ enum sem_tune {
   SEM_TUNE_COL_TILE = 5,  /* SEM_COL_TILE: column kernel tile                                     */
   SEM_TUNE_NS_APPLY = 6,  /* SEM_NS_APPLY: 1 = sem_ns_apply's LDS-tile form instead of the band form
                            * (the one knob whose variants agree to rounding, not bitwise)           */
-  SEM_TUNE_COUNT = 7
+  SEM_TUNE_EDGE_THOMAS = 7, /* SEM_EDGE_THOMAS: 1 = the ABI-9 runtime-width edge sweep of sem_nested_solve
+                             * instead of the templated one (A/B only; agrees to rounding)             */
+  SEM_TUNE_COUNT = 8
 };
 
 /* ---- library ------------------------------------------------------------ */
@@ -295,9 +297,12 @@ typedef struct sem_nested_desc {
   double* Ye;
   /* ABI 9: the edge Schur complement as its block-Thomas factors instead of the dense inverse Se (Se = NULL):
    * per column Ed[k] = inverse pivot block k (N_ey+1 of ne1 x ne1), El[k] = lower block (edge k+1 <- k) and
-   * Eu[k] = Ed[k] A_up[k] (edge k <- k+1), N_ey each, column-major; the edge solve is then a forward and a
+   * Eu[k] = Ed[k] A_up[k] (edge k <- k+1), N_ey each; the edge solve is then a forward and a
    * back sweep over the column's N_ey+1 edges (one wavefront per column) reading O(N_ey ne1^2) doubles
-   * instead of the n_e^2 of the dense inverse (cfg5: 1.5 MB instead of 64 MB per column).  ne1 <= 32. */
+   * instead of the n_e^2 of the dense inverse (cfg5: 1.5 MB instead of 64 MB per column).  ne1 <= 32.
+   * ABI 10: these three are stored ROW-major (half-rows are 16-byte vector loads in the templated sweep), and
+   * the sweep computes the edge offsets as pe[k ne1 + (l-1) nc + c] = (l-1) m + c N_y + k P instead of
+   * loading pe (the layout VelocityJacobianSolver._nested_index builds). */
   const double* Ed;
   const double* El;
   const double* Eu;

@@ -46,6 +46,7 @@ Tuning& tuning() {
     r.v[SEM_TUNE_MFMA_TILE] = env_int("SEM_MFMA_TILE");
     r.v[SEM_TUNE_COL_TILE] = env_int("SEM_COL_TILE");
     r.v[SEM_TUNE_NS_APPLY] = env_int("SEM_NS_APPLY");
+    r.v[SEM_TUNE_EDGE_THOMAS] = env_int("SEM_EDGE_THOMAS");
     return r;
   }();
   return t;

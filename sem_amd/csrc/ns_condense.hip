@@ -172,19 +172,159 @@ __global__ __launch_bounds__(kCondThreads) void cond_edge_kernel(const CondArgs 
   }
 }
 
-// K2, block-Thomas form (ABI 9): one wavefront per column, lane i = row i of the ne1 x ne1 edge blocks.
+// K2, block-Thomas form (ABI 10): one wavefront per column; the ne1 x ne1 edge blocks are row-major.
 //   forward  z_k = Ed_k (r_k - El_{k-1} z_{k-1}),   back  y_k = z_k - Eu_k y_{k+1}
-// Each step is two (forward) or one (back) lane-per-row GEMVs on the previous step's vector, broadcast from
-// LDS; the next step's blocks are loaded into registers while the current step computes, so the sweep runs
-// at the latency of its dependent FMA chains, not of memory.  Columns are independent (grid = nex).
+// Templated on the block width B = ne1, so every row/column guard is compile-time (the runtime-width kernel
+// of ABI 9 spilled 112 SGPRs and held 422 VGPRs: each `j < b` of its 32-wide unrolled rows was an exec-mask
+// branch).  Lane (h, i) = half h of row i: it owns the H columns [h H, h H + H) of row i, so one GEMV is H
+// dependent FMAs per lane instead of B, and the two halves' partial sums meet in LDS, where every lane reads
+// the pair sums of its own columns for the next GEMV (one LDS round trip per GEMV, the halves' combination
+// folded into the broadcast).  The operands of the next kD steps (the half-rows of El_{k-1}, Ed_k or Eu_k,
+// and the step's right-hand side) are loaded kD steps ahead into a register ring: the edge offsets are
+// arithmetic (no index load in front of the right-hand side's load), so no load waits on another and the
+// sweep runs at the latency of its FMA chains and LDS round trips, not of memory.  Columns are independent
+// (grid = nex).
 constexpr int kThomasB = 32;  // largest ne1 (= nc (P-1)) of the block-Thomas form
 
-__device__ __forceinline__ void load_block_col(const double* __restrict__ M, int b, int i, double (&r)[kThomasB]) {
+template <int B>
+struct EdgeThomas {
+  static constexpr int H = B <= 1 ? 2 : (((B + 1) / 2 + 1) & ~1);  // columns per half-row (even)
+  static constexpr bool VEC = (B % 2) == 0;                         // 16-byte aligned half-rows
+  static constexpr int D = 3;                                       // steps loaded ahead
+};
+
+// half-row h of row i (columns [h H, h H + H) below B) of the row-major B x B block M; zero elsewhere
+template <int B>
+__device__ __forceinline__ void load_half_row(const double* __restrict__ M, int i, int h,
+                                              double (&r)[EdgeThomas<B>::H]) {
+  constexpr int H = EdgeThomas<B>::H;
+  const int j0 = h * H;
+  if constexpr (EdgeThomas<B>::VEC) {
 #pragma unroll
-  for (int j = 0; j < kThomasB; ++j) r[j] = (j < b && i < b) ? M[j * b + i] : 0.0;
+    for (int q = 0; q < H; q += 2) {
+      double2 v = make_double2(0.0, 0.0);
+      if (i < B && j0 + q < B) v = *reinterpret_cast<const double2*>(M + i * B + j0 + q);
+      r[q] = v.x;
+      r[q + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < H; ++q) r[q] = (i < B && j0 + q < B) ? M[i * B + j0 + q] : 0.0;
+  }
 }
 
+// sum over this lane's columns of M-row * (p[0][j] + p[1][j]): the two halves' partial sums of the vector
+template <int H>
+__device__ __forceinline__ double half_dot(const double (&r)[H], const double* p0, const double* p1) {
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int q = 0; q < H; q += 2) {
+    a0 = fma(r[q], p0[q] + p1[q], a0);
+    a1 = fma(r[q + 1], p0[q + 1] + p1[q + 1], a1);
+  }
+  return a0 + a1;
+}
+
+template <int B>
 __global__ __launch_bounds__(64) void cond_edge_thomas_kernel(const CondArgs a) {
+  constexpr int H = EdgeThomas<B>::H, D = EdgeThomas<B>::D;
+  constexpr int64_t bb = static_cast<int64_t>(B) * B;
+  __shared__ double pt[2][2 * H], pz[2][2 * H];  // [half][row] partial sums of t (forward) and z / y
+  const int e = blockIdx.x, nb = a.ney + 1, lane = threadIdx.x, i = lane & 31, h = lane >> 5, j0 = h * H;
+  const bool row = i < B, own = row && h == 0;  // own: the lane that holds row i's value
+  const double* C = a.C + static_cast<int64_t>(e) * a.ney * 2 * B;
+  const double* Ed = a.Ed + static_cast<int64_t>(e) * nb * bb;
+  const double* El = a.El + static_cast<int64_t>(e) * a.ney * bb;
+  const double* Eu = a.Eu + static_cast<int64_t>(e) * a.ney * bb;
+  double* Ye = a.Ye + static_cast<int64_t>(e) * a.n_e;
+  double* Y = a.Y + e * a.ld_y;
+  // edge offset of row i of edge k: i = (l-1) nc + c  ->  (l-1) m + c N_y + k P  (VelocityJacobianSolver._pe)
+  const int nc = B / (a.P - 1), NY = a.m / nc;
+  const int64_t off_i = static_cast<int64_t>(i / nc) * a.m + static_cast<int64_t>(i % nc) * NY;
+  auto edge_off = [&](int k) { return off_i + static_cast<int64_t>(k) * a.P; };
+  auto redge = [&](int k) {  // reduced edge right-hand side of row i of edge k (own lanes)
+    double v = 0.0;
+    if (own) {
+      v = rhs(a, e, edge_off(k));
+      if (k < a.ney) v -= C[static_cast<int64_t>(k) * 2 * B + i];
+      if (k > 0) v -= C[static_cast<int64_t>(k - 1) * 2 * B + B + i];
+    }
+    return v;
+  };
+  if (i >= 2 * H) return;  // no row and no column of this lane (B <= 2 H - 1 < 32); never reaches a barrier
+  // ---- forward sweep, operands of steps k .. k+D-1 in the ring (slot k % D)
+  double rl[D][H], rd[D][H], rr[D];
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+    if (s < nb) {
+      if (s > 0) load_half_row<B>(El + (s - 1) * bb, i, h, rl[s]);
+      load_half_row<B>(Ed + s * bb, i, h, rd[s]);
+      rr[s] = redge(s);
+    }
+  for (int k0 = 0; k0 < nb; k0 += D) {
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      const int k = k0 + s;
+      if (k < nb) {
+        // t_i = r_i - (El_{k-1} z_{k-1})_i, as the two halves' partial sums
+        double t = rr[s];
+        if (k > 0) t -= half_dot<H>(rl[s], &pz[0][j0], &pz[1][j0]);
+        __syncthreads();
+        pt[h][i] = row ? t : 0.0;
+        __syncthreads();
+        const double z = half_dot<H>(rd[s], &pt[0][j0], &pt[1][j0]);
+        __syncthreads();
+        pz[h][i] = row ? z : 0.0;
+        __syncthreads();
+        if (own) Ye[static_cast<int64_t>(k) * B + i] = pz[0][i] + pz[1][i];
+        if (k + D < nb) {  // refill the slot with step k + D
+          load_half_row<B>(El + (k + D - 1) * bb, i, h, rl[s]);
+          load_half_row<B>(Ed + (k + D) * bb, i, h, rd[s]);
+          rr[s] = redge(k + D);
+        }
+      }
+    }
+  }
+  // ---- back sweep: pz holds y_{nb-1} = z_{nb-1} (as partial sums); steps k = nb-2 .. 0, slot (nb-2-k) % D
+  if (own) Y[edge_off(nb - 1)] = pz[0][i] + pz[1][i];
+  double ru[D][H], rz[D];
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+    if (nb - 2 - s >= 0) {
+      load_half_row<B>(Eu + (nb - 2 - s) * bb, i, h, ru[s]);
+      rz[s] = own ? Ye[static_cast<int64_t>(nb - 2 - s) * B + i] : 0.0;
+    }
+  for (int c0 = 0; c0 < nb - 1; c0 += D) {
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      const int k = nb - 2 - (c0 + s);
+      if (k >= 0) {
+        const double y = rz[s] - half_dot<H>(ru[s], &pz[0][j0], &pz[1][j0]);
+        __syncthreads();
+        pz[h][i] = row ? y : 0.0;
+        __syncthreads();
+        if (own) {
+          const double v = pz[0][i] + pz[1][i];
+          Ye[static_cast<int64_t>(k) * B + i] = v;
+          Y[edge_off(k)] = v;
+        }
+        if (k - D >= 0) {
+          load_half_row<B>(Eu + (k - D) * bb, i, h, ru[s]);
+          rz[s] = own ? Ye[static_cast<int64_t>(k - D) * B + i] : 0.0;
+        }
+      }
+    }
+  }
+}
+
+// The ABI-9 sweep (runtime block width, one lane per row, one step loaded ahead), kept for in-process A/B
+// against the templated kernel (SEM_EDGE_THOMAS=1); it reads the ABI-10 row-major blocks.
+__device__ __forceinline__ void load_block_row(const double* __restrict__ M, int b, int i, double (&r)[kThomasB]) {
+#pragma unroll
+  for (int j = 0; j < kThomasB; ++j) r[j] = (j < b && i < b) ? M[i * b + j] : 0.0;
+}
+
+__global__ __launch_bounds__(64) void cond_edge_thomas_rt_kernel(const CondArgs a) {
   __shared__ double vb[2][kThomasB];
   const int e = blockIdx.x, b = a.ne1, nb = a.ney + 1, i = threadIdx.x;
   const int64_t bb = static_cast<int64_t>(b) * b;
@@ -193,22 +333,20 @@ __global__ __launch_bounds__(64) void cond_edge_thomas_kernel(const CondArgs a) 
   const double* El = a.El + static_cast<int64_t>(e) * a.ney * bb;
   const double* Eu = a.Eu + static_cast<int64_t>(e) * a.ney * bb;
   double* Ye = a.Ye + static_cast<int64_t>(e) * a.n_e;
-  auto redge = [&](int k) {  // reduced edge right-hand side of row i of edge k
+  auto redge = [&](int k) {
     if (i >= b) return 0.0;
-    const int r = k * b + i;
-    double v = rhs(a, e, a.pe[r]);
+    double v = rhs(a, e, a.pe[k * b + i]);
     if (k < a.ney) v -= C[static_cast<int64_t>(k) * 2 * b + i];
     if (k > 0) v -= C[static_cast<int64_t>(k - 1) * 2 * b + b + i];
     return v;
   };
   double ml[kThomasB], md[kThomasB], nl[kThomasB], nd[kThomasB];
-  load_block_col(Ed, b, i, md);
+  load_block_row(Ed, b, i, md);
   double rk = redge(0);
-  // forward sweep
   for (int k = 0; k < nb; ++k) {
-    if (k + 1 < nb) {  // prefetch step k+1: El_k, Ed_{k+1}, its right-hand side
-      load_block_col(El + k * bb, b, i, nl);
-      load_block_col(Ed + (k + 1) * bb, b, i, nd);
+    if (k + 1 < nb) {
+      load_block_row(El + k * bb, b, i, nl);
+      load_block_row(Ed + (k + 1) * bb, b, i, nd);
     }
     const double rn = k + 1 < nb ? redge(k + 1) : 0.0;
     double t = rk;
@@ -238,11 +376,10 @@ __global__ __launch_bounds__(64) void cond_edge_thomas_kernel(const CondArgs a) 
     }
     rk = rn;
   }
-  // back sweep: vb[0] holds y_{nb-1} = z_{nb-1}
   if (i < b) a.Y[e * a.ld_y + a.pe[static_cast<int64_t>(nb - 1) * b + i]] = vb[0][i];
-  if (nb > 1) load_block_col(Eu + (nb - 2) * bb, b, i, md);
+  if (nb > 1) load_block_row(Eu + (nb - 2) * bb, b, i, md);
   for (int k = nb - 2; k >= 0; --k) {
-    if (k > 0) load_block_col(Eu + (k - 1) * bb, b, i, nd);
+    if (k > 0) load_block_row(Eu + (k - 1) * bb, b, i, nd);
     const double zk = i < b ? Ye[static_cast<int64_t>(k) * b + i] : 0.0;
     double acc = 0.0;
 #pragma unroll
@@ -259,6 +396,14 @@ __global__ __launch_bounds__(64) void cond_edge_thomas_kernel(const CondArgs a) 
 #pragma unroll
     for (int j = 0; j < kThomasB; ++j) md[j] = nd[j];
   }
+}
+
+template <int B>
+static void launch_edge_thomas(const CondArgs& a, hipStream_t s) {
+  if (a.ne1 == B)
+    hipLaunchKernelGGL(cond_edge_thomas_kernel<B>, dim3(a.nex), dim3(64), 0, s, a);
+  else if constexpr (B < kThomasB)
+    launch_edge_thomas<B + 1>(a, s);
 }
 
 // K3: y_i = T - Yie [y_e[n]; y_e[n+1]] for element (e, n), written to the element's interior nodes.
@@ -363,8 +508,10 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
   const size_t part = sem::part_size() * sizeof(double);
   hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(elems), blk, part + 2 * a.ni * sizeof(double), s, a);
   if (int st = sem::launch_check("nested_solve fwd")) return st;
-  if (thomas)
-    hipLaunchKernelGGL(sem::cond_edge_thomas_kernel, dim3(d->nex), dim3(64), 0, s, a);
+  if (thomas && sem::tune(SEM_TUNE_EDGE_THOMAS) == 1)
+    hipLaunchKernelGGL(sem::cond_edge_thomas_rt_kernel, dim3(d->nex), dim3(64), 0, s, a);
+  else if (thomas)
+    sem::launch_edge_thomas<1>(a, s);
   else
     hipLaunchKernelGGL(sem::cond_edge_kernel, dim3((a.n_e + sem::kEdgeRows - 1) / sem::kEdgeRows, d->nex), blk,
                        part + a.n_e * sizeof(double), s, a);

@@ -75,6 +75,18 @@ class GMRESResult:
         self.reorth = reorth
 
 
+def _sizes(N, restart, maxiter, inner, default_restart):
+    """Restart length and iteration cap.  A partitioned solve (inner given) sizes nothing from its local
+    length N: ranks holding strips of different sizes would otherwise leave the Arnoldi loop at different
+    iterations and their collectives would mismatch (found by the world-8 gloo test of the NS update with
+    one-column strips); the caller passes sizes every rank shares."""
+    if inner is not None:
+        if maxiter is None:
+            raise ValueError("a partitioned Krylov solve needs maxiter (a size every rank shares)")
+        return restart or default_restart, maxiter
+    return min(N, restart or default_restart), maxiter or 10 * N
+
+
 def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, precond=None, callback=None,
           inner=None, basis_out=None):
     """Right-preconditioned restarted GMRES.
@@ -96,8 +108,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
 
     N = b.numel()
     dt, dev = b.dtype, b.device
-    restart = min(N, restart or 100)
-    maxiter = maxiter or 10 * N
+    restart, maxiter = _sizes(N, restart, maxiter, inner, 100)
     x = torch.zeros_like(b) if x0 is None else x0.clone()
     bnorm = vnorm(b)
     tol = max(atol, rtol * bnorm)
@@ -223,8 +234,7 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
     """
     N = b.numel()
     dt, dev = b.dtype, b.device
-    restart = min(N, restart or 20)
-    maxiter = maxiter or 10 * N
+    restart, maxiter = _sizes(N, restart, maxiter, inner, 20)
     psolve = precond if precond is not None else (lambda t: t)
     if inner is None:
         dot = lambda A, w: A @ w  # noqa: E731

@@ -35,12 +35,15 @@ def _libs():
 
 
 def _handle(dev):
+    """One rocBLAS handle per device, created with that device current (rocblas_create_handle binds the
+    handle to the current device)."""
     key = ("h", dev.index)
     if key not in _state:
         rb, _ = _libs()
         h = C.c_void_p()
-        if rb.rocblas_create_handle(C.byref(h)) != 0:
-            raise RuntimeError("rocblas_create_handle failed")
+        with torch.cuda.device(dev):
+            if rb.rocblas_create_handle(C.byref(h)) != 0:
+                raise RuntimeError("rocblas_create_handle failed")
         _state[key] = h
     return _state[key]
 
@@ -60,7 +63,8 @@ def strided_inverse(A):
     ipiv = torch.empty((nb, n), dtype=torch.int32, device=A.device)
     info = torch.empty(nb, dtype=torch.int32, device=A.device)
     h = _handle(A.device)
-    rb.rocblas_set_stream(h, C.c_void_p(torch.cuda.current_stream(A.device).cuda_stream))
+    with torch.cuda.device(A.device):
+        rb.rocblas_set_stream(h, C.c_void_p(torch.cuda.current_stream(A.device).cuda_stream))
     p = C.c_void_p
     st = rs.rocsolver_dgetrf_strided_batched(h, n, n, p(X.data_ptr()), n, n * n, p(ipiv.data_ptr()), n,
                                              p(info.data_ptr()), nb)

@@ -222,6 +222,14 @@ class Partition:
         self.inner = DistributedInner(self.part, mesh, self.dist, self.group)
         return mesh
 
+    def max_local_dofs(self):
+        """The largest strip's DOF count over all ranks (from the bounds, no communication): a Krylov
+        restart length sized from it is the same on every rank, so every rank leaves the Arnoldi loop at the
+        same iteration and calls the same collectives (uneven strips gave ranks different
+        restarts)."""
+        b, P, NY = self.part.bounds, self.mesh.P, self.mesh.NY
+        return max((b[r + 1] - b[r]) * P + 1 for r in range(self.world)) * NY
+
     def local(self, v):
         """This rank's slice of a global vector (x-major numbering)."""
         m = self.mesh

@@ -267,7 +267,7 @@ class ConvectionDiffusionSolver:
             restart = min(restart, 100)
         if self._part is not None:
             r = gmres(lambda v: self._get_dresiduals(v), b, x0=x0, atol=self._mtol * np.sqrt(self.N), rtol=0.0,
-                      restart=restart, precond=precond, callback=cb, inner=self._part.inner)
+                      restart=restart, maxiter=10 * self.N, precond=precond, callback=cb, inner=self._part.inner)
         else:
             if self._recycle_bytes and self._recycle is None:
                 n = self._mesh.n_local

@@ -366,15 +366,18 @@ class NavierStokesSolver:
 
         it = [0]
         prog = getattr(self, "_progress", 0)
+        t_start = time.perf_counter()
 
         def cb(est):
             it[0] += 1
             if 'LGMRES_iter' in self._iprint or (prog and it[0] % prog == 0):
-                print(f'NavierStokes GMRES: {it[0]}\t{est}', flush=True)
+                print(f'NavierStokes GMRES: {it[0]}\t{est}\t{time.perf_counter() - t_start:.1f}s', flush=True)
 
-        restart = max(1, min(self.N, self._max_basis, int(32e9 // (16 * m.n_local))))
+        # restart and maxiter from sizes every rank shares (the largest strip, the global N): the ranks
+        # run the same Arnoldi iterations and so call the same collectives
+        restart = max(1, min(self.N, self._max_basis, int(32e9 // (16 * part.max_local_dofs()))))
         r = gmres(schur_mv, b_schur, x0=self._dev(dp0), atol=self._mtol * np.sqrt(self.N), rtol=0.0,
-                  restart=restart, precond=precon, callback=cb, inner=part.inner)
+                  restart=restart, maxiter=10 * self.N, precond=precon, callback=cb, inner=part.inner)
         if r.info != 0:
             raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {r.info} iterations')
         dp = r.x

@@ -23,7 +23,7 @@ on shared lines.
 """
 import torch
 
-from .velocity_solve import VelocityJacobianSolver, pivot_inverse
+from .velocity_solve import VelocityJacobianSolver, fused_thomas_operators, fused_thomas_solve, pivot_inverse
 
 
 class StripLineSolver(VelocityJacobianSolver):
@@ -93,7 +93,12 @@ class StripLineSolver(VelocityJacobianSolver):
                 X1[i] = -(Uh[i] @ X1[i + 1])
             R = torch.stack((torch.stack((S_diag[0] - S_up[0] @ X0[0], -(S_up[0] @ X1[0]))),
                              torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
-            self._T = (Dinv, Uh, S_lo[1:n - 1].contiguous() if n > 2 else None, X0, X1)
+            # the solve's operators: the fused block-Thomas sweep of the interior lines (one GEMV per line and
+            # direction, as the whole-mesh sweep) and [X0 | X1] for the back substitution in one batched GEMV
+            th = fused_thomas_operators(Dinv, S_lo[1:n - 1] if n > 2 else None, Uh[:k - 1])
+            X01 = torch.cat((X0, X1), dim=2)
+            del Dinv, Uh, X0, X1
+            self._T = (th, X01)
         self._S_up0, self._S_lon = S_up[0].clone(), S_lo[n - 1].clone()
         del S_diag, S_up, S_lo
         # the reduced system over the G + 1 strip-boundary lines, factored on every rank
@@ -119,36 +124,49 @@ class StripLineSolver(VelocityJacobianSolver):
             g[-1] -= B[-1]
 
     def _thomas(self, g):
-        """y = T^-1 g for the local interior lines (g: (k, m), overwritten)."""
-        Dinv, Uh, Slo, _, _ = self._T
-        k = g.shape[0]
-        g[0] = Dinv[0] @ g[0]
-        for i in range(1, k):
-            g[i] = Dinv[i] @ (g[i] - Slo[i - 1] @ g[i - 1])
-        for i in range(k - 2, -1, -1):
-            g[i] -= Uh[i] @ g[i + 1]
-        return g
+        """y = T^-1 g for the local interior lines (g: (k, m)): the fused block-Thomas sweep."""
+        return fused_thomas_solve(*self._T[0], g)
 
     def _iface_solve(self, g):
+        """No host synchronisation under RCCL (the all-gather stays on the device): stream-capturable."""
         if self.G == 1:
             return super()._iface_solve(g)
         n = self.nex
         if self._T is not None:
-            y = self._thomas(g[1:n].clone())
+            y = self._thomas(g[1:n])
             h = torch.stack((g[0] - self._S_up0 @ y[0], g[n] - self._S_lon @ y[-1]))
         else:
             y, h = None, torch.stack((g[0], g[1]))
-        hs = self._all_gather(h)
-        G = self.G
-        rhs = torch.zeros((G + 1, self.m), dtype=torch.float64, device=self.device)
-        for j, hj in enumerate(hs):
-            rhs[j] += hj[0]
-            rhs[j + 1] += hj[1]
+        H = torch.stack(self._all_gather(h))          # (G, 2, m): the boundary right-hand sides of every strip
+        rhs = torch.zeros((self.G + 1, self.m), dtype=torch.float64, device=self.device)
+        rhs[:-1] += H[:, 0]
+        rhs[1:] += H[:, 1]
         xb = self._red._cr_solve(rhs)
-        x0, x1 = xb[self.rank], xb[self.rank + 1]
         out = torch.empty_like(g)
-        out[0], out[n] = x0, x1
-        if y is not None:
-            _, _, _, X0, X1 = self._T
-            out[1:n] = y - (X0 @ x0[:, None])[..., 0] - (X1 @ x1[:, None])[..., 0]
+        out[0], out[n] = xb[self.rank], xb[self.rank + 1]
+        if y is not None:   # y - X0 x0 - X1 x1 = y - [X0 | X1] [x0; x1], one batched GEMV
+            out[1:n] = y - torch.matmul(self._T[1], xb[self.rank:self.rank + 2].reshape(-1))
         return out
+
+    def capture(self):
+        """Graph capture of the solve: only when the reduced system's all-gather runs on the device (RCCL,
+        capturable); under gloo the all-gather goes through the host, so the solve stays eager.
+        Under RCCL the captured graph is checked against the eager solve before it is used."""
+        if self.G > 1 and self.gather_device.type != "cuda":
+            return False
+        if not super().capture():
+            return False
+        if self.G == 1:
+            return True
+        g = torch.Generator(device=self.device).manual_seed(11)
+        b = torch.rand(self._bin.shape, dtype=torch.float64, device=self.device, generator=g)
+        want = self._solve_lines(b.clone())
+        self._bin.copy_(b)
+        self._graph.replay()
+        err = (self._xout - want).abs().max() / want.abs().max().clamp(min=1e-300)
+        ok = torch.tensor([1.0 if bool(err <= 1e-12) else 0.0], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(ok, op=self.dist.ReduceOp.MIN, group=self.group)
+        if float(ok.item()) < 1.0:     # every rank takes the same decision
+            self._graph = None
+            return False
+        return True

@@ -39,28 +39,31 @@ _STRIDED = os.environ.get("SEM_STRIDED_INV", "1") != "0"
 
 
 def _inverse(A):
-    """Inverse of a batch: rocSOLVER strided-batched on the GPU, else torch.linalg.inv; on a getrf
-    workspace-allocation failure the batch is halved."""
+    """Inverse of a batch and its per-block LU status (0 = regular; None when the route reports none):
+    rocSOLVER strided-batched on the GPU, else torch.linalg.inv_ex; on a getrf workspace-allocation failure
+    the batch is halved."""
     if _STRIDED and A.is_cuda and A.dim() == 3:
         from .. import linalg
         if linalg.available():
             try:
-                return linalg.strided_inverse(A)[0]
+                return linalg.strided_inverse(A)
             except RuntimeError:
                 if A.shape[0] == 1:
                     raise
                 h = A.shape[0] // 2
-                return torch.cat((_inverse(A[:h]), _inverse(A[h:])))
+                (x1, i1), (x2, i2) = _inverse(A[:h]), _inverse(A[h:])
+                return torch.cat((x1, x2)), torch.cat((i1, i2))
     try:
-        return torch.linalg.inv(A)
+        return torch.linalg.inv_ex(A)
     except RuntimeError as e:
         if "ALLOC_FAILED" not in str(e) or A.dim() < 3 or A.shape[0] == 1:
             raise
     out = torch.empty_like(A)
+    info = torch.empty(A.shape[0], dtype=torch.int32, device=A.device)
     step = max(1, A.shape[0] // 2)
     for i in range(0, A.shape[0], step):
-        out[i:i + step] = _inverse(A[i:i + step])
-    return out
+        out[i:i + step], info[i:i + step] = _inverse(A[i:i + step])
+    return out, info
 
 
 def _bad_blocks(A, X):
@@ -91,8 +94,10 @@ def batched_inverse(A, max_batch=None, sample=8):
     and runs at 5.2 TFLOP/s there against 0.17 for the sliced torch route, so it is the GPU path
     (_inverse).  Either way the batch is inverted in slices of max_batch (4096 strided, 128 through torch)
     and each slice is spot-checked through the residual A X - I of `sample` blocks (its first, its last
-    and evenly spaced ones); a slice whose sample misses is checked in full, and a block that misses is
-    inverted again on its own (then by a solve against the identity) before giving up."""
+    and evenly spaced ones); a slice is checked in full when its sample misses, when the LU reports a
+    singular pivot for any block or when any block of the result is not finite (both checks read the batch
+    once, cheap beside getri); a block that misses is inverted again on its own (then by a solve against the
+    identity) before giving up."""
     if A.dim() < 3:
         return batched_inverse(A[None], max_batch, sample)[0]
     if max_batch is None:   # rocSOLVER's strided path measured correct up to 16384 blocks; torch's to 512
@@ -100,11 +105,14 @@ def batched_inverse(A, max_batch=None, sample=8):
     out = torch.empty_like(A)
     for i in range(0, A.shape[0], max_batch):
         a = A[i:i + max_batch]
-        x = _inverse(a)
+        x, info = _inverse(a)
         nb = a.shape[0]
         pick = torch.linspace(0, nb - 1, min(nb, sample), device=a.device).round().long().unique()
-        bad = _bad_blocks(a[pick], x[pick])
-        for j in (_bad_blocks(a, x).tolist() if bad.numel() else []):
+        suspect = ~x.isfinite().all(dim=-1).all(dim=-1)
+        if info is not None:
+            suspect |= info != 0
+        full = _bad_blocks(a[pick], x[pick]).numel() > 0 or bool(suspect.any())
+        for j in (_bad_blocks(a, x).tolist() if full else []):
             xj = torch.linalg.inv(a[j])
             if _bad_blocks(a[j:j + 1], xj[None]).numel():
                 eye = torch.eye(a.shape[-1], dtype=a.dtype, device=a.device)
@@ -164,6 +172,37 @@ def pivot_inverse(A):
     if not _pivot_ok(A, X, r):
         return batched_inverse(A)
     return X
+
+
+def fused_thomas_operators(Dinv, S_lo, Uh):
+    """Operators of the fused block-Thomas solve of a block-tridiagonal system with lines 0..n-1, from its
+    factors (explicit pivot-block inverses Dinv (n, m, m), lower blocks S_lo (n-1, m, m), Uh_L = Dinv_L S_up_L):
+    z_0 = D_0 g_0, z_L = F_L [g_L; z_{L-1}] with F_L = [D_L | -D_L S_lo[L-1]] (m x 2m), back z_L -= Uh_L z_{L+1}:
+    one GEMV per line and direction, each operator read once (the m x 2m GEMV runs at 5.7 TB/s at cfg5's
+    m = 3,074, tools/gemv_probe.py)."""
+    n, m = Dinv.shape[0], Dinv.shape[1]
+    F = torch.empty((max(n - 1, 0), m, 2 * m), dtype=Dinv.dtype, device=Dinv.device)
+    if n > 1:
+        F[:, :, :m] = Dinv[1:]
+    for L in range(n - 1):
+        F[L, :, m:] = -(Dinv[L + 1] @ S_lo[L])
+    return Dinv[0].clone(), F, Uh
+
+
+def fused_thomas_solve(D0, F, Uh, g):
+    """x = S^-1 g from fused_thomas_operators (g: (n, m), not modified).  W[L] = [g_L | z_{L-1}]: the
+    forward GEMV of line L reads one contiguous 2m vector and writes z_L straight into W[L+1]'s second
+    half, so no copy sits in the chain; no host synchronisation (stream-capturable)."""
+    n, m = g.shape[0], g.shape[1]
+    W = torch.empty((n + 1, 2 * m), dtype=g.dtype, device=g.device)
+    W[:n, :m] = g
+    torch.mv(D0, g[0], out=W[1, m:])
+    for L in range(1, n):
+        torch.mv(F[L - 1], W[L], out=W[L + 1, m:])
+    z = W[1:, m:]                       # z_L at row L
+    for L in range(n - 2, -1, -1):
+        z[L].addmv_(Uh[L], z[L + 1], alpha=-1.0)
+    return z.contiguous()             # sem_nested_solve reads x_B as a packed (n, m) array
 
 
 class VelocityJacobianSolver:
@@ -311,8 +350,8 @@ class VelocityJacobianSolver:
         if self._edge_thomas:   # block-Thomas factors of the edge Schur complement instead of its inverse
             shapes = shapes[:3]
             Et = [torch.empty(sh, **z) for sh in ((nex, ney + 1, ne1, ne1), (nex, ney, ne1, ne1), (nex, ney, ne1, ne1))]
-            self._EtT = tuple(Et)                                   # column-major blocks
-            self._Ed, self._El, self._Eu = (t.transpose(-1, -2) for t in Et)
+            self._EtT = tuple(Et)                                   # row-major blocks (ABI 10)
+            self._Ed, self._El, self._Eu = Et
         if self.device.type == "cuda":
             T = [torch.empty(s[:-2] + (s[-1], s[-2]), **z) for s in shapes]
             if self._edge_thomas:
@@ -615,14 +654,7 @@ class VelocityJacobianSolver:
         self.Dinv, self.Uh, self.S_lo = Dinv, Uh, S_lo
         self._th = None
         if self.device.type == "cuda" and os.environ.get("SEM_THOMAS_FUSED", "1") != "0":
-            # fused forward operators: z_0 = D_0^-1 g_0, z_L = [D_L^-1 | -D_L^-1 S_lo[L-1]] [g_L; z_{L-1}], then
-            # z_L -= Uh_L z_{L+1}: one GEMV per line and direction, each operator read once (the m x 2m GEMV runs
-            # at 5.7 TB/s at cfg5's m = 3,074, tools/gemv_probe.py); the subtraction of round 2's form is gone
-            F = torch.empty((nex, m, 2 * m), dtype=torch.float64, device=self.device)
-            F[:, :, :m] = Dinv[1:]
-            for L in range(nex):
-                F[L, :, m:] = -(Dinv[L + 1] @ S_lo[L])
-            self._th = (Dinv[0].clone(), F, Uh)
+            self._th = fused_thomas_operators(Dinv, S_lo, Uh)
             self.Dinv = self.S_lo = None
         self.factored = True
 
@@ -814,6 +846,12 @@ class VelocityJacobianSolver:
             p = lambda t: t.data_ptr()  # noqa: E731
             XiT, AeiT, YieT, SeT = self._hipT
             Et = self._EtT if self._edge_thomas else (None, None, None)   # ABI 9: Se = NULL -> block Thomas
+            if self._edge_thomas:   # ABI 10: the sweep computes the edge offsets; they must be _pe's
+                kk = torch.arange(ney + 1, device=self.device)[:, None]
+                q = torch.arange(ne1, device=self.device)[None, :]
+                want = (q // self.ncomp) * m + (q % self.ncomp) * self.NY + kk * P
+                if not torch.equal(want.reshape(-1), self._pe):
+                    raise RuntimeError("nested solve: edge offsets differ from the block-Thomas sweep's layout")
             q = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
             self._nd = _lib.SemNestedDesc(P, nex, ney, self.ncomp, self.NY, p(XiT), p(AeiT), p(YieT), q(SeT),
                                           p(self._pi), p(self._pe), p(T), p(Cw), p(Ye), *(q(t) for t in Et))
@@ -828,19 +866,7 @@ class VelocityJacobianSolver:
         if self.sweep == "cr":
             return self._cr_solve(g)
         if getattr(self, "_th", None) is not None:
-            # W[L] = [g_L | z_{L-1}]: the forward GEMV of line L reads one contiguous 2m vector and writes z_L
-            # straight into W[L+1]'s second half (z_nex into the last row's), so no copy sits in the chain
-            D0, F, Uh = self._th
-            nex, m = self.nex, self.m
-            W = torch.empty((nex + 2, 2 * m), dtype=g.dtype, device=g.device)
-            W[:nex + 1, :m] = g
-            torch.mv(D0, g[0], out=W[1, m:])
-            for L in range(1, nex + 1):
-                torch.mv(F[L - 1], W[L], out=W[L + 1, m:])
-            z = W[1:, m:]                       # z_L at row L
-            for L in range(nex - 1, -1, -1):
-                z[L].addmv_(Uh[L], z[L + 1], alpha=-1.0)
-            return z.contiguous()             # sem_nested_solve reads x_B as a packed (nex+1, m) array
+            return fused_thomas_solve(*self._th, g)
         # block Thomas with the pivot blocks' explicit inverses: 2 GEMVs per line forward, 1 back
         z = g
         z[0] = self.Dinv[0] @ g[0]

@@ -58,7 +58,7 @@ def test_repairs_blocks_the_batched_call_got_wrong(monkeypatch):
         calls.append(a.shape[0])
         x[0] *= 3.0
         x[len(calls) % a.shape[0] + 1] *= 3.0
-        return x
+        return x, torch.zeros(a.shape[0], dtype=torch.int32)
 
     monkeypatch.setattr(VS, "_inverse", corrupt)
     X = VS.batched_inverse(A, max_batch=128)
@@ -67,9 +67,29 @@ def test_repairs_blocks_the_batched_call_got_wrong(monkeypatch):
     assert (X - want).abs().max() <= 1e-13 * want.abs().max()
 
 
+def test_unsampled_bad_block_found_by_lu_status(monkeypatch):
+    """A block the 8-block sample misses is still repaired when the LU reports it singular (info != 0) or its
+    computed inverse is not finite: either sends the slice to the full check."""
+    A = _blocks(300, 12, 9)
+    for how in ("info", "nan"):
+        def route(a):
+            x = torch.linalg.inv(a)
+            info = torch.zeros(a.shape[0], dtype=torch.int32)
+            x[37] *= 3.0                   # never among the 8 sampled blocks of a 128-block slice
+            if how == "info":
+                info[37] = 5
+            else:
+                x[38, 0, 0] = float("nan")
+            return x, info
+        monkeypatch.setattr(VS, "_inverse", route)
+        X = VS.batched_inverse(A, max_batch=128)
+        want = torch.linalg.inv(A)
+        assert (X - want).abs().max() <= 1e-13 * want.abs().max(), how
+
+
 def test_raises_when_no_route_inverts(monkeypatch):
     A = _blocks(10, 8, 6)
-    monkeypatch.setattr(VS, "_inverse", lambda a: torch.zeros_like(a))
+    monkeypatch.setattr(VS, "_inverse", lambda a: (torch.zeros_like(a), None))
     real_inv = torch.linalg.inv
     monkeypatch.setattr(torch.linalg, "inv", lambda a: real_inv(a) * 2.0)
     monkeypatch.setattr(torch.linalg, "solve", lambda a, b: torch.zeros_like(b))

@@ -1,4 +1,4 @@
-"""World-size 2/3 gloo tests (CPU) of the strip-partitioned Navier-Stokes solver
+"""World-size 2/3/8 gloo tests (CPU) of the strip-partitioned Navier-Stokes solver
 (NavierStokesSolver(partition=...)), the NS half of the element-partitioned Boussinesq (cfg5):
 
 * _get_residuals / _calc_jacobians / _get_dresiduals (global NumPy in, global NumPy out) on element
@@ -88,6 +88,8 @@ def _worker(rank, world, port, case, q):
     (2, (4, 4, 3, "allreduce", 100.0, 50.0, "distributed", True)),
     (2, (4, 4, 3, "p2p", 200.0, 100.0, "central", False)),
     (3, (4, 6, 3, "allreduce", 50.0, 20.0, "distributed", False)),
+    # cfg5's world size: 8 ranks over 9 element columns (strips 2, 1, ..., 1), the distributed update
+    (8, (4, 9, 2, "allreduce", 50.0, 20.0, "distributed", False)),
 ])
 def test_partitioned_ns_solver_gloo(world, case):
     ctx = mp.get_context("spawn")

@@ -1,4 +1,4 @@
-"""World-size 1/2/3 gloo tests (CPU) of the element-partitioned condensed direct solve
+"""World-size 1/2/3/8 gloo tests (CPU) of the element-partitioned condensed direct solve
 (sem_amd/solvers/strip_solve.py, StripLineSolver): each rank factors its strip's pieces -- the oracle
 Jacobian's (NavierStokes_Solver.py:176-183, or the CD operator ConvectionDiffusion_Solver.py:104-121),
 restricted to the strip, a shared interface line's own block held by its right owner -- eliminates its
@@ -86,6 +86,10 @@ def _worker(rank, world, port, case, q):
     (2, (3, 2, 4, 100.0, 2, True)),     # one column per strip: no interior line; block-LU edge inverses
     (3, (4, 7, 2, 700.0, 2, False)),    # uneven strips (3, 2, 2 columns)
     (3, (5, 6, 3, 40.0, 1, False)),     # the one-component (CD) operator
+    # cfg5's world size: 8 ranks over 11 columns (strips of 2, 2, 2, 1, 1, 1, 1, 1 columns:
+    # uneven, one-column strips with no interior line), and the CD operator over 9 columns (2, 1 x 7)
+    (8, (4, 11, 2, 300.0, 2, False)),
+    (8, (3, 9, 3, 40.0, 1, True)),
 ])
 def test_strip_line_solver_gloo(world, case):
     ctx = mp.get_context("spawn")

@@ -139,7 +139,8 @@ def test_scalar_blocks_and_solve_match_oracle_cd_jacobian(gpu, P, nex, ney, Pe):
 
 
 @pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 2, 100.0), (8, 4, 4, 1000.0), (5, 3, 6, 250.0), (2, 7, 2, 300.0),
-                                           (12, 3, 2, 1000.0), (12, 2, 5, 100.0)])
+                                           (12, 3, 2, 1000.0), (12, 2, 5, 100.0),
+                                           (16, 2, 3, 300.0), (7, 2, 2, 100.0), (3, 3, 4, 50.0)])
 def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     """sem_nested_solve + sem_interface_rhs (ns_condense.hip) against the torch formulation of the
     same condensation, for the velocity pair and the one-component CD Jacobian."""

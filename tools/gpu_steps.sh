@@ -28,6 +28,7 @@ for s in "$@"; do
     cfg4)       step cfg4 300 $PYT -s tests/test_gpu_cfg4.py ;;
     nsapply)    step nsapply 300 $PYT tests/test_gpu_ns_apply.py ;;
     velocity)   step velocity 600 $PYT tests/test_gpu_ns_velocity.py ;;
+    batchedinv) step batchedinv 300 $PYT tests/test_batched_inverse.py tests/test_gpu_dense_inverse.py ;;
     smoke)      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)      step bench 600 python bench.py ;;
     inv)        step inv 300 python tools/inv_repro.py ;;
@@ -35,7 +36,7 @@ for s in "$@"; do
     pivot)      step pivot 300 python tools/pivot_probe.py ;;
     gemvprobe)  step gemvprobe 300 python tools/gemv_probe.py ;;
     dist)       step dist 900 $PYT tests/test_gpu_dist.py -k "not cfg5_element_partitioned_ns_update" ;;
-    distcfg5)   SEM_SLOW_GPU_TESTS=1 step distcfg5 900 $PYT -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
+    distcfg5)   SEM_SLOW_GPU_TESTS=1 step distcfg5 1000 ${PYT/--timeout 300/--timeout 900} -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
     cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5factor_inv) SEM_PIVOT_INV=inv SEM_PROFILE_FACTOR=1 step cfg5factor_inv 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5ns)     SEM_PROFILE_FACTOR=1 step cfg5ns 900 python tools/cfg5_ns_probe.py ;;
@@ -56,6 +57,15 @@ for s in "$@"; do
       step cfg5trace 900 rocprofv3 --kernel-trace --stats -d "$O/cfg5trace" -o trace --output-format csv -- \
         python tools/cfg5_ns_probe.py --update 0
       python tools/pmc_compact.py "$O/cfg5trace" && python tools/prof_summary.py "$O/cfg5trace" "" > "$O/cfg5trace/prof_summary.txt" ;;
+    vsolve)     step vsolve 600 python tools/vsolve_probe.py --out "$O/vsolve.json" ;;
+    vsolvetrace)  # kernel trace of one factor + the A/B + 20 solves; FETCH_SIZE / WRITE_SIZE passes of their own
+      step vsolvetrace 900 rocprofv3 --kernel-trace --stats -d "$O/vsolvetrace" -o trace --output-format csv -- \
+        python tools/vsolve_probe.py --out "$O/vsolvetrace.json"
+      TAILN=40 step vsolve_window 120 python tools/trace_window.py "$O/vsolvetrace" 20 cond_fwd_kernel 2
+      step vsolve_fetch 600 timeout -s KILL 580 rocprofv3 --pmc FETCH_SIZE -d "$O/vsolve_pmc1" -o pmc --output-format csv -- \
+        python tools/vsolve_probe.py --ab-edge 0
+      step vsolve_write 600 timeout -s KILL 580 rocprofv3 --pmc WRITE_SIZE -d "$O/vsolve_pmc2" -o pmc --output-format csv -- \
+        python tools/vsolve_probe.py --ab-edge 0 ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
     benchtrace)

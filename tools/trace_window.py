@@ -7,11 +7,15 @@ python tools/trace_window.py <trace_kernel_trace.csv> [reps] [marker] [per_rep]
 """
 import collections
 import csv
+import glob
+import os
 import sys
 
 
 def main():
     path = sys.argv[1]
+    if os.path.isdir(path):   # a rocprofv3 -d directory: its kernel trace
+        path = sorted(glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True))[0]
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     marker = sys.argv[3] if len(sys.argv) > 3 else "ns_apply"
     per_rep = int(sys.argv[4]) if len(sys.argv) > 4 else 2
