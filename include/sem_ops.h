@@ -330,6 +330,15 @@ int sem_interface_rhs(int P, int nex, int m, const double* B, int64_t ld_b, cons
 int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* src, const int64_t* ld_src,
                    const int64_t* xrow, double* y, int64_t ld_y, const int64_t* yrow, int accumulate, void* stream);
 
+/* ---- streaming row-major GEMV (the block-Thomas interface sweep) -------- */
+/* y = alpha A x + beta y (beta = 0: y is not read) for a row-major M x K operator (row i at A + i lda):
+ * one forward ([D^-1 | -D^-1 S_lo], m x 2m) or back (D^-1 S_up, m x m) step of the block-Thomas sweep of
+ * the condensed velocity solve (sem_amd/solvers/velocity_solve.py fused_thomas_solve), which replaces the
+ * reference's SuperLU triangular solves (NavierStokes_Solver.py:189-203).  Deterministic (fixed summation
+ * order).  Device pointers; y must not overlap A or x.  Stream-ordered.  (ABI 10) */
+int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, const double* x, double beta, double* y,
+                  void* stream);
+
 /* ---- small dense inverse (leaves of the sweep's pivot inverses) --------- */
 /* X = A^-1 for one n x n row-major block, n <= 64 (row r of A at A + r lda, of X at X + r ldx; device
  * memory; X must not overlap A): Gauss-Jordan elimination with partial pivoting in one workgroup (ABI 8).

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsemops.so")
+LIB_PATH = os.path.join(os.environ.get("SEM_LIBDIR") or os.path.join(_HERE, "lib"), "libsemops.so")
 
 ABI_VERSION = 10
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
@@ -105,6 +105,8 @@ _SIGS = {
     "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,
                                  C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p]),
     "sem_dense_inverse_small": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_void_p]),
+    "sem_gemv_rows": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_int64, C.c_void_p, C.c_double,
+                                C.c_void_p, C.c_void_p]),
 }
 
 _lib = None

@@ -11,7 +11,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-LIBDIR = os.path.join(HERE, "lib")
+# SEM_LIBDIR: another in-tree output directory (e.g. sem_amd/lib_diag for a diagnostic build beside the
+# release one, tools/kbench.py ablations); default sem_amd/lib
+LIBDIR = os.environ.get("SEM_LIBDIR") or os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libsemops.so")
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 

@@ -145,6 +145,30 @@ __device__ __forceinline__ void contract_generic(const double* Kt, const double*
   }
 }
 
+// The same with the staged nodes read through get(l), l = -P..P relative to the element's node 0 (a
+// swizzled LDS tile, apply_tp_mfma).
+template <int P, typename Get>
+__device__ __forceinline__ void contract_generic_f(const double* Kt, const double* Gt, Get get, int row, bool hasR,
+                                                   bool hasL, double& k, double& g) {
+  constexpr int n = P + 1;
+  k = 0.0;
+  g = 0.0;
+  if (row == 0 && hasL) {
+    for (int l = 0; l <= P; ++l) {
+      const double t = get(l - P);
+      k = fma(Kt[P * n + l], t, k);
+      g = fma(Gt[P * n + l], t, g);
+    }
+  }
+  if (hasR) {
+    for (int l = 0; l <= P; ++l) {
+      const double t = get(l);
+      k = fma(Kt[row * n + l], t, k);
+      g = fma(Gt[row * n + l], t, g);
+    }
+  }
+}
+
 // Buffer resource over `bytes` bytes at p (wave-uniform inputs only).  Loads at offsets outside
 // [0, bytes) -- including "negative" offsets, which wrap to huge unsigned values -- return 0
 // without touching memory, so halo staging needs no clamps.

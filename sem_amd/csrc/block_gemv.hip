@@ -109,9 +109,124 @@ __global__ __launch_bounds__(64 * kGemvWaves) void block_gemv_narrow_kernel(cons
   }
 }
 
+// ---- Streaming row-major GEMV (round 4): y = alpha A x + beta y, A (M x K) row-major, one operator read
+// once per call -- the block-Thomas interface sweep of the cfg5 velocity solve (one m x 2m forward operator
+// [D^-1 | -D^-1 S_lo] and one m x m back operator per interface line, 29 GB per solve).  rocBLAS's gemvt
+// streamed them at 3.6 TB/s there (8.1 ms of a 12.4 ms solve, profiles/r04/cfg5_vsolve/); its 5.7 TB/s in
+// tools/gemv_probe.py came from repeating one 151 MB operator out of the 256 MB MALL.
+// Workgroup = kRowsWG rows x 4 waves; wave w takes the K-quarter w of all of them, so one 16-byte x load
+// (two doubles per lane) feeds kRowsWG 16-byte row loads, and kSweepUnroll iterations of those loads are
+// issued before their FMAs (~20 KB in flight per wave).  Lane partials -> wave sum -> the four waves' sums
+// in LDS in wave order: deterministic.  VEC = false: an unaligned operand, 8-byte loads.
+constexpr int kRowsWG = 4;
+constexpr int kSweepUnroll = 4;
+
+struct RowGemvArgs {
+  const double* A;
+  const double* x;
+  double* y;
+  int64_t lda;
+  double alpha, beta;
+  int M, K;
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemvArgs a) {
+  __shared__ double part[4][kRowsWG];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * kRowsWG;
+  // the wave's K range, in units of 2 doubles (VEC) or 1
+  constexpr int W = VEC ? 2 : 1;
+  const int KU = (a.K + W - 1) / W;
+  const int kb = static_cast<int>(static_cast<int64_t>(KU) * wave / 4), ke = static_cast<int>(static_cast<int64_t>(KU) * (wave + 1) / 4);
+  const double* rows[kRowsWG];
+#pragma unroll
+  for (int i = 0; i < kRowsWG; ++i) rows[i] = a.A + static_cast<int64_t>(min(r0 + i, a.M - 1)) * a.lda;  // clamped rows: not stored
+  double acc[kRowsWG][2] = {};
+  int u = kb + lane;
+  if constexpr (VEC) {  // K even: every pair holds two columns
+    // main loop: kSweepUnroll pairs per lane per iteration, every load issued before the FMAs
+    for (; u + 64 * (kSweepUnroll - 1) < ke; u += 64 * kSweepUnroll) {
+      double2 xv[kSweepUnroll], av[kSweepUnroll][kRowsWG];
+#pragma unroll
+      for (int t = 0; t < kSweepUnroll; ++t) {
+        xv[t] = *reinterpret_cast<const double2*>(a.x + 2 * (u + 64 * t));
+#pragma unroll
+        for (int i = 0; i < kRowsWG; ++i) av[t][i] = *reinterpret_cast<const double2*>(rows[i] + 2 * (u + 64 * t));
+      }
+#pragma unroll
+      for (int t = 0; t < kSweepUnroll; ++t)
+#pragma unroll
+        for (int i = 0; i < kRowsWG; ++i) {
+          acc[i][0] = fma(av[t][i].x, xv[t].x, acc[i][0]);
+          acc[i][1] = fma(av[t][i].y, xv[t].y, acc[i][1]);
+        }
+    }
+    for (; u < ke; u += 64) {
+      const double2 xv = *reinterpret_cast<const double2*>(a.x + 2 * u);
+#pragma unroll
+      for (int i = 0; i < kRowsWG; ++i) {
+        const double2 av = *reinterpret_cast<const double2*>(rows[i] + 2 * u);
+        acc[i][0] = fma(av.x, xv.x, acc[i][0]);
+        acc[i][1] = fma(av.y, xv.y, acc[i][1]);
+      }
+    }
+  } else {
+    for (; u + 64 * (kSweepUnroll - 1) < ke; u += 64 * kSweepUnroll) {
+      double xv[kSweepUnroll], av[kSweepUnroll][kRowsWG];
+#pragma unroll
+      for (int t = 0; t < kSweepUnroll; ++t) {
+        xv[t] = a.x[u + 64 * t];
+#pragma unroll
+        for (int i = 0; i < kRowsWG; ++i) av[t][i] = rows[i][u + 64 * t];
+      }
+#pragma unroll
+      for (int t = 0; t < kSweepUnroll; ++t)
+#pragma unroll
+        for (int i = 0; i < kRowsWG; ++i) acc[i][t & 1] = fma(av[t][i], xv[t], acc[i][t & 1]);
+    }
+    for (; u < ke; u += 64) {
+      const double xv = a.x[u];
+#pragma unroll
+      for (int i = 0; i < kRowsWG; ++i) acc[i][0] = fma(rows[i][u], xv, acc[i][0]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kRowsWG; ++i) {
+    const double v = wave_sum(acc[i][0] + acc[i][1]);
+    if (lane == 0) part[wave][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kRowsWG && r0 + static_cast<int>(threadIdx.x) < a.M) {
+    const int i = threadIdx.x;
+    const double v = a.alpha * (((part[0][i] + part[1][i]) + part[2][i]) + part[3][i]);
+    double* yp = a.y + r0 + i;
+    *yp = a.beta == 0.0 ? v : fma(a.beta, *yp, v);
+  }
+}
+
 }  // namespace sem
 
 extern "C" {
+
+int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, const double* x, double beta, double* y,
+                  void* stream) {
+  if (M < 0 || K < 0 || lda < K) return sem::set_error(SEM_EINVAL, "gemv_rows: bad sizes");
+  if (M == 0) return SEM_OK;
+  if (!A || !x || !y) return sem::set_error(SEM_EINVAL, "gemv_rows: null argument");
+  sem::RowGemvArgs a{A, x, y, lda, alpha, beta, M, K};
+  const bool vec = (reinterpret_cast<uintptr_t>(A) % 16) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
+                   (lda % 2) == 0 && (K % 2) == 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((M + sem::kRowsWG - 1) / sem::kRowsWG), block(256);
+  if (vec)
+    hipLaunchKernelGGL(sem::row_gemv_kernel<true>, grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL(sem::row_gemv_kernel<false>, grid, block, 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("gemv_rows launch: ") + hipGetErrorString(e));
+  return SEM_OK;
+}
 
 int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* src, const int64_t* ld_src,
                    const int64_t* xrow, double* y, int64_t ld_y, const int64_t* yrow, int accumulate, void* stream) {

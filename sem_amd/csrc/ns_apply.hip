@@ -260,7 +260,11 @@ struct NsBand {
   // ds_write_b64 in four 16-lane groups) bank-conflict free (P = 4, 8, 12, 16 exactly; counted per order
   // with the LDS banking of MI355X_MICROARCH.md); element fastest for the orders where it conflicts less.
   static constexpr bool RF = !(P == 3 || P == 6 || P == 7 || P == 10);
-  static constexpr int SCP = BY | 1;          // odd pitch of the staged cv lines
+  // pitch of the staged cv lines: the staged fields' PIT, so the Y phase's cv reads r SCP + b P + j have the
+  // bank pattern of its window reads (P + r) PIT + b P + q, conflict-free for the RF orders (round 4: BY | 1
+  // made them 2-way at P = 12, ~80 k of the 108 k conflict cycles per cfg5 Jacobian launch,
+  // profiles/r03/ns_lds/pmc_ns128_kernarg_reload.txt)
+  static constexpr int SCP = PIT;
   static __device__ __forceinline__ int yline(int lane) { return RF ? lane % P : lane / TYE; }
   static __device__ __forceinline__ int yelem(int lane) { return RF ? lane / P : lane % TYE; }
   static constexpr int rows(int w) { return w < P ? (P - 1 - w) / NW + 1 : 0; }

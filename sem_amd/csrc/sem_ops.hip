@@ -271,9 +271,8 @@ static int launch_apply(const ApplyArgs& args_in, const sem_handle* h, hipStream
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int pitch18(int w) { return w + ((18 - (w % 32)) + 32) % 32; }  // >= w, == 18 (mod 32)
 
-template <int P, int TX_, int TY_, int NW_, bool SPLIT_>
+template <int P, int TX_, int TY_, int NW_, bool SPLIT_, bool SWZ_ = true>
 struct MCfg {
   static constexpr int n = P + 1, TX = TX_, TY = TY_, NW = NW_, THREADS = 64 * NW_;
   static constexpr bool SPLIT = SPLIT_;                   // K and G chains as separate wave tasks
@@ -282,14 +281,30 @@ struct MCfg {
   static constexpr int KS = (n + 3) / 4;                  // k-steps of 4
   static constexpr int RX = cmax(TX * P + 4 * KS, P + 16 * NLB);    // staged lines from gx0-P
   static constexpr int RY = cmax(TY * P + 4 * KS, P + 16 * NCB);    // staged columns from gy0-P
-  static constexpr int PT = pitch18(RY);
+  // Staged tile layout (round 4, bank-conflict-free; tools/lds_banks_mfma.py): rows of R16 = RY rounded up to
+  // 16 slots, pitch PT == 16 (mod 32) doubles, column c of row r at c ^ 2 ((r >> 1) & 7) (a permutation inside
+  // each aligned 16-column block).  Phase A reads two rows x 16 columns per 32-lane group: PT puts the rows in
+  // opposite bank halves.  Phase B reads 16 rows x 2 columns: the swizzle spreads the rows of each parity over
+  // 8 distinct 2-double bank slots.  Staging stores one aligned 16-column run per 16-lane group.  (pitch18 with
+  // row-major staging had 2-way conflicts in phase A, staging and the epilogue: 95,488 conflict cycles per cfg2
+  // dispatch, profiles/r03/mfma64/.)
+  // SWZ = false (the persistent large-tile variants, where the swizzle's address arithmetic spilled VGPRs):
+  // the round-3 layout, row-major staging at pitch == 18 (mod 32).
+  static constexpr bool SWZ = SWZ_;
+  static constexpr int R16 = (RY + 15) / 16 * 16;
+  static constexpr int PT = SWZ ? R16 + ((16 - R16 % 32) + 32) % 32 : RY + ((18 - (RY % 32)) + 32) % 32;
+  __host__ __device__ static constexpr int ts(int r, int c) { return r * PT + (SWZ ? c ^ (((r >> 1) & 7) << 1) : c); }
   static constexpr int EC = 16 * NCB;   // E (x-results) column pitch
   static constexpr int FL = 16 * NLB;   // F (y-results) lines per element row
   static constexpr int TA = (TX + 1) * NCB, TB = (TY + 1) * NLB;
   static constexpr int NWA = NW > 1 ? NW / 2 : 1;         // waves running phase A (the rest: phase B)
   static_assert(NW >= 2, "phase A and B run on separate waves");
   static constexpr int MAXG = 4;                          // tasks batched per wave (register bound)
-  static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
+  // staging slots per row: R16 when that costs no extra staging register, else the unpadded RY (the
+  // large-tile persistent variants, whose prefetched next tile would spill)
+  static constexpr int SR =
+      SWZ && (RX * R16 + THREADS - 1) / THREADS == (RX * RY + THREADS - 1) / THREADS ? R16 : RY;
+  static constexpr int NSTAGE = (RX * SR + THREADS - 1) / THREADS;
   static constexpr int NMAIN = (BX * BY + THREADS - 1) / THREADS;  // epilogue nodes per thread
   static_assert(n <= 16, "MFMA path needs P+1 <= 16");
 };
@@ -306,7 +321,7 @@ struct MSmem {
 
 template <int P, int TX, int TY, int NW, bool PERSIST, bool SPLIT>
 __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void apply_tp_mfma(const ApplyArgs a) {
-  using C = MCfg<P, TX, TY, NW, SPLIT>;
+  using C = MCfg<P, TX, TY, NW, SPLIT, !PERSIST>;
   constexpr int n = C::n;
   __shared__ MSmem<C> sm;
 
@@ -334,8 +349,8 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
 #pragma unroll
   for (int s = 0; s < C::NSTAGE; ++s) {
     const int idx = tid + s * C::THREADS;
-    const int rr = idx / C::RY, cc = idx - rr * C::RY;
-    soff[s] = (rr * NY + cc) * 8;
+    const int rr = idx / C::SR, cc = idx - rr * C::SR;
+    soff[s] = rr < C::RX && cc < C::RY ? (rr * NY + cc) * 8 : -(1 << 30);  // padding slots: no memory touched
   }
 #pragma unroll
   for (int qn = 0; qn < C::NMAIN; ++qn) {
@@ -391,10 +406,8 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
 #pragma unroll
     for (int s = 0; s < C::NSTAGE; ++s) {
       const int idx = tid + s * C::THREADS;
-      if ((s + 1) * C::THREADS <= C::RX * C::RY || idx < C::RX * C::RY) {
-        const int rr = idx / C::RY, cc = idx - rr * C::RY;
-        sm.Ts[rr * C::PT + cc] = st[s];
-      }
+      const int rr = idx / C::SR, cc = idx - rr * C::SR;
+      if (rr < C::RX && cc < C::RY) sm.Ts[C::ts(rr, cc)] = st[s];
     }
     if (!ws_done) {
       if (tid < n) sm.ws[tid] = wreg;
@@ -428,7 +441,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
 #pragma unroll
             for (int s = 0; s < C::KS; ++s) {
               const int k = 4 * s + lk;
-              const double v = sm.Ts[(e * P + k) * C::PT + P + cb * 16 + lr];
+              const double v = sm.Ts[C::ts(e * P + k, P + cb * 16 + lr)];
               bv[tt][s] = (4 * s + 3 > P && k > P) ? 0.0 : v;  // next element's nodes: keep NaN/Inf out
             }
           }
@@ -471,7 +484,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
 #pragma unroll
             for (int s = 0; s < C::KS; ++s) {
               const int k = 4 * s + lk;
-              const double v = sm.Ts[(P + lbk * 16 + lr) * C::PT + e * P + k];
+              const double v = sm.Ts[C::ts(P + lbk * 16 + lr, e * P + k)];
               av[tt][s] = (4 * s + 3 > P && k > P) ? 0.0 : v;
             }
           }
@@ -520,7 +533,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
       const int off = nbase + noff[qn];
       const int i = rl % P, ex = rl / P, j = c % P, ey = c / P;
       const bool hasLx = i == 0 && (ex > 0 || leftx), hasLy = j == 0 && (ey > 0 || lefty);
-      const double xv = sm.Ts[(P + rl) * C::PT + P + c];
+      const double xv = sm.Ts[C::ts(P + rl, P + c)];
       const double kl = sm.EK[(ex * n + P) * C::EC + c], gl = sm.EG[(ex * n + P) * C::EC + c];
       const double kr = sm.EK[((ex + 1) * n + i) * C::EC + c], gr = sm.EG[((ex + 1) * n + i) * C::EC + c];
       const double fkl = sm.FK[(ey * C::FL + rl) * n + P], fgl = sm.FG[(ey * C::FL + rl) * n + P];
@@ -557,7 +570,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
         const int gx = gx0 + rl, gy = gy0 + c;
         const int p = (gx - lb0) * NY + gy;
         const double uu = a.cu ? a.cu[p] : 1.0, vv = a.cv ? a.cv[p] : 1.0;
-        const double xv = sm.Ts[(P + rl) * C::PT + P + c];
+        const double xv = sm.Ts[C::ts(P + rl, P + c)];
         if (kDiag && (a.diag & 2)) {
           a.y[p] = xv * uu + vv;
           return;
@@ -576,8 +589,8 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
             XG += sm.EG[((ex + 1) * n + i) * C::EC + c];
           }
         } else {
-          contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl - i) * C::PT + P + c], C::PT, i, hasR, hasLx, XK,
-                              XG);
+          contract_generic_f<P>(a.tab, a.tab + n * n, [&](int l) { return sm.Ts[C::ts(P + rl - i + l, P + c)]; }, i,
+                                hasR, hasLx, XK, XG);
         }
         const int j = c % P, ey = c / P;
         const int nR = n0 + ey;
@@ -593,8 +606,8 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
             YG += sm.FG[((ey + 1) * C::FL + rl) * n + j];
           }
         } else {
-          contract_generic<P>(a.tab, a.tab + n * n, &sm.Ts[(P + rl) * C::PT + P + c - j], 1, j, hasRy, hasLy, YK,
-                              YG);
+          contract_generic_f<P>(a.tab, a.tab + n * n, [&](int l) { return sm.Ts[C::ts(P + rl, P + c - j + l)]; }, j,
+                                hasRy, hasLy, YK, YG);
         }
         const double mx = wsum<P>(gx, a.ex_begin, a.ex_end, sm.ws);
         const double my = wsum<P>(gy, 0, a.ney, sm.ws);
@@ -634,7 +647,7 @@ __global__ __launch_bounds__(64 * NW, PERSIST ? 2 : (NW >= 4 ? 4 : 2)) void appl
 
 template <int P, int TX, int TY, int NW, bool PERSIST, bool SPLIT>
 static int launch_apply_mfma(const ApplyArgs& args_in, const sem_handle* h, hipStream_t s) {
-  using C = MCfg<P, TX, TY, NW, SPLIT>;
+  using C = MCfg<P, TX, TY, NW, SPLIT, !PERSIST>;
   ApplyArgs args = args_in;
   const int ncols = h->ex_end - h->ex_begin;
   args.tiles_x = (ncols + TX - 1) / TX;

@@ -351,10 +351,12 @@ class NavierStokesSolver:
         part.assemble(c0)
         b_schur = rc - c0
         count = [0]
+        if self._schur is None:
+            self._schur = _StripSchur(self, vs, graph=self._velocity_graph)
 
         def schur_mv(dp):
             count[0] += 1
-            return self._schur_strips(vs, dp)
+            return self._schur(dp)
 
         pin = self._pin_local
 
@@ -547,6 +549,63 @@ class NavierStokesSolver:
         u, v, p = self._get_solution(T)
         return self._get_interpol(u, points_plot), self._get_interpol(v, points_plot), self._get_interpol(p,
                                                                                                          points_plot)
+
+
+class _StripSchur:
+    """The strip-partitioned Schur-complement operator (_schur_strips: gradient launch + interface assembly,
+    the element-partitioned velocity solve with its all-gather, divergence launch + assembly).  Under RCCL
+    every step stays on the device (collectives included), so the whole matvec is captured in one hipGraph
+    per linearisation, as the whole-mesh _SchurComplement is; the capture is used only after its replay has
+    reproduced the eager matvec on a probe vector, and every rank takes the same decision.  Under gloo (the
+    CPU rehearsal, host-staged collectives) the matvec stays eager."""
+
+    def __init__(self, ns, vs, graph=True):
+        self.ns, self.vs = ns, vs
+        m, part = ns._mesh, ns._part
+        self._graph = None
+        if graph and m.device.type == "cuda" and part.backend_device().type == "cuda":
+            self._capture()
+
+    def _capture(self):
+        ns, m, part = self.ns, self.ns._mesh, self.ns._part
+        dev = m.device
+        g0 = torch.Generator(device=dev).manual_seed(5)
+        probe = torch.rand(m.n_local, dtype=torch.float64, device=dev, generator=g0)
+        self._x = torch.zeros_like(probe)
+        cur = torch.cuda.current_stream(dev)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            want = ns._schur_strips(self.vs, probe)   # warm-up outside the capture (workspaces, communicators)
+        cur.wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        try:   # a capture executes no collective, so a rank whose capture fails cannot desynchronise the others
+            with no_gc(), torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._out = ns._schur_strips(self.vs, self._x)
+            ok = 1.0
+        except RuntimeError:
+            torch.cuda.synchronize(dev)
+            ok = 0.0
+        if self._agree(ok):    # every rank captured: replay (its collectives need every rank) and compare
+            self._x.copy_(probe)
+            g.replay()
+            err = (self._out - want).abs().max() / want.abs().max().clamp(min=1e-300)
+            if self._agree(1.0 if bool(err <= 1e-12) else 0.0):
+                self._graph = g
+
+    def _agree(self, ok):
+        """True when every rank reports ok (one all-reduce)."""
+        part = self.ns._part
+        flag = torch.tensor([ok], dtype=torch.float64, device=self.ns._mesh.device)
+        part.dist.all_reduce(flag, op=part.dist.ReduceOp.MIN, group=part.group)
+        return float(flag.item()) == 1.0
+
+    def __call__(self, dp):
+        if self._graph is None:
+            return self.ns._schur_strips(self.vs, dp)
+        self._x.copy_(dp)
+        self._graph.replay()
+        return self._out.clone()
 
 
 class _SchurComplement:

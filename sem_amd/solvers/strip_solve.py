@@ -154,19 +154,25 @@ class StripLineSolver(VelocityJacobianSolver):
         Under RCCL the captured graph is checked against the eager solve before it is used."""
         if self.G > 1 and self.gather_device.type != "cuda":
             return False
-        if not super().capture():
-            return False
+        captured = super().capture()       # a capture executes no collective: a failure desynchronises no rank
         if self.G == 1:
-            return True
+            return captured
+        if not self._agree(captured):
+            self._graph = None
+            return False
         g = torch.Generator(device=self.device).manual_seed(11)
         b = torch.rand(self._bin.shape, dtype=torch.float64, device=self.device, generator=g)
         want = self._solve_lines(b.clone())
         self._bin.copy_(b)
-        self._graph.replay()
+        self._graph.replay()           # every rank replays: its all-gather needs every rank
         err = (self._xout - want).abs().max() / want.abs().max().clamp(min=1e-300)
-        ok = torch.tensor([1.0 if bool(err <= 1e-12) else 0.0], dtype=torch.float64, device=self.device)
-        self.dist.all_reduce(ok, op=self.dist.ReduceOp.MIN, group=self.group)
-        if float(ok.item()) < 1.0:     # every rank takes the same decision
+        if not self._agree(bool(err <= 1e-12)):
             self._graph = None
             return False
         return True
+
+    def _agree(self, ok):
+        """True when every rank reports ok (one all-reduce; every rank takes the same decision)."""
+        flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=self.gather_device)
+        self.dist.all_reduce(flag, op=self.dist.ReduceOp.MIN, group=self.group)
+        return float(flag.item()) == 1.0

@@ -189,6 +189,30 @@ def fused_thomas_operators(Dinv, S_lo, Uh):
     return Dinv[0].clone(), F, Uh
 
 
+_SWEEP_GEMV = os.environ.get("SEM_SWEEP_GEMV", "hip")   # "hip": sem_gemv_rows; "torch": rocBLAS (A/B)
+
+
+def _gemv(A, x, y, alpha=1.0, beta=0.0):
+    """y = alpha A x + beta y for a row-major operator: the library's streaming GEMV on the GPU
+    (sem_gemv_rows: 5+ TB/s on operators read once, where rocBLAS's gemvt streamed 3.6), torch elsewhere."""
+    if A.is_cuda and _SWEEP_GEMV == "hip" and A.dtype == torch.float64 and A.stride(1) == 1 and x.stride(0) == 1 \
+            and y.stride(0) == 1:
+        import ctypes as C
+        from .. import _lib
+        lib = _lib.load()
+        _lib.check(lib.sem_gemv_rows(A.shape[0], A.shape[1], alpha, C.c_void_p(A.data_ptr()), A.stride(0),
+                                     C.c_void_p(x.data_ptr()), beta, C.c_void_p(y.data_ptr()),
+                                     C.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)))
+        return y
+    if beta == 0.0:
+        torch.mv(A, x, out=y)
+        if alpha != 1.0:
+            y.mul_(alpha)
+    else:
+        y.mul_(beta).addmv_(A, x, alpha=alpha)
+    return y
+
+
 def fused_thomas_solve(D0, F, Uh, g):
     """x = S^-1 g from fused_thomas_operators (g: (n, m), not modified).  W[L] = [g_L | z_{L-1}]: the
     forward GEMV of line L reads one contiguous 2m vector and writes z_L straight into W[L+1]'s second
@@ -196,12 +220,12 @@ def fused_thomas_solve(D0, F, Uh, g):
     n, m = g.shape[0], g.shape[1]
     W = torch.empty((n + 1, 2 * m), dtype=g.dtype, device=g.device)
     W[:n, :m] = g
-    torch.mv(D0, g[0], out=W[1, m:])
+    _gemv(D0, g[0], W[1, m:])
     for L in range(1, n):
-        torch.mv(F[L - 1], W[L], out=W[L + 1, m:])
+        _gemv(F[L - 1], W[L], W[L + 1, m:])
     z = W[1:, m:]                       # z_L at row L
     for L in range(n - 2, -1, -1):
-        z[L].addmv_(Uh[L], z[L + 1], alpha=-1.0)
+        _gemv(Uh[L], z[L + 1], z[L], alpha=-1.0, beta=1.0)
     return z.contiguous()             # sem_nested_solve reads x_B as a packed (n, m) array
 
 

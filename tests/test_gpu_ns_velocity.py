@@ -168,6 +168,36 @@ def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     assert err <= 1e-10, err
 
 
+@pytest.mark.parametrize("M,K,lda,alpha,beta", [(3074, 6148, 6148, 1.0, 0.0), (3074, 3074, 3074, -1.0, 1.0),
+                                               (1537, 3074, 3074, 1.0, 0.0), (1537, 1537, 1537, -1.0, 1.0),
+                                               (5, 7, 9, 0.5, -2.0), (1, 1, 1, 1.0, 0.0), (13, 130, 131, 2.0, 0.0),
+                                               (770, 1540, 1600, -1.0, 1.0)])
+def test_gemv_rows_matches_torch(gpu, M, K, lda, alpha, beta):
+    """sem_gemv_rows (the block-Thomas sweep's streaming GEMV): both load widths (16-byte for even K / lda
+    and aligned operands, 8-byte otherwise), row counts not a multiple of the workgroup's 4, alpha / beta,
+    a leading dimension wider than K; beta = 0 must not read y (NaN there)."""
+    import ctypes as C
+    from sem_amd import _lib
+    lib = _lib.load()
+    dev = torch.device("cuda")
+    r = np.random.default_rng(M + K)
+    A = torch.as_tensor(r.uniform(-1, 1, (M, lda)), device=dev)
+    x = torch.as_tensor(r.uniform(-1, 1, K), device=dev)
+    y0 = torch.as_tensor(r.uniform(-1, 1, M), device=dev)
+    y = torch.full_like(y0, float("nan")) if beta == 0.0 else y0.clone()
+    want = alpha * (A[:, :K] @ x) + (beta * y0 if beta != 0.0 else 0.0)
+    P_ = C.c_void_p
+    _lib.check(lib.sem_gemv_rows(M, K, alpha, P_(A.data_ptr()), lda, P_(x.data_ptr()), beta, P_(y.data_ptr()),
+                                 P_(torch.cuda.current_stream().cuda_stream)))
+    assert torch.isfinite(y).all()
+    assert (y - want).abs().max().item() <= 1e-13 * max(1.0, want.abs().max().item()) * np.sqrt(K)
+    # deterministic: a second call gives the same bits
+    y2 = torch.full_like(y0, float("nan")) if beta == 0.0 else y0.clone()
+    _lib.check(lib.sem_gemv_rows(M, K, alpha, P_(A.data_ptr()), lda, P_(x.data_ptr()), beta, P_(y2.data_ptr()),
+                                 P_(torch.cuda.current_stream().cuda_stream)))
+    assert torch.equal(y, y2)
+
+
 @pytest.mark.parametrize("nb,m,S", [(1, 770, 3), (2, 385, 2), (40, 200, 3), (24, 770, 2), (3, 17, 1), (5, 1537, 3),
                                     (4, 1537, 2), (1, 2730, 3)])
 def test_block_gemv_wide_and_narrow(gpu, nb, m, S):

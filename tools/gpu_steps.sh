@@ -28,6 +28,8 @@ for s in "$@"; do
     cfg4)       step cfg4 300 $PYT -s tests/test_gpu_cfg4.py ;;
     nsapply)    step nsapply 300 $PYT tests/test_gpu_ns_apply.py ;;
     velocity)   step velocity 600 $PYT tests/test_gpu_ns_velocity.py ;;
+    mfmatest)   step mfmatest 600 $PYT tests/test_gpu_apply.py ;;
+    mfmapmc)    tools/pmc_run.sh "$O/pmc_mfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1 ;;
     batchedinv) step batchedinv 300 $PYT tests/test_batched_inverse.py tests/test_gpu_dense_inverse.py ;;
     smoke)      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)      step bench 600 python bench.py ;;
@@ -58,14 +60,29 @@ for s in "$@"; do
         python tools/cfg5_ns_probe.py --update 0
       python tools/pmc_compact.py "$O/cfg5trace" && python tools/prof_summary.py "$O/cfg5trace" "" > "$O/cfg5trace/prof_summary.txt" ;;
     vsolve)     step vsolve 600 python tools/vsolve_probe.py --out "$O/vsolve.json" ;;
+    vsolveab)   # interface-sweep GEMV A/B: the library's streaming GEMV (default) against rocBLAS, one process each
+      SEM_SWEEP_GEMV=torch TAILN=2 step vsolve_rocblas 600 python tools/vsolve_probe.py --ab-edge 0 --out "$O/vsolve_rocblas.json"
+      TAILN=2 step vsolve_hip 600 python tools/vsolve_probe.py --ab-edge 1 --out "$O/vsolve_hip.json" ;;
     vsolvetrace)  # kernel trace of one factor + the A/B + 20 solves; FETCH_SIZE / WRITE_SIZE passes of their own
       step vsolvetrace 900 rocprofv3 --kernel-trace --stats -d "$O/vsolvetrace" -o trace --output-format csv -- \
         python tools/vsolve_probe.py --out "$O/vsolvetrace.json"
-      TAILN=40 step vsolve_window 120 python tools/trace_window.py "$O/vsolvetrace" 20 cond_fwd_kernel 2
+      TAILN=40 step vsolve_window 120 python tools/trace_window.py "$O/vsolvetrace" 20 cond_fwd_kernel 2 \
+        --save "$O/vsolvetrace/window_20_solves.csv"
+      find "$O/vsolvetrace" -name "*kernel_trace.csv" -delete   # the window and --stats stay; the full trace is ~100 MB
       step vsolve_fetch 600 timeout -s KILL 580 rocprofv3 --pmc FETCH_SIZE -d "$O/vsolve_pmc1" -o pmc --output-format csv -- \
         python tools/vsolve_probe.py --ab-edge 0
       step vsolve_write 600 timeout -s KILL 580 rocprofv3 --pmc WRITE_SIZE -d "$O/vsolve_pmc2" -o pmc --output-format csv -- \
-        python tools/vsolve_probe.py --ab-edge 0 ;;
+        python tools/vsolve_probe.py --ab-edge 0
+      python tools/pmc_compact.py "$O/vsolve_pmc1" && python tools/pmc_compact.py "$O/vsolve_pmc2" && du -sh "$O" ;;
+    bandlab)    # cfg2 latency anatomy: diagnostic ablations (sem_amd/lib_diag) and the trivial-kernel floor
+      step dispatch 120 tools/dispatch_bench
+      for kp in 0 -1; do for d in 0 16 32 48 112; do
+        SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_BAND_KP=$kp SEM_DIAG=$d \
+          step bandlab_kp${kp}_d$d 120 python tools/kbench.py --meshes 8:64 --reps 1000
+      done; done
+      SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_BAND_KP=-1 SEM_DIAG=8 SEM_DIAG_BUF=auto TAILN=30 \
+        step bandlab_stamps 120 python tools/kbench.py --meshes 8:64 --stamps --stride 16 --nstamps 6 --roles X:0-1,Y:2-3 ;;
+    schurab)    TAILN=4 step schurab 900 python tools/schur_ab.py --out "$O/schur_ab.jsonl" ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
     benchtrace)

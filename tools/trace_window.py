@@ -3,7 +3,8 @@
 The window starts at the (2 reps)-th last dispatch of a marker kernel that runs `per_rep` times per
 repetition (default: sem::ns_apply_kernel, twice per Schur-complement matvec).
 
-python tools/trace_window.py <trace_kernel_trace.csv> [reps] [marker] [per_rep]
+python tools/trace_window.py <trace_kernel_trace.csv | rocprofv3 -d dir> [reps] [marker] [per_rep] [--save out.csv]
+(--save: the window's dispatches as a small CSV, so the full trace need not travel back from the GPU box)
 """
 import collections
 import csv
@@ -13,6 +14,11 @@ import sys
 
 
 def main():
+    save = None
+    if "--save" in sys.argv:
+        i = sys.argv.index("--save")
+        save = sys.argv[i + 1]
+        del sys.argv[i:i + 2]
     path = sys.argv[1]
     if os.path.isdir(path):   # a rocprofv3 -d directory: its kernel trace
         path = sorted(glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True))[0]
@@ -28,6 +34,13 @@ def main():
         k = r["Kernel_Name"][:80] + " grid=%s,%s" % (r["Grid_Size_X"], r["Grid_Size_Y"])
         tot[k][0] += 1
         tot[k][1] += d
+    if save:
+        with open(save, "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["Kernel_Name", "Grid_Size_X", "Grid_Size_Y", "Start_Timestamp", "End_Timestamp"])
+            for r in seg:
+                w.writerow([r["Kernel_Name"], r["Grid_Size_X"], r["Grid_Size_Y"], r["Start_Timestamp"],
+                            r["End_Timestamp"]])
     span = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e3
     busy = sum(v[1] for v in tot.values())
     print(f"per repetition: span {span / reps:.1f} us, kernel busy {busy / reps:.1f} us, {len(seg) / reps:.1f} launches")
