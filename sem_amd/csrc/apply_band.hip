@@ -444,10 +444,32 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
 
   // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
   // tiles (y fastest) and neighbouring tiles share their halo lines through that XCD's L2.
-  const int nb = pnblk, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nb >> 3, rem = nb & 7;
-  const int L = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (bid >> 3);
-  const int tx = L / ptiles_y, ty = L - tx * ptiles_y;
+  // Round 4: within each XCD's share the full tiles come first and the tiles of the last tile row and
+  // column (the ghost positions: one line or one column, light) last, and every XCD gets its share of
+  // both.  The dispatcher deals an XCD's blocks over its CUs in order, so the full tiles spread evenly (at
+  // cfg2: 512 full tiles, 2 per CU, 8 waves over 4 SIMDs) and the light ones top up; with the ghost tiles
+  // interleaved, some SIMDs ran three full waves.  Only the block -> tile map changes: results are bitwise
+  // those of any other order.
+  // (a negative tiles_y selects the round-3 order: SEM_BAND_ORDER=1, in-process A/B)
+  const int nb = pnblk, bid = blockIdx.x, tyn = ptiles_y < 0 ? -ptiles_y : ptiles_y, txn = nb / tyn;
+  const int NI = ptiles_y < 0 ? 0 : (txn - 1) * (tyn - 1);  // full tiles: off the last tile row and column
+  const int xcd = bid & 7, rk = bid >> 3, q8 = nb >> 3, rem = nb & 7, qi = NI >> 3, ri = NI & 7;
+  const int Fx = qi + (xcd < ri ? 1 : 0);  // full tiles of this XCD
+  int tx, ty;
+  if (ptiles_y < 0) {  // round 3: one contiguous run of tiles per XCD, ghost tiles where they fall
+    const int Lr = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + rk;
+    tx = Lr / tyn;
+    ty = Lr - tx * tyn;
+  } else if (rk < Fx) {
+    const int fi = xcd * qi + min(xcd, ri) + rk;
+    tx = fi / (tyn - 1);
+    ty = fi - tx * (tyn - 1);
+  } else {
+    const int gi = (xcd * q8 + min(xcd, rem)) - (xcd * qi + min(xcd, ri)) + (rk - Fx);
+    tx = gi < tyn ? txn - 1 : gi - tyn;
+    ty = gi < tyn ? gi : tyn - 1;
+  }
+  const int L = tx * tyn + ty;
 
   const int lb0 = plb0, NY = pNY;
   // element positions [m0, m1) x [n0, n1); position ex_end (ney) is the ghost holding the closing line (column)
@@ -1036,7 +1058,7 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   b.ney = g.ney;
   b.nex = g.nex;
   b.NXg = static_cast<int>(g.NXg);
-  b.tiles_y = tiles_y;
+  b.tiles_y = tune(SEM_TUNE_BAND_ORDER) == 1 ? -tiles_y : tiles_y;
   b.nbytes = g.n_local32 * 8;
   b.dir_mode = g.dir_mode;
   b.diag = g.diag;

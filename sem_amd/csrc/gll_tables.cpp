@@ -47,6 +47,7 @@ Tuning& tuning() {
     r.v[SEM_TUNE_COL_TILE] = env_int("SEM_COL_TILE");
     r.v[SEM_TUNE_NS_APPLY] = env_int("SEM_NS_APPLY");
     r.v[SEM_TUNE_EDGE_THOMAS] = env_int("SEM_EDGE_THOMAS");
+    r.v[SEM_TUNE_BAND_ORDER] = env_int("SEM_BAND_ORDER");
     return r;
   }();
   return t;

@@ -179,8 +179,8 @@ __global__ __launch_bounds__(kCondThreads) void cond_edge_kernel(const CondArgs 
 // branch).  Lane (h, i) = half h of row i: it owns the H columns [h H, h H + H) of row i, so one GEMV is H
 // dependent FMAs per lane instead of B, and the two halves' partial sums meet in LDS, where every lane reads
 // the pair sums of its own columns for the next GEMV (one LDS round trip per GEMV, the halves' combination
-// folded into the broadcast).  The operands of the next kD steps (the half-rows of El_{k-1}, Ed_k or Eu_k,
-// and the step's right-hand side) are loaded kD steps ahead into a register ring: the edge offsets are
+// folded into the broadcast).  The operands of the next D steps (the half-rows of El_{k-1}, Ed_k or Eu_k,
+// and the step's right-hand side) are loaded D steps ahead into a register ring: the edge offsets are
 // arithmetic (no index load in front of the right-hand side's load), so no load waits on another and the
 // sweep runs at the latency of its FMA chains and LDS round trips, not of memory.  Columns are independent
 // (grid = nex).
@@ -190,7 +190,9 @@ template <int B>
 struct EdgeThomas {
   static constexpr int H = B <= 1 ? 2 : (((B + 1) / 2 + 1) & ~1);  // columns per half-row (even)
   static constexpr bool VEC = (B % 2) == 0;                         // 16-byte aligned half-rows
-  static constexpr int D = 3;                                       // steps loaded ahead
+  // steps loaded ahead: as deep as the register file allows without scratch (the ring spills into AGPRs for
+  // B > 12; round 4: 3 steps left the sweep at 1.2 us per step, HBM latency over three steps of compute)
+  static constexpr int D = B <= 8 ? 8 : (B <= 16 ? 6 : 5);
 };
 
 // half-row h of row i (columns [h H, h H + H) below B) of the row-major B x B block M; zero elsewhere

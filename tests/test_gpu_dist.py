@@ -384,7 +384,7 @@ def test_cfg5_element_partitioned_ns_update(gpu):
     procs = [ctx.Process(target=_worker_cfg5_update, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    err, tol, nmv, secs, verr = q.get(timeout=840)
+    err, tol, nmv, secs, verr = q.get(timeout=660)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -38,7 +38,7 @@ for s in "$@"; do
     pivot)      step pivot 300 python tools/pivot_probe.py ;;
     gemvprobe)  step gemvprobe 300 python tools/gemv_probe.py ;;
     dist)       step dist 900 $PYT tests/test_gpu_dist.py -k "not cfg5_element_partitioned_ns_update" ;;
-    distcfg5)   SEM_SLOW_GPU_TESTS=1 step distcfg5 1000 ${PYT/--timeout 300/--timeout 900} -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
+    distcfg5)   SEM_SLOW_GPU_TESTS=1 step distcfg5 720 ${PYT/--timeout 300/--timeout 680} -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
     cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5factor_inv) SEM_PIVOT_INV=inv SEM_PROFILE_FACTOR=1 step cfg5factor_inv 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5ns)     SEM_PROFILE_FACTOR=1 step cfg5ns 900 python tools/cfg5_ns_probe.py ;;
@@ -79,9 +79,13 @@ for s in "$@"; do
       for kp in 0 -1; do for d in 0 16 32 48 112; do
         SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_BAND_KP=$kp SEM_DIAG=$d \
           step bandlab_kp${kp}_d$d 120 python tools/kbench.py --meshes 8:64 --reps 1000
-      done; done
-      SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_BAND_KP=-1 SEM_DIAG=8 SEM_DIAG_BUF=auto TAILN=30 \
-        step bandlab_stamps 120 python tools/kbench.py --meshes 8:64 --stamps --stride 16 --nstamps 6 --roles X:0-1,Y:2-3 ;;
+      done; done ;;
+    kbench)     TAILN=4 step kbench 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 1000 ;;
+    bandtests)  step bandtests 600 $PYT tests/test_gpu_apply.py tests/test_gpu_partition.py ;;
+    orderab)    # band tile order A/B: full tiles first (0) against the round-3 order (1), alternated, one process each
+      for rep in 1 2 3; do for o in 0 1; do
+        SEM_BAND_ORDER=$o TAILN=2 step orderab_${o}_$rep 120 python tools/kbench.py --meshes 8:64,8:256 --reps 2000
+      done; done ;;
     schurab)    TAILN=4 step schurab 900 python tools/schur_ab.py --out "$O/schur_ab.jsonl" ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
