@@ -137,8 +137,8 @@ enum sem_tune {
                            * (the one knob whose variants agree to rounding, not bitwise)           */
   SEM_TUNE_EDGE_THOMAS = 7, /* SEM_EDGE_THOMAS: 1 = the ABI-9 runtime-width edge sweep of sem_nested_solve
                              * instead of the templated one (A/B only; agrees to rounding)             */
-  SEM_TUNE_BAND_ORDER = 8,  /* SEM_BAND_ORDER: 1 = the round-3 block -> tile order of the band kernel (ghost
-                             * tiles interleaved) instead of full tiles first (A/B only; bitwise identical) */
+  SEM_TUNE_BAND_ORDER = 8,  /* SEM_BAND_ORDER: 1 = the band kernel's full tiles before its ghost tiles in
+                             * every XCD's share (measured slower; A/B only; bitwise identical) */
   SEM_TUNE_COUNT = 9
 };
 

@@ -444,19 +444,17 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
 
   // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
   // tiles (y fastest) and neighbouring tiles share their halo lines through that XCD's L2.
-  // Round 4: within each XCD's share the full tiles come first and the tiles of the last tile row and
-  // column (the ghost positions: one line or one column, light) last, and every XCD gets its share of
-  // both.  The dispatcher deals an XCD's blocks over its CUs in order, so the full tiles spread evenly (at
-  // cfg2: 512 full tiles, 2 per CU, 8 waves over 4 SIMDs) and the light ones top up; with the ghost tiles
-  // interleaved, some SIMDs ran three full waves.  Only the block -> tile map changes: results are bitwise
-  // those of any other order.
-  // (a negative tiles_y selects the round-3 order: SEM_BAND_ORDER=1, in-process A/B)
+  // SEM_BAND_ORDER=1 (a negative tiles_y): within each XCD's share the full tiles first and the tiles of the
+  // last tile row and column (the ghost positions: one line or one column, light) last, so that the
+  // dispatcher deals two full workgroups to every CU at cfg2.  Measured 3.5 % SLOWER at cfg2 (4.35 against
+  // 4.19 us, profiles/r04/cfg2_anatomy/order_ab.txt) and at 256^2, so the default is the contiguous order
+  // below.  Only the block -> tile map changes: results are bitwise those of any other order.
   const int nb = pnblk, bid = blockIdx.x, tyn = ptiles_y < 0 ? -ptiles_y : ptiles_y, txn = nb / tyn;
-  const int NI = ptiles_y < 0 ? 0 : (txn - 1) * (tyn - 1);  // full tiles: off the last tile row and column
+  const int NI = ptiles_y < 0 ? (txn - 1) * (tyn - 1) : 0;  // full tiles: off the last tile row and column
   const int xcd = bid & 7, rk = bid >> 3, q8 = nb >> 3, rem = nb & 7, qi = NI >> 3, ri = NI & 7;
   const int Fx = qi + (xcd < ri ? 1 : 0);  // full tiles of this XCD
   int tx, ty;
-  if (ptiles_y < 0) {  // round 3: one contiguous run of tiles per XCD, ghost tiles where they fall
+  if (ptiles_y > 0) {  // default: one contiguous run of tiles per XCD, ghost tiles where they fall
     const int Lr = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + rk;
     tx = Lr / tyn;
     ty = Lr - tx * tyn;
@@ -535,18 +533,26 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
     const int r = q / LW, c = q - r * LW;
     const bool ok = q < BX * LW && r < rows_ok && c < cols_ok && !(kDiag && (a.diag & 32));  // diag 32: no u/v/y traffic
     eoff[e] = ok ? nodeb + r * NY + c : -(1 << 26);  // out of bounds: touches no memory
-    if (a.cpol & 256) {  // u, v are read once per launch: non-temporal
-      pu[e] = bload_c<2>(ru, eoff[e] * 8);
-      pv[e] = bload_c<2>(rv, eoff[e] * 8);
-    } else {
-      pu[e] = bload(ru, eoff[e] * 8);
-      pv[e] = bload(rv, eoff[e] * 8);
-    }
   }
-  if constexpr (FULL) {
+  // The epilogue's pointwise operands are issued after the staged window has gone to LDS (round 4): issued
+  // with it, behind the cache-policy branch, they made the compiler wait for every load (vmcnt(0)) before
+  // the staging stores, so u and v landed before the barrier instead of during the contractions.
+  auto issue_pointwise = [&]() {
 #pragma unroll
-    for (int e = 0; e < C::NE; ++e) ops[e] = load_node_ops(a, eoff[e]);
-  }
+    for (int e = 0; e < C::NE; ++e) {
+      if (a.cpol & 256) {  // u, v are read once per launch: non-temporal
+        pu[e] = bload_c<2>(ru, eoff[e] * 8);
+        pv[e] = bload_c<2>(rv, eoff[e] * 8);
+      } else {
+        pu[e] = bload(ru, eoff[e] * 8);
+        pv[e] = bload(rv, eoff[e] * 8);
+      }
+    }
+    if constexpr (FULL) {
+#pragma unroll
+      for (int e = 0; e < C::NE; ++e) ops[e] = load_node_ops(a, eoff[e]);
+    }
+  };
   if constexpr (KP) {  // the struct's fields: fetched now, while the staging loads are in flight
     BPIN(a.y);
     BPIN(a.fKx);
@@ -574,6 +580,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
       Ts[rr * PT + cc] = (gy >= 0 && gy < NY) ? st[s] : 0.0;
     }
   }
+  issue_pointwise();
   BSTAMP(1);
   __syncthreads();
   BSTAMP(2);

@@ -190,30 +190,58 @@ template <int B>
 struct EdgeThomas {
   static constexpr int H = B <= 1 ? 2 : (((B + 1) / 2 + 1) & ~1);  // columns per half-row (even)
   static constexpr bool VEC = (B % 2) == 0;                         // 16-byte aligned half-rows
-  // steps loaded ahead: as deep as the register file allows without scratch (the ring spills into AGPRs for
-  // B > 12; round 4: 3 steps left the sweep at 1.2 us per step, HBM latency over three steps of compute)
-  static constexpr int D = B <= 8 ? 8 : (B <= 16 ? 6 : 5);
+  // steps loaded ahead: 3 (5-8, AGPR-backed, measured no faster at cfg5: 10.37 against 10.33 ms per velocity
+  // solve, so the ~1.2 us per step is the chain of LDS round trips, barriers and FMAs, not memory latency)
+  static constexpr int D = 3;
 };
 
-// half-row h of row i (columns [h H, h H + H) below B) of the row-major B x B block M; zero elsewhere
+// half-row h of row i (columns [h H, h H + H) below B) of the row-major B x B block M.  Every lane issues the
+// same loads, from clamped addresses, and nothing is computed from the loaded values here: the compiler's
+// wait-count pass waits for all outstanding loads (vmcnt(0)) wherever a path issues fewer loads (a load under a
+// lane-dependent branch) or a loaded value is used before the loop's back edge (a select), which would turn
+// the operand ring into one memory round trip per round.  Columns at or past B hold in-block values of the
+// clamped column and meet zero partial sums in half_dot (pt / pz are zero past B); rows past B are unused.
 template <int B>
 __device__ __forceinline__ void load_half_row(const double* __restrict__ M, int i, int h,
                                               double (&r)[EdgeThomas<B>::H]) {
   constexpr int H = EdgeThomas<B>::H;
-  const int j0 = h * H;
+  const int j0 = h * H, ic = i < B ? i : B - 1;
   if constexpr (EdgeThomas<B>::VEC) {
 #pragma unroll
     for (int q = 0; q < H; q += 2) {
-      double2 v = make_double2(0.0, 0.0);
-      if (i < B && j0 + q < B) v = *reinterpret_cast<const double2*>(M + i * B + j0 + q);
+      const int j = j0 + q, jc = j < B ? j : B - 2;  // B even: j < B means j <= B - 2
+      const double2 v = *reinterpret_cast<const double2*>(M + ic * B + jc);
       r[q] = v.x;
       r[q + 1] = v.y;
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < H; ++q) r[q] = (i < B && j0 + q < B) ? M[i * B + j0 + q] : 0.0;
+    for (int q = 0; q < H; ++q) {
+      const int j = j0 + q, jc = j < B ? j : B - 1;
+      r[q] = M[ic * B + jc];
+    }
   }
 }
+
+// LDS ordering inside a one-wave workgroup (round 4).  __syncthreads() is a workgroup release + acquire on
+// every address space: after the sweep's global stores (Ye) it compiled to s_waitcnt vmcnt(0), i.e. it also
+// waited for the loads the operand ring had issued steps ahead, so every step paid a full memory round trip
+// (1.2 us per step, no faster with a deeper ring).  A wave's LDS operations execute in order; all the sweep
+// needs is that the compiler keeps them in program order and that the writes have completed.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// the terms of one edge row's reduced right-hand side, r - (a0 x0 + a1 x1) - c0 - c1 (rhs() and the two
+// element couplings of edge k), as loaded; value() selects the present terms, in rhs()'s order of operations
+struct EdgeRhs {
+  double r, a0, x0, a1, x1, c0, c1;
+  __device__ __forceinline__ double value(bool own, bool coupled, int k, int ney) const {
+    double v = r;
+    if (coupled) v -= a0 * x0 + a1 * x1;
+    if (k < ney) v -= c0;
+    if (k > 0) v -= c1;
+    return own ? v : 0.0;
+  }
+};
 
 // sum over this lane's columns of M-row * (p[0][j] + p[1][j]): the two halves' partial sums of the vector
 template <int H>
@@ -244,79 +272,99 @@ __global__ __launch_bounds__(64) void cond_edge_thomas_kernel(const CondArgs a) 
   const int nc = B / (a.P - 1), NY = a.m / nc;
   const int64_t off_i = static_cast<int64_t>(i / nc) * a.m + static_cast<int64_t>(i % nc) * NY;
   auto edge_off = [&](int k) { return off_i + static_cast<int64_t>(k) * a.P; };
-  auto redge = [&](int k) {  // reduced edge right-hand side of row i of edge k (own lanes)
-    double v = 0.0;
-    if (own) {
-      v = rhs(a, e, edge_off(k));
-      if (k < a.ney) v -= C[static_cast<int64_t>(k) * 2 * B + i];
-      if (k > 0) v -= C[static_cast<int64_t>(k - 1) * 2 * B + B + i];
-    }
-    return v;
+  // the terms of the reduced edge right-hand side of row i of edge k, loaded raw into the ring (see
+  // load_half_row): clamped row and couplings, loaded from R when there are none; EdgeRhs::value() combines them
+  const int ic = i < B ? i : B - 1;
+  const int64_t off_c = static_cast<int64_t>(ic / nc) * a.m + static_cast<int64_t>(ic % nc) * NY;
+  const bool coupled = a.aIB != nullptr;
+  auto redge = [&](int k, EdgeRhs& q) {
+    const int64_t o = off_c + static_cast<int64_t>(k) * a.P, l1 = o / a.m, r = o - l1 * a.m;
+    const double* rp = a.R + e * a.ld_r + o;
+    const double* ab = coupled ? a.aIB + ((static_cast<int64_t>(e) * (a.P - 1) + l1) * 2) * a.m + r : rp;
+    const double* xb = coupled ? a.xB + static_cast<int64_t>(e) * a.m + r : rp;
+    const int64_t am = coupled ? a.m : 0;
+    const int kc0 = k < a.ney ? k : a.ney - 1, kc1 = k > 0 ? k - 1 : 0;
+    q.r = *rp;
+    q.a0 = ab[0];
+    q.x0 = xb[0];
+    q.a1 = ab[am];
+    q.x1 = xb[am];
+    q.c0 = C[static_cast<int64_t>(kc0) * 2 * B + ic];
+    q.c1 = C[static_cast<int64_t>(kc1) * 2 * B + B + ic];
   };
   if (i >= 2 * H) return;  // no row and no column of this lane (B <= 2 H - 1 < 32); never reaches a barrier
-  // ---- forward sweep, operands of steps k .. k+D-1 in the ring (slot k % D)
-  double rl[D][H], rd[D][H], rr[D];
+  // ---- forward sweep, operands of steps k .. k+D-1 in the ring (slot k % D).  Whole rounds of D steps
+  // refill unconditionally (past the last step: clamped, unused), so every path through the loop issues the
+  // same loads and each step waits only for its own operands; the last nb % D steps run without refills.
+  double rl[D][H], rd[D][H];
+  EdgeRhs rr[D];
+  auto load_fwd = [&](int k, int s) {
+    const int kk = k < nb ? k : nb - 1;
+    load_half_row<B>(El + (kk > 0 ? kk - 1 : 0) * bb, i, h, rl[s]);
+    load_half_row<B>(Ed + kk * bb, i, h, rd[s]);
+    redge(kk, rr[s]);
+  };
+  auto fwd_step = [&](int k, int s) {
+    // t_i = r_i - (El_{k-1} z_{k-1})_i, as the two halves' partial sums
+    double t = rr[s].value(own, coupled, k, a.ney);
+    if (k > 0) t -= half_dot<H>(rl[s], &pz[0][j0], &pz[1][j0]);
+    wave_lds_sync();
+    pt[h][i] = row ? t : 0.0;
+    wave_lds_sync();
+    const double z = half_dot<H>(rd[s], &pt[0][j0], &pt[1][j0]);
+    wave_lds_sync();
+    pz[h][i] = row ? z : 0.0;
+    wave_lds_sync();
+    if (own) Ye[static_cast<int64_t>(k) * B + i] = pz[0][i] + pz[1][i];
+  };
 #pragma unroll
-  for (int s = 0; s < D; ++s)
-    if (s < nb) {
-      if (s > 0) load_half_row<B>(El + (s - 1) * bb, i, h, rl[s]);
-      load_half_row<B>(Ed + s * bb, i, h, rd[s]);
-      rr[s] = redge(s);
-    }
-  for (int k0 = 0; k0 < nb; k0 += D) {
+  for (int s = 0; s < D; ++s) load_fwd(s, s);
+  int k0 = 0;
+  for (; k0 + D <= nb; k0 += D) {
 #pragma unroll
     for (int s = 0; s < D; ++s) {
-      const int k = k0 + s;
-      if (k < nb) {
-        // t_i = r_i - (El_{k-1} z_{k-1})_i, as the two halves' partial sums
-        double t = rr[s];
-        if (k > 0) t -= half_dot<H>(rl[s], &pz[0][j0], &pz[1][j0]);
-        __syncthreads();
-        pt[h][i] = row ? t : 0.0;
-        __syncthreads();
-        const double z = half_dot<H>(rd[s], &pt[0][j0], &pt[1][j0]);
-        __syncthreads();
-        pz[h][i] = row ? z : 0.0;
-        __syncthreads();
-        if (own) Ye[static_cast<int64_t>(k) * B + i] = pz[0][i] + pz[1][i];
-        if (k + D < nb) {  // refill the slot with step k + D
-          load_half_row<B>(El + (k + D - 1) * bb, i, h, rl[s]);
-          load_half_row<B>(Ed + (k + D) * bb, i, h, rd[s]);
-          rr[s] = redge(k + D);
-        }
-      }
+      fwd_step(k0 + s, s);
+      load_fwd(k0 + s + D, s);
     }
   }
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s)
+    if (k0 + s < nb) fwd_step(k0 + s, s);
   // ---- back sweep: pz holds y_{nb-1} = z_{nb-1} (as partial sums); steps k = nb-2 .. 0, slot (nb-2-k) % D
   if (own) Y[edge_off(nb - 1)] = pz[0][i] + pz[1][i];
   double ru[D][H], rz[D];
-#pragma unroll
-  for (int s = 0; s < D; ++s)
-    if (nb - 2 - s >= 0) {
-      load_half_row<B>(Eu + (nb - 2 - s) * bb, i, h, ru[s]);
-      rz[s] = own ? Ye[static_cast<int64_t>(nb - 2 - s) * B + i] : 0.0;
+  auto load_back = [&](int k, int s) {
+    const int kk = k > 0 ? k : 0;
+    load_half_row<B>(Eu + kk * bb, i, h, ru[s]);
+    rz[s] = Ye[static_cast<int64_t>(kk) * B + ic];
+  };
+  auto back_step = [&](int k, int s) {
+    const double y = (own ? rz[s] : 0.0) - half_dot<H>(ru[s], &pz[0][j0], &pz[1][j0]);
+    wave_lds_sync();
+    pz[h][i] = row ? y : 0.0;
+    wave_lds_sync();
+    if (own) {
+      const double v = pz[0][i] + pz[1][i];
+      Ye[static_cast<int64_t>(k) * B + i] = v;
+      Y[edge_off(k)] = v;
     }
-  for (int c0 = 0; c0 < nb - 1; c0 += D) {
+  };
+  const int nback = nb - 1;
+  if (nback > 0) {
+#pragma unroll
+    for (int s = 0; s < D; ++s) load_back(nb - 2 - s, s);
+  }
+  int c0 = 0;
+  for (; c0 + D <= nback; c0 += D) {
 #pragma unroll
     for (int s = 0; s < D; ++s) {
-      const int k = nb - 2 - (c0 + s);
-      if (k >= 0) {
-        const double y = rz[s] - half_dot<H>(ru[s], &pz[0][j0], &pz[1][j0]);
-        __syncthreads();
-        pz[h][i] = row ? y : 0.0;
-        __syncthreads();
-        if (own) {
-          const double v = pz[0][i] + pz[1][i];
-          Ye[static_cast<int64_t>(k) * B + i] = v;
-          Y[edge_off(k)] = v;
-        }
-        if (k - D >= 0) {
-          load_half_row<B>(Eu + (k - D) * bb, i, h, ru[s]);
-          rz[s] = own ? Ye[static_cast<int64_t>(k - D) * B + i] : 0.0;
-        }
-      }
+      back_step(nb - 2 - (c0 + s), s);
+      load_back(nb - 2 - (c0 + s) - D, s);
     }
   }
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s)
+    if (c0 + s < nback) back_step(nb - 2 - (c0 + s), s);
 }
 
 // The ABI-9 sweep (runtime block width, one lane per row, one step loaded ahead), kept for in-process A/B

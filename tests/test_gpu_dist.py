@@ -314,6 +314,9 @@ def test_strip_velocity_solve_real_kernels(gpu, world, case):
         assert err <= 1e-9, (rank, err)
 
 
+MTOL5 = 1e-13   # the couplers' mtol_internal (Boussinesq_SequentialCoupler.py:61-63)
+
+
 def _smooth_step(x, y):
     """A smooth (du, dv, dp) with zero Dirichlet velocities on the walls of the unit square."""
     s = np.sin(np.pi * x) * np.sin(np.pi * y)
@@ -335,9 +338,9 @@ def _worker_cfg5_update(rank, world, port, q):
         from sem_amd.parallel import Partition
         from sem_amd.solvers import NavierStokesSolver
         c5 = CFG5
-        ns = NavierStokesSolver(1.0, 1.0, c5["Re"], c5["Ra"] / c5["Pr"], c5["P"], c5["ne"], c5["ne"], mtol=1e-10,
-                                mtol_newton=1e-10, iprint=[], partition=Partition(dist))
-        x, y = ns.points
+        ns = NavierStokesSolver(1.0, 1.0, c5["Re"], c5["Ra"] / c5["Pr"], c5["P"], c5["ne"], c5["ne"], mtol=MTOL5,
+                                mtol_newton=MTOL5, iprint=[], partition=Partition(dist))
+        x, y = ns.points                  # this rank's nodes (a partitioned solver's points are its strip's)
         say = (lambda msg: print(f"[cfg5 update rank 0 {_t.strftime('%H:%M:%S')}] {msg}", flush=True)) \
             if rank == 0 else (lambda msg: None)
         say(f"solver built, strip {ns._mesh.ex_begin}..{ns._mesh.ex_end} of {c5['ne']} columns")
@@ -360,12 +363,15 @@ def _worker_cfg5_update(rank, world, port, q):
             f"per matvec incl. GMRES)")
         lin = ns._get_dresiduals(du, dv, dp)
         err = ns._norm(*(a - b for a, b in zip(lin, rhs)))
-        sl = slice(ns._mesh.dof_begin, ns._mesh.dof_begin + ns._mesh.n_local)
-        verr = max(float((du - ns._dev(step[0][sl])).abs().max()), float((dv - ns._dev(step[1][sl])).abs().max()))
-        say(f"residual {err:.3e} (tolerance 1e-10 sqrt(N) = {1e-10 * np.sqrt(ns.N):.3e}), "
-            f"max velocity error against the step {verr:.2e}")
+        # velocity error relative to the step's largest velocity, over all ranks (max-reduced)
+        e = torch.tensor([float((du - ns._dev(step[0])).abs().max()), float((dv - ns._dev(step[1])).abs().max()),
+                          float(max(np.abs(step[0]).max(), np.abs(step[1]).max()))], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        verr = float(max(e[0], e[1]) / e[2])
+        say(f"residual {err:.3e} (tolerance {MTOL5:g} sqrt(N) = {MTOL5 * np.sqrt(ns.N):.3e}), "
+            f"velocity error against the step {verr:.2e} (relative)")
         if rank == 0:
-            q.put((err, 1e-10 * np.sqrt(ns.N), ns.schur_matvecs, secs, verr))
+            q.put((err, MTOL5 * np.sqrt(ns.N), ns.schur_matvecs, secs, verr))
     finally:
         dist.destroy_process_group()
 
@@ -390,4 +396,4 @@ def test_cfg5_element_partitioned_ns_update(gpu):
         assert p.exitcode == 0
     print(f"cfg5 partitioned NS update: {nmv} Schur matvecs, {secs:.1f} s, residual {err:.3e} (tol {tol:.3e}), "
           f"velocity error {verr:.2e}")
-    assert err <= 10 * tol and verr < 2e-5
+    assert err <= 10 * tol and verr < 2e-5   # the cfg4 test's bar for the same stopping rule

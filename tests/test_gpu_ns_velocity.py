@@ -140,7 +140,8 @@ def test_scalar_blocks_and_solve_match_oracle_cd_jacobian(gpu, P, nex, ney, Pe):
 
 @pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 2, 100.0), (8, 4, 4, 1000.0), (5, 3, 6, 250.0), (2, 7, 2, 300.0),
                                            (12, 3, 2, 1000.0), (12, 2, 5, 100.0),
-                                           (16, 2, 3, 300.0), (7, 2, 2, 100.0), (3, 3, 4, 50.0)])
+                                           (16, 2, 3, 300.0), (7, 2, 2, 100.0), (3, 3, 4, 50.0),
+                                           (4, 3, 1, 100.0), (8, 2, 7, 500.0)])
 def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     """sem_nested_solve + sem_interface_rhs (ns_condense.hip) against the torch formulation of the
     same condensation, for the velocity pair and the one-component CD Jacobian."""
@@ -166,6 +167,61 @@ def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     y_torch = vc._solve_lines(b.clone())
     err = (y_hip - y_torch).abs().max().item() / y_torch.abs().max().item()
     assert err <= 1e-10, err
+
+
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 1, 100.0), (6, 2, 2, 1000.0), (8, 2, 3, 500.0), (12, 2, 5, 100.0),
+                                           (3, 3, 4, 50.0), (16, 2, 6, 300.0), (7, 2, 8, 200.0)])
+def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
+    """The templated edge block-Thomas sweep (round 4: operand ring of raw loads, branch-free refills in whole
+    rounds of D steps plus a tail, wave-local LDS ordering) against the ABI-9 sweep (SEM_TUNE_EDGE_THOMAS=1:
+    one lane per row, one step ahead, __syncthreads), on edge chains shorter than, equal to and longer than
+    the ring (N_ey + 1 = 2 .. 9 steps against D = 3), odd and even block widths.  Same factors, different
+    summation order in the two half-row dot products: 1e-12 relative."""
+    from sem_amd import _lib
+    from sem_amd.solvers.velocity_solve import VelocityJacobianSolver
+    ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex + ney)
+    ns = _device_solver(P, nex, ney, Re, u, v)
+    kw = dict(juu=ns._Jac_u_u._coeffs()[4], juv=ns._Jac_u_v._coeffs()[4], jvu=ns._Jac_v_u._coeffs()[4],
+              jvv=ns._Jac_v_v._coeffs()[4], dir_mask=ns._dir.mask, dir_sides=ns._dir.sides, **ns._sys_kw(ns._Sys))
+    ch = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
+    ch.edge_dense_max, ch.edge_solve = 0, "auto"
+    ch.factor_mesh(ns._mesh, budget_bytes=1, **kw)
+    assert ch._edge_thomas
+    r = np.random.default_rng(9)
+    bu, bv = ns._dev(r.uniform(-1, 1, ns.N)), ns._dev(r.uniform(-1, 1, ns.N))
+    x_new = torch.cat(ch.solve(bu, bv))
+    lib = _lib.load()
+    _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 1))
+    try:
+        x_old = torch.cat(ch.solve(bu, bv))
+    finally:
+        _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
+    err = (x_new - x_old).abs().max().item() / x_old.abs().max().item()
+    assert err <= 1e-12, err
+    assert torch.equal(torch.cat(ch.solve(bu, bv)), x_new)  # deterministic
+    sol = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu.cpu().numpy(), bv.cpu().numpy())))
+    assert np.abs(x_new.cpu().numpy() - sol).max() <= 1e-9 * np.abs(sol).max()
+    # one component (the CD preconditioner): block width P - 1, odd for even P (the scalar-load half rows)
+    from sem_amd.solvers import ConvectionDiffusionSolver
+    refc, A, uc, vc = oracle_cd_jacobian(P, nex, ney, Re, seed=P + nex)
+    cd = ConvectionDiffusionSolver(1.0, 1.0, Re, P, nex, ney, T_W=0.5, T_E=-0.5)
+    cd._get_residuals(np.zeros(cd.N), uc, vc)
+    cX, cu, cY, cv, d = cd._Sys._coeffs()
+    c1 = VelocityJacobianSolver(P, nex, ney, cd._mesh.device, ncomp=1)
+    c1.edge_dense_max, c1.edge_solve = 0, "auto"
+    c1.factor_mesh(cd._mesh, budget_bytes=1, c_stiff=cd._Sys.cK, c_gradx=cX, cu=cu, c_grady=cY, cv=cv,
+                   **cd._dir.kw())
+    assert c1._edge_thomas
+    b = cd._dev(np.random.default_rng(11).uniform(-1, 1, cd.N))
+    y_new = c1.solve1(b)
+    _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 1))
+    try:
+        y_old = c1.solve1(b)
+    finally:
+        _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
+    assert (y_new - y_old).abs().max().item() <= 1e-12 * y_old.abs().max().item()
+    want = spla.spsolve(A.tocsc(), b.cpu().numpy())
+    assert np.abs(y_new.cpu().numpy() - want).max() <= 1e-9 * np.abs(want).max()
 
 
 @pytest.mark.parametrize("M,K,lda,alpha,beta", [(3074, 6148, 6148, 1.0, 0.0), (3074, 3074, 3074, -1.0, 1.0),

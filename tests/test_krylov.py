@@ -125,3 +125,33 @@ def test_gcro_recycling_sequence(precond):
     AU = (A @ (U.T)).T
     assert (AU - C).abs().max().item() < 1e-12
     assert max(its[1:]) <= its[0]
+
+
+def test_partitioned_krylov_sizes_ignore_the_local_length():
+    """A partitioned solve (inner given) must size nothing from its local length: ranks holding strips of
+    different sizes would leave the Arnoldi loop at different iterations and their collectives would
+    mismatch (the world-8 gloo NS test with one-column strips).  The restart is taken as given (not clamped to
+    the local N) and maxiter is required."""
+    from sem_amd.krylov import _sizes, gmres_left
+    assert _sizes(10, 40, None, None, 100) == (10, 100)          # one process: clamped to N, default cap 10 N
+    assert _sizes(10, 40, 500, lambda A, w: A @ w, 100) == (40, 500)
+    with pytest.raises(ValueError, match="maxiter"):
+        _sizes(10, 40, None, lambda A, w: A @ w, 100)
+    A = torch.eye(5, dtype=torch.float64) * 2.0
+    b = torch.ones(5, dtype=torch.float64)
+    with pytest.raises(ValueError, match="maxiter"):
+        gmres(lambda v: A @ v, b, atol=1e-12, inner=lambda V, w: V @ w)
+    with pytest.raises(ValueError, match="maxiter"):
+        gmres_left(lambda v: A @ v, b, atol=1e-12, inner=lambda V, w: V @ w)
+    # a restart above the local length still converges on the local system (the Krylov space saturates)
+    r = gmres(lambda v: A @ v, b, atol=1e-12, restart=40, maxiter=100, inner=lambda V, w: V @ w)
+    assert r.info == 0 and torch.allclose(r.x, b / 2.0)
+
+
+def test_strip_solver_never_captures_over_host_collectives():
+    """Under gloo the strip solve's all-gather goes through the host, so StripLineSolver.capture declines
+    (a capture there failed part-way after a collective warm-up)."""
+    from sem_amd.solvers.strip_solve import StripLineSolver
+    vs = StripLineSolver(4, 4, 2, "cpu", [0, 2, 4], 0, dist=None, gather_device="cpu")
+    vs.factored = True
+    assert vs.capture() is False

@@ -89,6 +89,9 @@ for s in "$@"; do
     schurab)    TAILN=4 step schurab 900 python tools/schur_ab.py --out "$O/schur_ab.jsonl" ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
+    cfg5part)   # rehearsal of cfg5's element-partitioned coupled solve: 4 ranks on one GPU over gloo, Ra = 1e3 from rest
+      step cfg5part 1080 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29611 tools/bous_cfg5_solve.py --backend gloo --Ra 1e3 --out "$O/cfg5_part4_ra1e3.json" ;;
     benchtrace)
       step bench 600 python bench.py
       step benchtrace 600 rocprofv3 --kernel-trace --stats -d "$O/benchtrace" -o trace --output-format csv -- \
