@@ -34,9 +34,9 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
 // n <= 64, 256 threads.  Lane l of wave w holds column c = 16 w + (l & 15), rows 16 (l >> 4) .. + 15:
 // all 64 rows of a column sit in one wave, so the pivot row's entry of every column is one lane
 // permute away and a step needs a single barrier (for the broadcast of column k to all four waves).
-// The pivot search runs in every wave on the same LDS copy of column k: one key per row (|a[r][k]| as a
-// float with its low 6 bits replaced by 63 - r, rows already pivoted 0) and one DPP maximum -- the
-// largest magnitude to 17 bits, the lowest row among equals.
+// The pivot search runs in every wave on the same LDS copy of column k: one key per row (the high word
+// of |a[r][k]| with its low 6 bits replaced by 63 - r, rows already pivoted 0) and one DPP maximum -- the
+// largest magnitude to 14 mantissa bits, the lowest row among equals.
 __global__ __launch_bounds__(256) void gj_inverse_kernel(const double* __restrict__ A, int64_t lda,
                                                          double* __restrict__ X, int64_t ldx, int n) {
   constexpr int R = 16;
@@ -59,7 +59,10 @@ __global__ __launch_bounds__(256) void gj_inverse_kernel(const double* __restric
     const int b = k & 1;
     __syncthreads();
     const double x = colk[b][lane];
-    const unsigned kx = max(__float_as_uint(static_cast<float>(fabs(x))) & ~63u, 64u) | static_cast<unsigned>(63 - lane);
+    // key from the double's own high word (exponent + 20 mantissa bits): monotone in |x| over the whole
+    // double range, subnormals included (a float conversion collapsed everything below ~1e-38)
+    const unsigned hi = static_cast<unsigned>(static_cast<unsigned long long>(__double_as_longlong(fabs(x))) >> 32);
+    const unsigned kx = max(hi & ~63u, 64u) | static_cast<unsigned>(63 - lane);
     const unsigned key = used ? 0u : kx;
     const int p = 63 - static_cast<int>(wave_max_u32(key) & 63u);
     if (lane == p) used = true;

@@ -43,6 +43,21 @@ def test_small_inverse_views_and_pivoting(gpu):
     assert out[0].abs().max().item() == 0.0 and out[:, :n // 2].abs().max().item() == 0.0   # nothing outside X
 
 
+def test_small_inverse_pivots_tiny_scaled_blocks(gpu):
+    """A block that needs row pivoting, scaled to 1e-300: the pivot key comes from the double itself, so
+    magnitudes far below the float range still order the rows."""
+    from sem_amd.linalg import small_inverse_into
+    n = 40
+    g = torch.Generator(device="cuda").manual_seed(5)
+    Pm = torch.zeros((n, n), dtype=torch.float64, device="cuda")
+    Pm[torch.arange(n), (torch.arange(n) + 1) % n] = 1.0
+    A = 1e-300 * (Pm + 1e-3 * torch.rand((n, n), dtype=torch.float64, device="cuda", generator=g))
+    X = torch.zeros_like(A)
+    small_inverse_into(A, X)
+    assert torch.isfinite(X).all().item()
+    assert _rel_res(A, X) < 1e-13
+
+
 def test_small_inverse_singular_is_non_finite(gpu):
     from sem_amd.linalg import small_inverse_into
     A = torch.ones((8, 8), dtype=torch.float64, device="cuda")
