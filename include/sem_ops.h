@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 10
+#define SEM_ABI_VERSION 11
 
 enum sem_status {
   SEM_OK = 0,
@@ -308,12 +308,24 @@ typedef struct sem_nested_desc {
   const double* Ed;
   const double* El;
   const double* Eu;
+  /* ABI 11 (nullable): per element XiB = Xi A_iB (ni x 2 ne1) and AXB = A_ei Xi A_iB (2 ne1 x 2 ne1), column-major,
+   * where A_iB couples element n's interior to the interface nodes at its interior heights (columns ordered
+   * (side s, component c, height j = 1..P-1): x_B[e+s][c N_y + n P + j]).  Used by sem_nested_back_solve. */
+  const double* XiB;
+  const double* AXB;
 } sem_nested_desc;
 /* Column e's right-hand side at R + e ld_r (interior offsets o = (l-1) m + c N_y + gy), minus
  * aIB[e][l-1][s][.] xB[e+s][.] when aIB and xB are given (the back substitution r = b - A_IB x_B);
  * the solution goes to Y + e ld_y at the same offsets.  Three launches, stream-ordered. */
 int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB, const double* xB,
                      double* Y, int64_t ld_y, void* stream);
+/* ABI 11: the back substitution x_I = A_II^-1 (b_I - A_IB x_B) of the condensed solve, called right after
+ * sem_nested_solve(d, R, ld_r, NULL, NULL, ...) with the SAME R and descriptor (whose work arrays T and C still
+ * hold that solve's Xi b_i and A_ei Xi b_i): the element step becomes T -= XiB x_B|n, C -= AXB x_B|n, reading
+ * 2 ne1 columns per element instead of Xi's ni (cfg5: 1.65 GB instead of 9.09 GB).  The edge and back steps
+ * are sem_nested_solve's with the interface correction (aIB, xB).  Needs d->XiB and d->AXB. */
+int sem_nested_back_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB,
+                          const double* xB, double* Y, int64_t ld_y, void* stream);
 /* g[L] = B[L P] - sum_l aBI[L][0][l] yI[L][l] - sum_l aBI[L-1][1][l] yI[L-1][l] (L = 0..nex, rows
  * of m doubles; B rows ld_b apart, yI columns ld_yI apart): the interface right-hand side of the
  * condensed solve. */

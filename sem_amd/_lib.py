@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.environ.get("SEM_LIBDIR") or os.path.join(_HERE, "lib"), "libsemops.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 (TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE, TUNE_NS_APPLY,
  TUNE_EDGE_THOMAS, TUNE_BAND_ORDER) = range(9)
@@ -50,7 +50,7 @@ class SemNestedDesc(C.Structure):
     _fields_ = [("P", C.c_int), ("nex", C.c_int), ("ney", C.c_int), ("nc", C.c_int), ("NY", C.c_int64),
                 ("Xi", C.c_void_p), ("Aei", C.c_void_p), ("Yie", C.c_void_p), ("Se", C.c_void_p),
                 ("pi", C.c_void_p), ("pe", C.c_void_p), ("T", C.c_void_p), ("C", C.c_void_p), ("Ye", C.c_void_p),
-                ("Ed", C.c_void_p), ("El", C.c_void_p), ("Eu", C.c_void_p)]
+                ("Ed", C.c_void_p), ("El", C.c_void_p), ("Eu", C.c_void_p), ("XiB", C.c_void_p), ("AXB", C.c_void_p)]
 
 
 class SemNsDesc(C.Structure):
@@ -100,6 +100,8 @@ _SIGS = {
     "sem_ns_apply": (C.c_int, [C.c_void_p, C.POINTER(SemNsDesc)] + [C.c_void_p] * 7),
     "sem_nested_solve": (C.c_int, [C.POINTER(SemNestedDesc), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_int64, C.c_void_p]),
+    "sem_nested_back_solve": (C.c_int, [C.POINTER(SemNestedDesc), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_int64, C.c_void_p]),
     "sem_interface_rhs": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                     C.c_int64, C.c_void_p, C.c_void_p]),
     "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,

@@ -37,6 +37,7 @@ constexpr int kEdgeRows = 64;                         // edge-kernel rows per wo
 
 struct CondArgs {
   const double *Xi, *Aei, *Yie, *Se;
+  const double *XiB, *AXB;     // ABI 11: Xi A_iB (ni x 2 ne1) and A_ei Xi A_iB (2 ne1 x 2 ne1) per element
   const double *Ed, *El, *Eu;  // block-Thomas factors of the edge Schur complement (Se == nullptr)
   const int64_t *pi, *pe;
   double *T, *C, *Ye;
@@ -125,6 +126,28 @@ __global__ __launch_bounds__(kCondThreads) void cond_fwd_kernel(const CondArgs a
   const double* Aei = a.Aei + static_cast<int64_t>(el) * 2 * a.ne1 * a.ni;
   double* C = a.C + static_cast<int64_t>(el) * 2 * a.ne1;
   colmajor_gemv(Aei, 2 * a.ne1, a.ni, t, part, [&](int r, double v) { C[r] = v; });
+}
+
+// K1 of the back substitution (ABI 11): r_i = b_i - A_iB x_B, so Xi r_i = Xi b_i - XiB x_B|n and
+// A_ei Xi r_i = A_ei Xi b_i - AXB x_B|n, where T and C still hold Xi b_i and A_ei Xi b_i from the forward
+// solve of the same b.  x_B|n: the 2 ne1 interface values at element n's interior heights, column order
+// (side s, component c, height j) = x_B[e + s][c N_y + n P + 1 + j'].  Reads 2 ne1 (ni + 2 ne1) doubles per
+// element instead of the forward step's (ni + 2 ne1) ni.
+__global__ __launch_bounds__(kCondThreads) void cond_fwd_coupled_kernel(const CondArgs a) {
+  extern __shared__ double lds[];
+  double* part = lds;                     // part_size()
+  double* x = lds + part_size();          // G = 2 ne1: x_B|n
+  const int el = blockIdx.x, e = el / a.ney, n = el - e * a.ney;
+  const int G = 2 * a.ne1, pm1 = a.P - 1, nc = a.ne1 / pm1, NY = a.m / nc;
+  for (int q = threadIdx.x; q < G; q += blockDim.x) {
+    const int s = q / a.ne1, r = q - s * a.ne1, c = r / pm1, j = r - c * pm1;
+    x[q] = a.xB[static_cast<int64_t>(e + s) * a.m + static_cast<int64_t>(c) * NY + static_cast<int64_t>(n) * a.P + 1 + j];
+  }
+  __syncthreads();
+  double* T = a.T + static_cast<int64_t>(el) * a.ni;
+  colmajor_gemv(a.XiB + static_cast<int64_t>(el) * a.ni * G, a.ni, G, x, part, [&](int r, double v) { T[r] -= v; });
+  double* C = a.C + static_cast<int64_t>(el) * G;
+  colmajor_gemv(a.AXB + static_cast<int64_t>(el) * G * G, G, G, x, part, [&](int r, double v) { C[r] -= v; });
 }
 
 // K2: y_e = Se (r_e - edge contributions of C); grid (ceil(n_e / 64), nex).  Every workgroup
@@ -508,25 +531,24 @@ static int launch_check(const char* what) {
   return set_error(SEM_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-}  // namespace sem
-
-extern "C" {
-
-int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB, const double* xB,
-                     double* Y, int64_t ld_y, void* stream) {
-  if (!d || !R || !Y) return sem::set_error(SEM_EINVAL, "nested_solve: null argument");
+// CondArgs of a nested solve from the descriptor (checks shared by both entry points)
+static int nested_args(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB, const double* xB,
+                       double* Y, int64_t ld_y, CondArgs& a) {
+  if (!d || !R || !Y) return set_error(SEM_EINVAL, "nested_solve: null argument");
   if (d->P < 2 || d->nex < 1 || d->ney < 1 || (d->nc != 1 && d->nc != 2) || d->NY != d->ney * d->P + 1)
-    return sem::set_error(SEM_EINVAL, "nested_solve: bad sizes");
+    return set_error(SEM_EINVAL, "nested_solve: bad sizes");
   const bool thomas = d->Se == nullptr;
   if (!d->Xi || !d->Aei || !d->Yie || !d->pi || !d->pe || !d->T || !d->C || !d->Ye ||
       (thomas && (!d->Ed || (d->ney > 0 && (!d->El || !d->Eu)))))
-    return sem::set_error(SEM_EINVAL, "nested_solve: null factor or work array");
-  if ((aIB == nullptr) != (xB == nullptr)) return sem::set_error(SEM_EINVAL, "nested_solve: aIB and xB go together");
-  sem::CondArgs a{};
+    return set_error(SEM_EINVAL, "nested_solve: null factor or work array");
+  if ((aIB == nullptr) != (xB == nullptr)) return set_error(SEM_EINVAL, "nested_solve: aIB and xB go together");
+  a = CondArgs{};
   a.Xi = d->Xi;
   a.Aei = d->Aei;
   a.Yie = d->Yie;
   a.Se = d->Se;
+  a.XiB = d->XiB;
+  a.AXB = d->AXB;
   a.Ed = d->Ed;
   a.El = d->El;
   a.Eu = d->Eu;
@@ -548,26 +570,57 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
   a.ne1 = d->nc * (d->P - 1);
   a.ni = a.ne1 * (d->P - 1);
   a.n_e = (d->ney + 1) * a.ne1;
-  if (thomas && a.ne1 > sem::kThomasB)
-    return sem::set_error(SEM_EUNSUPPORTED, "nested_solve: edge blocks wider than the block-Thomas form's 32");
-  if (!thomas && static_cast<size_t>(a.n_e + sem::part_size()) * sizeof(double) > 64 * 1024)
-    return sem::set_error(SEM_EUNSUPPORTED, "nested_solve: too many edge unknowns per column");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 blk(sem::kCondThreads);
-  const unsigned elems = static_cast<unsigned>(d->nex) * d->ney;
-  const size_t part = sem::part_size() * sizeof(double);
-  hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(elems), blk, part + 2 * a.ni * sizeof(double), s, a);
-  if (int st = sem::launch_check("nested_solve fwd")) return st;
-  if (thomas && sem::tune(SEM_TUNE_EDGE_THOMAS) == 1)
-    hipLaunchKernelGGL(sem::cond_edge_thomas_rt_kernel, dim3(d->nex), dim3(64), 0, s, a);
-  else if (thomas)
-    sem::launch_edge_thomas<1>(a, s);
+  if (thomas && a.ne1 > kThomasB)
+    return set_error(SEM_EUNSUPPORTED, "nested_solve: edge blocks wider than the block-Thomas form's 32");
+  if (!thomas && static_cast<size_t>(a.n_e + part_size()) * sizeof(double) > 64 * 1024)
+    return set_error(SEM_EUNSUPPORTED, "nested_solve: too many edge unknowns per column");
+  return SEM_OK;
+}
+
+// K2 (edge solve) and K3 (element back step) of a nested solve
+static int nested_edge_back(const CondArgs& a, hipStream_t s) {
+  const size_t part = part_size() * sizeof(double);
+  if (a.Se == nullptr && tune(SEM_TUNE_EDGE_THOMAS) == 1)
+    hipLaunchKernelGGL(cond_edge_thomas_rt_kernel, dim3(a.nex), dim3(64), 0, s, a);
+  else if (a.Se == nullptr)
+    launch_edge_thomas<1>(a, s);
   else
-    hipLaunchKernelGGL(sem::cond_edge_kernel, dim3((a.n_e + sem::kEdgeRows - 1) / sem::kEdgeRows, d->nex), blk,
+    hipLaunchKernelGGL(cond_edge_kernel, dim3((a.n_e + kEdgeRows - 1) / kEdgeRows, a.nex), dim3(kCondThreads),
                        part + a.n_e * sizeof(double), s, a);
-  if (int st = sem::launch_check("nested_solve edge")) return st;
-  hipLaunchKernelGGL(sem::cond_back_kernel, dim3(elems), blk, part + 2 * a.ne1 * sizeof(double), s, a);
-  return sem::launch_check("nested_solve back");
+  if (int st = launch_check("nested_solve edge")) return st;
+  hipLaunchKernelGGL(cond_back_kernel, dim3(static_cast<unsigned>(a.nex) * a.ney), dim3(kCondThreads),
+                     part + 2 * a.ne1 * sizeof(double), s, a);
+  return launch_check("nested_solve back");
+}
+
+}  // namespace sem
+
+extern "C" {
+
+int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB, const double* xB,
+                     double* Y, int64_t ld_y, void* stream) {
+  sem::CondArgs a;
+  if (int st = sem::nested_args(d, R, ld_r, aIB, xB, Y, ld_y, a)) return st;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t part = sem::part_size() * sizeof(double);
+  hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(static_cast<unsigned>(a.nex) * a.ney), dim3(sem::kCondThreads),
+                     part + 2 * a.ni * sizeof(double), s, a);
+  if (int st = sem::launch_check("nested_solve fwd")) return st;
+  return sem::nested_edge_back(a, s);
+}
+
+int sem_nested_back_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB,
+                          const double* xB, double* Y, int64_t ld_y, void* stream) {
+  sem::CondArgs a;
+  if (!aIB || !xB) return sem::set_error(SEM_EINVAL, "nested_back_solve: aIB and xB are required");
+  if (int st = sem::nested_args(d, R, ld_r, aIB, xB, Y, ld_y, a)) return st;
+  if (!d->XiB || !d->AXB) return sem::set_error(SEM_EINVAL, "nested_back_solve: the descriptor has no XiB / AXB");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t part = sem::part_size() * sizeof(double);
+  hipLaunchKernelGGL(sem::cond_fwd_coupled_kernel, dim3(static_cast<unsigned>(a.nex) * a.ney), dim3(sem::kCondThreads),
+                     part + 2 * a.ne1 * sizeof(double), s, a);
+  if (int st = sem::launch_check("nested_back_solve fwd")) return st;
+  return sem::nested_edge_back(a, s);
 }
 
 int sem_interface_rhs(int P, int nex, int m, const double* B, int64_t ld_b, const double* aBI, const double* yI,

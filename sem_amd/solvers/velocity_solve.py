@@ -273,6 +273,9 @@ class VelocityJacobianSolver:
         # inverse -- 1.5 MB instead of 64 MB per cfg5 column); "dense" keeps the dense inverse
         self.edge_solve = "auto"
         self._edge_thomas = False
+        # back substitution of the HIP nested solve: "coupled" (ABI 11, T -= Xi A_iB x_B from the forward solve's
+        # work arrays) or "full" (a second nested solve of b_I - A_IB x_B through Xi, the ABI-10 path)
+        self.nested_back = os.environ.get("SEM_NESTED_BACK", "coupled")
 
     @contextlib.contextmanager
     def _phase(self, name):
@@ -382,8 +385,13 @@ class VelocityJacobianSolver:
                 T.append(None)
             self._hipT = tuple(T)
             self._Xi, self._Aei, self._Yie, self._Se_inv = (None if t is None else t.transpose(-1, -2) for t in T)
+            # ABI 11: Xi A_iB and A_ei Xi A_iB of every element (by-products of the coupling products), so the
+            # back substitution's element step reads 2 ne1 columns instead of Xi's ni (sem_nested_back_solve)
+            G = 2 * ne1
+            self._hipB = (torch.empty((nex, ney, G, ni), **z), torch.empty((nex, ney, G, G), **z))
+            self._XiB, self._AXB = (t.transpose(-1, -2) for t in self._hipB)
         else:
-            self._hipT = None
+            self._hipT = self._hipB = self._XiB = self._AXB = None
             self._Xi, self._Aei, self._Yie, self._Se_inv = [torch.empty(s, **z) for s in shapes] + (
                 [None] if self._edge_thomas else [])
 
@@ -500,6 +508,9 @@ class VelocityJacobianSolver:
             C_GG = ABi @ XiB                                   # (cc, ney, G, G)
             ZeG = -(Aei @ XiB)                                 # rows: edges n, n+1
             ZBG = -(ABi @ Yie)                                 # cols: edges n, n+1
+            if self._XiB is not None:                          # kept for sem_nested_back_solve (ABI 11)
+                self._XiB[c0:c1] = XiB
+                torch.neg(ZeG, out=self._AXB[c0:c1])
             del AiB, XiB, Xi, Yie
         with self._phase("coupling_products"):
             # V = S_e^-1 Z_e in the group order of the columns
@@ -877,8 +888,10 @@ class VelocityJacobianSolver:
                 if not torch.equal(want.reshape(-1), self._pe):
                     raise RuntimeError("nested solve: edge offsets differ from the block-Thomas sweep's layout")
             q = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+            hb = self._hipB if getattr(self, "_hipB", None) is not None else (None, None)
             self._nd = _lib.SemNestedDesc(P, nex, ney, self.ncomp, self.NY, p(XiT), p(AeiT), p(YieT), q(SeT),
-                                          p(self._pi), p(self._pe), p(T), p(Cw), p(Ye), *(q(t) for t in Et))
+                                          p(self._pi), p(self._pe), p(T), p(Cw), p(Ye), *(q(t) for t in Et),
+                                          *(q(t) for t in hb))
         return self._nd
 
     def _own_rhs(self, g, B):
@@ -921,8 +934,11 @@ class VelocityJacobianSolver:
         xB = self._iface_solve(g)
         out = torch.empty((NX, m), dtype=torch.float64, device=self.device)
         out[0::P] = xB
-        _lib.check(lib.sem_nested_solve(C.byref(d), v(b1), P * m, v(self.aIB.data_ptr()), v(xB.data_ptr()),
-                                        v(out.data_ptr() + 8 * m), P * m, st))
+        # back substitution x_I = A_II^-1 (b_I - A_IB x_B): by default from the forward solve's work arrays and
+        # Xi A_iB (ABI 11; nested_back = "full" re-solves with Xi, the ABI-10 path, for A/B)
+        back = lib.sem_nested_back_solve if d.XiB and self.nested_back == "coupled" else lib.sem_nested_solve
+        _lib.check(back(C.byref(d), v(b1), P * m, v(self.aIB.data_ptr()), v(xB.data_ptr()),
+                        v(out.data_ptr() + 8 * m), P * m, st))
         return out
 
     def _solve_lines(self, B):

@@ -169,6 +169,46 @@ def test_hip_nested_solve_matches_torch_path(gpu, P, nex, ney, Re):
     assert err <= 1e-10, err
 
 
+@pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 2, 100.0), (8, 4, 4, 1000.0), (12, 3, 2, 1000.0), (2, 7, 2, 300.0),
+                                           (16, 2, 3, 300.0), (7, 2, 2, 100.0), (3, 3, 4, 50.0), (8, 1, 6, 500.0)])
+def test_coupled_back_substitution_matches_full_resolve(gpu, P, nex, ney, Re):
+    """ABI 11: the back substitution from the forward solve's work arrays and Xi A_iB (sem_nested_back_solve,
+    the default) against the ABI-10 second nested solve of b_I - A_IB x_B through Xi (nested_back = "full"),
+    for the velocity pair and the one-component CD Jacobian, and both against SciPy's sparse solve.  The two
+    differ only in rounding (Xi b - (Xi A_iB) x_B against Xi (b - A_iB x_B))."""
+    ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex + 1)
+    ns = _device_solver(P, nex, ney, Re, u, v)
+    vs = ns._velocity_solver()
+    assert vs.nested_back == "coupled" and vs._XiB is not None
+    vs._graph = None   # a captured graph bakes one path in: eager solves for the A/B
+    r = np.random.default_rng(21)
+    bu, bv = ns._dev(r.uniform(-1, 1, ns.N)), ns._dev(r.uniform(-1, 1, ns.N))
+    x_c = torch.cat(vs.solve(bu, bv))
+    assert torch.equal(torch.cat(vs.solve(bu, bv)), x_c)   # deterministic
+    vs.nested_back = "full"
+    x_f = torch.cat(vs.solve(bu, bv))
+    vs.nested_back = "coupled"
+    sol = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu.cpu().numpy(), bv.cpu().numpy())))
+    scale = np.abs(sol).max()
+    assert np.abs(x_c.cpu().numpy() - sol).max() <= 1e-9 * scale
+    assert np.abs(x_f.cpu().numpy() - sol).max() <= 1e-9 * scale
+    assert (x_c - x_f).abs().max().item() <= 1e-11 * x_f.abs().max().item()
+    from sem_amd.solvers import ConvectionDiffusionSolver
+    refc, A, uc, vc_ = oracle_cd_jacobian(P, nex, ney, Re, seed=P + nex + 1)
+    cd = ConvectionDiffusionSolver(1.0, 1.0, Re, P, nex, ney, T_W=0.5, T_E=-0.5)
+    cd._get_residuals(np.zeros(cd.N), uc, vc_)
+    c1 = cd._jacobian_solver()
+    b = cd._dev(np.random.default_rng(22).uniform(-1, 1, cd.N))
+    c1._graph = None
+    y_c = c1.solve1(b)
+    c1.nested_back = "full"
+    y_f = c1.solve1(b)
+    c1.nested_back = "coupled"
+    want = spla.spsolve(A.tocsc(), b.cpu().numpy())
+    assert np.abs(y_c.cpu().numpy() - want).max() <= 1e-9 * np.abs(want).max()
+    assert (y_c - y_f).abs().max().item() <= 1e-11 * y_f.abs().max().item()
+
+
 @pytest.mark.parametrize("P,nex,ney,Re", [(4, 3, 1, 100.0), (6, 2, 2, 1000.0), (8, 2, 3, 500.0), (12, 2, 5, 100.0),
                                            (3, 3, 4, 50.0), (16, 2, 6, 300.0), (7, 2, 8, 200.0)])
 def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
@@ -196,11 +236,14 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
         x_old = torch.cat(ch.solve(bu, bv))
     finally:
         _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
+    sol = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu.cpu().numpy(), bv.cpu().numpy())))
+    e_new = np.abs(x_new.cpu().numpy() - sol).max() / np.abs(sol).max()
+    e_old = np.abs(x_old.cpu().numpy() - sol).max() / np.abs(sol).max()
+    print(f"velocity pair, block width {ch._ne1}: templated sweep {e_new:.2e}, ABI-9 sweep {e_old:.2e} against spsolve")
+    assert e_new <= 1e-9 and e_old <= 1e-9
     err = (x_new - x_old).abs().max().item() / x_old.abs().max().item()
     assert err <= 1e-12, err
     assert torch.equal(torch.cat(ch.solve(bu, bv)), x_new)  # deterministic
-    sol = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu.cpu().numpy(), bv.cpu().numpy())))
-    assert np.abs(x_new.cpu().numpy() - sol).max() <= 1e-9 * np.abs(sol).max()
     # one component (the CD preconditioner): block width P - 1, odd for even P (the scalar-load half rows)
     from sem_amd.solvers import ConvectionDiffusionSolver
     refc, A, uc, vc = oracle_cd_jacobian(P, nex, ney, Re, seed=P + nex)
@@ -219,9 +262,12 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
         y_old = c1.solve1(b)
     finally:
         _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
-    assert (y_new - y_old).abs().max().item() <= 1e-12 * y_old.abs().max().item()
     want = spla.spsolve(A.tocsc(), b.cpu().numpy())
-    assert np.abs(y_new.cpu().numpy() - want).max() <= 1e-9 * np.abs(want).max()
+    e_new = np.abs(y_new.cpu().numpy() - want).max() / np.abs(want).max()
+    e_old = np.abs(y_old.cpu().numpy() - want).max() / np.abs(want).max()
+    print(f"one component, block width {c1._ne1}: templated sweep {e_new:.2e}, ABI-9 sweep {e_old:.2e} against spsolve")
+    assert e_new <= 1e-9 and e_old <= 1e-9
+    assert (y_new - y_old).abs().max().item() <= 1e-12 * y_old.abs().max().item()
 
 
 @pytest.mark.parametrize("M,K,lda,alpha,beta", [(3074, 6148, 6148, 1.0, 0.0), (3074, 3074, 3074, -1.0, 1.0),

@@ -22,6 +22,10 @@ step() {  # name limit cmd...
 for s in "$@"; do
   case $s in
     gpu)        step gputests 1100 $PYT -m gpu tests ;;
+    gpunoab)    step gputests 1100 $PYT -m gpu tests -k "not edge_sweep_matches_abi9" ;;
+    edgeab)     # test failures (rc 1) do not end the call; a timeout, abort or crash does
+      ( TAILN=30 step edgeab 300 ${PYT/-x/--maxfail 20} -s tests/test_gpu_ns_velocity.py -k edge_sweep_matches_abi9 )
+      rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     gpurest)    step gpurest 900 $PYT -m gpu tests/test_gpu_krylov.py tests/test_gpu_ns_velocity.py \
                   tests/test_gpu_partition.py tests/test_gpu_solvers.py tests/test_gpu_boussinesq.py tests/test_gpu_cfg4.py ;;
     nsbenchab)  step nsbenchab 300 python tools/nsbench.py --kernels band,tile ;;

@@ -6,7 +6,8 @@ Per solve (velocity_solve.py _solve_lines_hip, csrc/ns_condense.hip):
   two nested interior solves, each reading  Xi (element-interior inverses), Aei (edge <- interior),
                                             Yie (interior <- edge), Ed/El (forward) and Eu (back) edge
                                             block-Thomas factors, the right-hand side lines;
-                                            the second also aIB and x_B;
+                                            the second also aIB and x_B -- by default (ABI 11) its element
+                                            step reads Xi A_iB and A_ei Xi A_iB instead of Xi and Aei;
   the interface right-hand side            aBI, the interface lines, y_I;
   the interface sweep (block Thomas)       D0, F_L = [D_L^-1 | -D_L^-1 S_lo] (m x 2m) forward,
                                             Uh_L (m x m) back; or the CR operators.
@@ -15,7 +16,8 @@ Writes: the solution lines, the nested work arrays (T, C, Ye) and y_I.
 Under rocprofv3 --kernel-trace, tools/trace_window.py <csv> SOLVES cond_fwd_kernel 2 splits the last
 SOLVES solves per kernel; the bytes here divide by those durations.
 
-python tools/vsolve_probe.py [--ne 128 --P 12 --Ra 1e6 --solves 20 --ab-edge 1]  (--ab-edge: first the ABI-9 edge sweep)
+python tools/vsolve_probe.py [--ne 128 --P 12 --Ra 1e6 --solves 20 --ab-edge 1 --ab-back 1]
+  (--ab-edge: first the ABI-9 edge sweep; --ab-back: first the ABI-10 back substitution)
 """
 import argparse
 import json
@@ -33,12 +35,20 @@ def nbytes(t):
     return 0 if t is None else t.numel() * t.element_size()
 
 
-def account(vs):
-    """Algorithmic bytes of one solve, by factor."""
+def account(vs, back=None):
+    """Algorithmic bytes of one solve, by factor (back: the back-substitution path, vs.nested_back)."""
     XiT, AeiT, YieT, SeT = vs._hipT
+    back = back or vs.nested_back
     b = {}
-    b["Xi (element-interior inverses) x2"] = 2 * nbytes(XiT)
-    b["Aei x2"] = 2 * nbytes(AeiT)
+    if back == "coupled" and getattr(vs, "_hipB", None) is not None:   # ABI 11
+        XiBT, AXBT = vs._hipB
+        b["Xi (element-interior inverses)"] = nbytes(XiT)
+        b["Aei"] = nbytes(AeiT)
+        b["XiB + AXB (back substitution)"] = nbytes(XiBT) + nbytes(AXBT)
+        b["T, C work (back: read + write)"] = 2 * (nbytes(vs._work[0]) + nbytes(vs._work[1]))
+    else:
+        b["Xi (element-interior inverses) x2"] = 2 * nbytes(XiT)
+        b["Aei x2"] = 2 * nbytes(AeiT)
     b["Yie x2"] = 2 * nbytes(YieT)
     if vs._edge_thomas:
         Ed, El, Eu = vs._EtT
@@ -68,6 +78,8 @@ def main():
     ap.add_argument("--solves", type=int, default=20)
     ap.add_argument("--out", default="")
     ap.add_argument("--ab-edge", type=int, default=1, help="also time the ABI-9 runtime-width edge sweep")
+    ap.add_argument("--ab-back", type=int, default=1,
+                    help="also time the ABI-10 back substitution (a second nested solve through Xi)")
     args = ap.parse_args()
     from sem_amd.solvers import NavierStokesSolver
     Re, Pr = 1e3, 0.71
@@ -114,7 +126,21 @@ def main():
         _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
         vs.capture()
         out["abi9_edge_sweep_solve_ms_median"] = float(np.median(ts_rt))
+    if args.ab_back and getattr(vs, "_hipB", None) is not None:
+        vs.nested_back = "full"
+        vs.capture()
+        ts_full, xu_f, xv_f = timed()
+        vs.nested_back = "coupled"
+        vs.capture()
+        bf = sum(account(vs, "full").values())
+        med_f = float(np.median(ts_full))
+        out["full_back_solve_ms_median"] = med_f
+        out["full_back_bytes_per_solve"] = bf
+        out["full_back_frac_8TBs"] = bf / (med_f * 1e-3) / 8e12
     ts, xu, xv = timed()
+    if args.ab_back and getattr(vs, "_hipB", None) is not None:
+        out["coupled_vs_full_rel_diff"] = float(max((xu - xu_f).abs().max(), (xv - xv_f).abs().max())
+                                                / max(xu.abs().max(), xv.abs().max()))
     if args.ab_edge and vs._edge_thomas:
         out["abi9_vs_templated_rel_diff"] = float(max((xu - xu_rt).abs().max(), (xv - xv_rt).abs().max())
                                                   / max(xu.abs().max(), xv.abs().max()))
