@@ -78,6 +78,12 @@ for s in "$@"; do
       step vsolve_write 600 timeout -s KILL 580 rocprofv3 --pmc WRITE_SIZE -d "$O/vsolve_pmc2" -o pmc --output-format csv -- \
         python tools/vsolve_probe.py --ab-edge 0
       python tools/pmc_compact.py "$O/vsolve_pmc1" && python tools/pmc_compact.py "$O/vsolve_pmc2" && du -sh "$O" ;;
+    vsolvetr)   # kernel trace of one factor + 20 solves of the default path (no A/B, no PMC passes)
+      step vsolvetr 600 rocprofv3 --kernel-trace --stats -d "$O/vsolvetr" -o trace --output-format csv -- \
+        python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 --out "$O/vsolvetr.json"
+      TAILN=40 step vsolvetr_window 120 python tools/trace_window.py "$O/vsolvetr" 20 cond_fwd_kernel 1 \
+        --save "$O/vsolvetr/window_20_solves.csv"
+      find "$O/vsolvetr" -name "*kernel_trace.csv" -delete ;;
     bandlab)    # cfg2 latency anatomy: diagnostic ablations (sem_amd/lib_diag) and the trivial-kernel floor
       step dispatch 120 tools/dispatch_bench
       for kp in 0 -1; do for d in 0 16 32 48 112; do
