@@ -313,6 +313,10 @@ typedef struct sem_nested_desc {
    * (side s, component c, height j = 1..P-1): x_B[e+s][c N_y + n P + j]).  Used by sem_nested_back_solve. */
   const double* XiB;
   const double* AXB;
+  /* (nullable) per element ABY = A_Bi Xi A_ie (2 ne1 x 2 ne1, column-major; rows (s, c, j) as XiB's columns,
+   * columns edges n, n+1), and a work array Pw of nex * 2 * m doubles.  Used by sem_nested_iface_rhs. */
+  const double* ABY;
+  double* Pw;
 } sem_nested_desc;
 /* Column e's right-hand side at R + e ld_r (interior offsets o = (l-1) m + c N_y + gy), minus
  * aIB[e][l-1][s][.] xB[e+s][.] when aIB and xB are given (the back substitution r = b - A_IB x_B);
@@ -326,6 +330,15 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
  * are sem_nested_solve's with the interface correction (aIB, xB).  Needs d->XiB and d->AXB. */
 int sem_nested_back_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* aIB,
                           const double* xB, double* Y, int64_t ld_y, void* stream);
+/* ABI 11: the forward half of the condensed solve in one call -- y_I = A_II^-1 b_I (sem_nested_solve's element
+ * and edge steps; the element values are NOT formed) and the interface right-hand side
+ * g[L] = B[L P] - A_BI y_I of sem_interface_rhs, taken from the element step's T = Xi b_i and the edge values:
+ * A_Bi y_i = A_Bi T - ABY [y_e(n); y_e(n+1)] per element, aBI on the edge nodes.  Reads ABY (2 ne1 columns per
+ * element) instead of Xi A_ie (ni rows) and writes no y_I.  R: column e's interior at R + e ld_r; B: lines ld_b
+ * apart (interface line L at B + L P ld_b); Y receives the edge values at the interior offsets (work, ld_y);
+ * g: (nex + 1) x m.  Needs d->ABY and d->Pw.  Follow with sem_nested_back_solve on the same R. */
+int sem_nested_iface_rhs(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* B, int64_t ld_b,
+                         const double* aBI, double* Y, int64_t ld_y, double* g, void* stream);
 /* g[L] = B[L P] - sum_l aBI[L][0][l] yI[L][l] - sum_l aBI[L-1][1][l] yI[L-1][l] (L = 0..nex, rows
  * of m doubles; B rows ld_b apart, yI columns ld_yI apart): the interface right-hand side of the
  * condensed solve. */

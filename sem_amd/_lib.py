@@ -50,7 +50,8 @@ class SemNestedDesc(C.Structure):
     _fields_ = [("P", C.c_int), ("nex", C.c_int), ("ney", C.c_int), ("nc", C.c_int), ("NY", C.c_int64),
                 ("Xi", C.c_void_p), ("Aei", C.c_void_p), ("Yie", C.c_void_p), ("Se", C.c_void_p),
                 ("pi", C.c_void_p), ("pe", C.c_void_p), ("T", C.c_void_p), ("C", C.c_void_p), ("Ye", C.c_void_p),
-                ("Ed", C.c_void_p), ("El", C.c_void_p), ("Eu", C.c_void_p), ("XiB", C.c_void_p), ("AXB", C.c_void_p)]
+                ("Ed", C.c_void_p), ("El", C.c_void_p), ("Eu", C.c_void_p), ("XiB", C.c_void_p), ("AXB", C.c_void_p),
+                ("ABY", C.c_void_p), ("Pw", C.c_void_p)]
 
 
 class SemNsDesc(C.Structure):
@@ -102,6 +103,8 @@ _SIGS = {
                                    C.c_void_p, C.c_int64, C.c_void_p]),
     "sem_nested_back_solve": (C.c_int, [C.POINTER(SemNestedDesc), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_int64, C.c_void_p]),
+    "sem_nested_iface_rhs": (C.c_int, [C.POINTER(SemNestedDesc), C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                       C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]),
     "sem_interface_rhs": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                     C.c_int64, C.c_void_p, C.c_void_p]),
     "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,

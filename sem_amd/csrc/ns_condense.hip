@@ -38,6 +38,9 @@ constexpr int kEdgeRows = 64;                         // edge-kernel rows per wo
 struct CondArgs {
   const double *Xi, *Aei, *Yie, *Se;
   const double *XiB, *AXB;     // ABI 11: Xi A_iB (ni x 2 ne1) and A_ei Xi A_iB (2 ne1 x 2 ne1) per element
+  const double* ABY;           // ABI 11: A_Bi Xi A_ie (2 ne1 x 2 ne1) per element
+  double* Pw;                  // ABI 11: per-column interface partial sums (nex, 2, m)
+  const double* aBI;           // ABI 11 (sem_nested_iface_rhs): interface <- interior lines, (nex, 2, P-1, m)
   const double *Ed, *El, *Eu;  // block-Thomas factors of the edge Schur complement (Se == nullptr)
   const int64_t *pi, *pe;
   double *T, *C, *Ye;
@@ -525,6 +528,59 @@ __global__ __launch_bounds__(256) void cond_iface_rhs_kernel(const IfaceArgs a) 
   a.g[t] = v;
 }
 
+// Interface partial sums of column e (ABI 11): p[e][s][r] = sum_l aBI[e][s][l][r] y_I[e][l][r] for side s, from
+// the element step's T = Xi b_i and the edge values y_e, without forming y_i = T - Yie [y_e(n); y_e(n+1)]:
+// at element n's interior heights  p = sum_l aBI T  -  (A_Bi Yie) [y_e(n); y_e(n+1)]  (ABY, 2 ne1 columns),
+// at the edge heights k = n (and k = ney for the last element)  p = sum_l aBI y_e(k).  One workgroup per element.
+__global__ __launch_bounds__(kCondThreads) void cond_iface_part_kernel(const CondArgs a) {
+  extern __shared__ double lds[];
+  double* part = lds;                     // part_size()
+  double* ye = lds + part_size();         // 2 ne1: edges n, n+1 (contiguous in Ye)
+  const int el = blockIdx.x, e = el / a.ney, n = el - e * a.ney;
+  const int G = 2 * a.ne1, pm1 = a.P - 1, nc = a.ne1 / pm1, NY = a.m / nc;
+  const double* src = a.Ye + static_cast<int64_t>(e) * a.n_e + static_cast<int64_t>(n) * a.ne1;
+  for (int i = threadIdx.x; i < G; i += blockDim.x) ye[i] = src[i];
+  __syncthreads();
+  const double* T = a.T + static_cast<int64_t>(el) * a.ni;
+  double* pw = a.Pw + static_cast<int64_t>(e) * 2 * a.m;
+  const double* ab = a.aBI + static_cast<int64_t>(e) * 2 * pm1 * a.m;   // [s][l][r]
+  colmajor_gemv(a.ABY + static_cast<int64_t>(el) * G * G, G, G, ye, part, [&](int q, double v) {
+    const int s = q / a.ne1, r1 = q - s * a.ne1, c = r1 / pm1, j = r1 - c * pm1;
+    const int64_t r = static_cast<int64_t>(c) * NY + static_cast<int64_t>(n) * a.P + 1 + j;
+    double acc = 0.0;
+    for (int l = 0; l < pm1; ++l) acc = fma(ab[(static_cast<int64_t>(s) * pm1 + l) * a.m + r], T[(l * nc + c) * pm1 + j], acc);
+    pw[static_cast<int64_t>(s) * a.m + r] = acc - v;
+  });
+  // edge heights: edge k = n, and the closing edge k = ney on the last element of the column
+  const int ne = n == a.ney - 1 ? 2 : 1;
+  for (int t = threadIdx.x; t < ne * 2 * nc; t += blockDim.x) {
+    const int k = n + t / (2 * nc), sc = t % (2 * nc), s = sc / nc, c = sc - s * nc;
+    const int64_t r = static_cast<int64_t>(c) * NY + static_cast<int64_t>(k) * a.P;
+    const double* yk = a.Ye + static_cast<int64_t>(e) * a.n_e + static_cast<int64_t>(k) * a.ne1;
+    double acc = 0.0;
+    for (int l = 0; l < pm1; ++l) acc = fma(ab[(static_cast<int64_t>(s) * pm1 + l) * a.m + r], yk[l * nc + c], acc);
+    pw[static_cast<int64_t>(s) * a.m + r] = acc;
+  }
+}
+
+// g[L] = B[L P] - p[L][0] - p[L-1][1]
+struct IfacePartArgs {
+  const double *B, *Pw;
+  double* g;
+  int64_t ld_b;
+  int P, nex, m;
+};
+
+__global__ __launch_bounds__(256) void cond_iface_sum_kernel(const IfacePartArgs a) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<int64_t>(a.nex + 1) * a.m) return;
+  const int L = static_cast<int>(t / a.m), r = static_cast<int>(t - static_cast<int64_t>(L) * a.m);
+  double v = a.B[static_cast<int64_t>(L) * a.P * a.ld_b + r];
+  if (L < a.nex) v -= a.Pw[static_cast<int64_t>(L) * 2 * a.m + r];
+  if (L > 0) v -= a.Pw[(static_cast<int64_t>(L - 1) * 2 + 1) * a.m + r];
+  a.g[t] = v;
+}
+
 static int launch_check(const char* what) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) return SEM_OK;
@@ -549,6 +605,8 @@ static int nested_args(const sem_nested_desc* d, const double* R, int64_t ld_r, 
   a.Se = d->Se;
   a.XiB = d->XiB;
   a.AXB = d->AXB;
+  a.ABY = d->ABY;
+  a.Pw = d->Pw;
   a.Ed = d->Ed;
   a.El = d->El;
   a.Eu = d->Eu;
@@ -577,19 +635,23 @@ static int nested_args(const sem_nested_desc* d, const double* R, int64_t ld_r, 
   return SEM_OK;
 }
 
-// K2 (edge solve) and K3 (element back step) of a nested solve
-static int nested_edge_back(const CondArgs& a, hipStream_t s) {
-  const size_t part = part_size() * sizeof(double);
+// K2 (edge solve) of a nested solve
+static int nested_edge(const CondArgs& a, hipStream_t s) {
   if (a.Se == nullptr && tune(SEM_TUNE_EDGE_THOMAS) == 1)
     hipLaunchKernelGGL(cond_edge_thomas_rt_kernel, dim3(a.nex), dim3(64), 0, s, a);
   else if (a.Se == nullptr)
     launch_edge_thomas<1>(a, s);
   else
     hipLaunchKernelGGL(cond_edge_kernel, dim3((a.n_e + kEdgeRows - 1) / kEdgeRows, a.nex), dim3(kCondThreads),
-                       part + a.n_e * sizeof(double), s, a);
-  if (int st = launch_check("nested_solve edge")) return st;
+                       (part_size() + a.n_e) * sizeof(double), s, a);
+  return launch_check("nested_solve edge");
+}
+
+// K2 and K3 (element back step) of a nested solve
+static int nested_edge_back(const CondArgs& a, hipStream_t s) {
+  if (int st = nested_edge(a, s)) return st;
   hipLaunchKernelGGL(cond_back_kernel, dim3(static_cast<unsigned>(a.nex) * a.ney), dim3(kCondThreads),
-                     part + 2 * a.ne1 * sizeof(double), s, a);
+                     (part_size() + 2 * a.ne1) * sizeof(double), s, a);
   return launch_check("nested_solve back");
 }
 
@@ -621,6 +683,28 @@ int sem_nested_back_solve(const sem_nested_desc* d, const double* R, int64_t ld_
                      part + 2 * a.ne1 * sizeof(double), s, a);
   if (int st = sem::launch_check("nested_back_solve fwd")) return st;
   return sem::nested_edge_back(a, s);
+}
+
+int sem_nested_iface_rhs(const sem_nested_desc* d, const double* R, int64_t ld_r, const double* B, int64_t ld_b,
+                         const double* aBI, double* Y, int64_t ld_y, double* g, void* stream) {
+  sem::CondArgs a;
+  if (!B || !aBI || !g) return sem::set_error(SEM_EINVAL, "nested_iface_rhs: null argument");
+  if (int st = sem::nested_args(d, R, ld_r, nullptr, nullptr, Y, ld_y, a)) return st;
+  if (!d->ABY || !d->Pw) return sem::set_error(SEM_EINVAL, "nested_iface_rhs: the descriptor has no ABY / Pw");
+  a.aBI = aBI;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const unsigned elems = static_cast<unsigned>(a.nex) * a.ney;
+  const size_t part = sem::part_size() * sizeof(double);
+  hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(elems), dim3(sem::kCondThreads), part + 2 * a.ni * sizeof(double), s, a);
+  if (int st = sem::launch_check("nested_iface_rhs fwd")) return st;
+  if (int st = sem::nested_edge(a, s)) return st;
+  hipLaunchKernelGGL(sem::cond_iface_part_kernel, dim3(elems), dim3(sem::kCondThreads),
+                     part + 2 * a.ne1 * sizeof(double), s, a);
+  if (int st = sem::launch_check("nested_iface_rhs part")) return st;
+  sem::IfacePartArgs b{B, d->Pw, g, ld_b, d->P, d->nex, a.m};
+  const int64_t n = static_cast<int64_t>(d->nex + 1) * a.m;
+  hipLaunchKernelGGL(sem::cond_iface_sum_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, b);
+  return sem::launch_check("nested_iface_rhs sum");
 }
 
 int sem_interface_rhs(int P, int nex, int m, const double* B, int64_t ld_b, const double* aBI, const double* yI,

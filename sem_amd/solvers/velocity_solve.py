@@ -273,8 +273,10 @@ class VelocityJacobianSolver:
         # inverse -- 1.5 MB instead of 64 MB per cfg5 column); "dense" keeps the dense inverse
         self.edge_solve = "auto"
         self._edge_thomas = False
-        # back substitution of the HIP nested solve: "coupled" (ABI 11, T -= Xi A_iB x_B from the forward solve's
-        # work arrays) or "full" (a second nested solve of b_I - A_IB x_B through Xi, the ABI-10 path)
+        # HIP nested solves: "coupled" (ABI 11: the interface right-hand side from the forward element step's
+        # T = Xi b_i and the edge values, sem_nested_iface_rhs; the back substitution T -= Xi A_iB x_B from the
+        # same work arrays, sem_nested_back_solve) or "full" (the ABI-10 path: y_I formed, then a second nested
+        # solve of b_I - A_IB x_B through Xi)
         self.nested_back = os.environ.get("SEM_NESTED_BACK", "coupled")
 
     @contextlib.contextmanager
@@ -387,11 +389,14 @@ class VelocityJacobianSolver:
             self._Xi, self._Aei, self._Yie, self._Se_inv = (None if t is None else t.transpose(-1, -2) for t in T)
             # ABI 11: Xi A_iB and A_ei Xi A_iB of every element (by-products of the coupling products), so the
             # back substitution's element step reads 2 ne1 columns instead of Xi's ni (sem_nested_back_solve)
+            # and A_Bi Xi A_ie, so the forward half forms the interface right-hand side without the element
+            # values y_i (sem_nested_iface_rhs)
             G = 2 * ne1
-            self._hipB = (torch.empty((nex, ney, G, ni), **z), torch.empty((nex, ney, G, G), **z))
-            self._XiB, self._AXB = (t.transpose(-1, -2) for t in self._hipB)
+            self._hipB = (torch.empty((nex, ney, G, ni), **z), torch.empty((nex, ney, G, G), **z),
+                          torch.empty((nex, ney, G, G), **z))
+            self._XiB, self._AXB, self._ABY = (t.transpose(-1, -2) for t in self._hipB)
         else:
-            self._hipT = self._hipB = self._XiB = self._AXB = None
+            self._hipT = self._hipB = self._XiB = self._AXB = self._ABY = None
             self._Xi, self._Aei, self._Yie, self._Se_inv = [torch.empty(s, **z) for s in shapes] + (
                 [None] if self._edge_thomas else [])
 
@@ -508,9 +513,10 @@ class VelocityJacobianSolver:
             C_GG = ABi @ XiB                                   # (cc, ney, G, G)
             ZeG = -(Aei @ XiB)                                 # rows: edges n, n+1
             ZBG = -(ABi @ Yie)                                 # cols: edges n, n+1
-            if self._XiB is not None:                          # kept for sem_nested_back_solve (ABI 11)
+            if self._XiB is not None:   # kept for sem_nested_back_solve / sem_nested_iface_rhs (ABI 11)
                 self._XiB[c0:c1] = XiB
                 torch.neg(ZeG, out=self._AXB[c0:c1])
+                torch.neg(ZBG, out=self._ABY[c0:c1])
             del AiB, XiB, Xi, Yie
         with self._phase("coupling_products"):
             # V = S_e^-1 Z_e in the group order of the columns
@@ -876,8 +882,8 @@ class VelocityJacobianSolver:
             z = dict(dtype=torch.float64, device=self.device)
             self._work = (torch.empty(nex * ney * ni, **z), torch.empty(nex * ney * 2 * ne1, **z),
                           torch.empty(nex * (ney + 1) * ne1, **z), torch.empty((nex, self.nI), **z),
-                          torch.empty((nex + 1, m), **z))
-            T, Cw, Ye, _, _ = self._work
+                          torch.empty((nex + 1, m), **z), torch.empty(nex * 2 * m, **z))
+            T, Cw, Ye, _, _, Pw = self._work
             p = lambda t: t.data_ptr()  # noqa: E731
             XiT, AeiT, YieT, SeT = self._hipT
             Et = self._EtT if self._edge_thomas else (None, None, None)   # ABI 9: Se = NULL -> block Thomas
@@ -888,10 +894,10 @@ class VelocityJacobianSolver:
                 if not torch.equal(want.reshape(-1), self._pe):
                     raise RuntimeError("nested solve: edge offsets differ from the block-Thomas sweep's layout")
             q = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
-            hb = self._hipB if getattr(self, "_hipB", None) is not None else (None, None)
+            hb = self._hipB if getattr(self, "_hipB", None) is not None else (None, None, None)
             self._nd = _lib.SemNestedDesc(P, nex, ney, self.ncomp, self.NY, p(XiT), p(AeiT), p(YieT), q(SeT),
                                           p(self._pi), p(self._pe), p(T), p(Cw), p(Ye), *(q(t) for t in Et),
-                                          *(q(t) for t in hb))
+                                          *(q(t) for t in hb), p(Pw))
         return self._nd
 
     def _own_rhs(self, g, B):
@@ -923,20 +929,26 @@ class VelocityJacobianSolver:
         if not (B.is_contiguous() and tuple(B.shape) == (NX, m) and B.dtype == torch.float64):
             raise ValueError("line array must be a contiguous float64 (NX, m) tensor")
         d = self._hip_nested()
-        _, _, _, yI, g = self._work
+        _, _, _, yI, g, _ = self._work
         st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         v = C.c_void_p
         b1 = B.data_ptr() + 8 * m   # line e P + 1: first interior line of column e
-        _lib.check(lib.sem_nested_solve(C.byref(d), v(b1), P * m, None, None, v(yI.data_ptr()), self.nI, st))
-        _lib.check(lib.sem_interface_rhs(P, nex, m, v(B.data_ptr()), m, v(self.aBI.data_ptr()), v(yI.data_ptr()),
-                                         self.nI, v(g.data_ptr()), st))
+        coupled = bool(d.XiB) and self.nested_back == "coupled"
+        if coupled:   # ABI 11: element and edge steps, then g from T and the edge values (no y_I formed)
+            _lib.check(lib.sem_nested_iface_rhs(C.byref(d), v(b1), P * m, v(B.data_ptr()), m,
+                                                v(self.aBI.data_ptr()), v(yI.data_ptr()), self.nI,
+                                                v(g.data_ptr()), st))
+        else:
+            _lib.check(lib.sem_nested_solve(C.byref(d), v(b1), P * m, None, None, v(yI.data_ptr()), self.nI, st))
+            _lib.check(lib.sem_interface_rhs(P, nex, m, v(B.data_ptr()), m, v(self.aBI.data_ptr()),
+                                             v(yI.data_ptr()), self.nI, v(g.data_ptr()), st))
         self._own_rhs(g, B)
         xB = self._iface_solve(g)
         out = torch.empty((NX, m), dtype=torch.float64, device=self.device)
         out[0::P] = xB
         # back substitution x_I = A_II^-1 (b_I - A_IB x_B): by default from the forward solve's work arrays and
         # Xi A_iB (ABI 11; nested_back = "full" re-solves with Xi, the ABI-10 path, for A/B)
-        back = lib.sem_nested_back_solve if d.XiB and self.nested_back == "coupled" else lib.sem_nested_solve
+        back = lib.sem_nested_back_solve if coupled else lib.sem_nested_solve
         _lib.check(back(C.byref(d), v(b1), P * m, v(self.aIB.data_ptr()), v(xB.data_ptr()),
                         v(out.data_ptr() + 8 * m), P * m, st))
         return out

@@ -41,15 +41,19 @@ def account(vs, back=None):
     back = back or vs.nested_back
     b = {}
     if back == "coupled" and getattr(vs, "_hipB", None) is not None:   # ABI 11
-        XiBT, AXBT = vs._hipB
+        XiBT, AXBT, ABYT = vs._hipB
         b["Xi (element-interior inverses)"] = nbytes(XiT)
         b["Aei"] = nbytes(AeiT)
+        b["ABY (interface right-hand side)"] = nbytes(ABYT)
         b["XiB + AXB (back substitution)"] = nbytes(XiBT) + nbytes(AXBT)
-        b["T, C work (back: read + write)"] = 2 * (nbytes(vs._work[0]) + nbytes(vs._work[1]))
+        b["Yie (back substitution)"] = nbytes(YieT)
+        # T written, read by the interface sums, read + written by the back step, read by the last step; C
+        # written, read + written, read by the edge sweeps; the interface partial sums written and read once
+        b["T, C, partial-sum work"] = 4 * nbytes(vs._work[0]) + 4 * nbytes(vs._work[1]) + 2 * nbytes(vs._work[5])
     else:
         b["Xi (element-interior inverses) x2"] = 2 * nbytes(XiT)
         b["Aei x2"] = 2 * nbytes(AeiT)
-    b["Yie x2"] = 2 * nbytes(YieT)
+        b["Yie x2"] = 2 * nbytes(YieT)
     if vs._edge_thomas:
         Ed, El, Eu = vs._EtT
         b["edge Thomas Ed+El+Eu x2"] = 2 * (nbytes(Ed) + nbytes(El) + nbytes(Eu))
