@@ -365,6 +365,11 @@ int sem_block_gemv(int nb, int m, int S, const double* M, const double* const* s
  * order).  Device pointers; y must not overlap A or x.  Stream-ordered.  (ABI 10) */
 int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, const double* x, double beta, double* y,
                   void* stream);
+/* ABI 11: two independent GEMVs of M rows each in ONE launch, y_j = alpha A_j x_j + beta y_j (j = 0, 1; K_j,
+ * lda_j per operator): the two chains of the twisted (two-ended) block-Thomas sweep step together, so the sweep
+ * is ~N_ex + 1 dependent launches instead of 2 N_ex (velocity_solve.py twisted_thomas_solve). */
+int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, int64_t lda0, const double* x0,
+                   double* y0, int K1, const double* A1, int64_t lda1, const double* x1, double* y1, void* stream);
 
 /* ---- small dense inverse (leaves of the sweep's pivot inverses) --------- */
 /* X = A^-1 for one n x n row-major block, n <= 64 (row r of A at A + r lda, of X at X + r ldx; device

@@ -130,11 +130,20 @@ struct RowGemvArgs {
   int M, K;
 };
 
+// One launch, up to two independent GEMVs of M rows each (the twisted sweep's two chains, round 4): blocks
+// [0, nb0) compute p[0], the rest p[1].  A single GEMV has nb0 = the grid size.
+struct RowGemv2Args {
+  RowGemvArgs p[2];
+  int nb0;
+};
+
 template <bool VEC>
-__global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemvArgs a) {
+__global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemv2Args g) {
   __shared__ double part[4][kRowsWG];
+  const bool second = static_cast<int>(blockIdx.x) >= g.nb0;
+  const RowGemvArgs a = second ? g.p[1] : g.p[0];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r0 = blockIdx.x * kRowsWG;
+  const int r0 = (static_cast<int>(blockIdx.x) - (second ? g.nb0 : 0)) * kRowsWG;
   // the wave's K range, in units of 2 doubles (VEC) or 1
   constexpr int W = VEC ? 2 : 1;
   const int KU = (a.K + W - 1) / W;
@@ -205,6 +214,12 @@ __global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemvArgs a) {
   }
 }
 
+// 16-byte loads need 16-byte aligned A rows and x, and an even K
+static bool row_vec(const RowGemvArgs& a) {
+  return (reinterpret_cast<uintptr_t>(a.A) % 16) == 0 && (reinterpret_cast<uintptr_t>(a.x) % 16) == 0 &&
+         (a.lda % 2) == 0 && (a.K % 2) == 0;
+}
+
 }  // namespace sem
 
 extern "C" {
@@ -214,17 +229,33 @@ int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, cons
   if (M < 0 || K < 0 || lda < K) return sem::set_error(SEM_EINVAL, "gemv_rows: bad sizes");
   if (M == 0) return SEM_OK;
   if (!A || !x || !y) return sem::set_error(SEM_EINVAL, "gemv_rows: null argument");
-  sem::RowGemvArgs a{A, x, y, lda, alpha, beta, M, K};
-  const bool vec = (reinterpret_cast<uintptr_t>(A) % 16) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
-                   (lda % 2) == 0 && (K % 2) == 0;
+  const int nb = (M + sem::kRowsWG - 1) / sem::kRowsWG;
+  sem::RowGemv2Args g{{sem::RowGemvArgs{A, x, y, lda, alpha, beta, M, K}, sem::RowGemvArgs{}}, nb};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((M + sem::kRowsWG - 1) / sem::kRowsWG), block(256);
-  if (vec)
-    hipLaunchKernelGGL(sem::row_gemv_kernel<true>, grid, block, 0, s, a);
+  if (sem::row_vec(g.p[0]))
+    hipLaunchKernelGGL(sem::row_gemv_kernel<true>, dim3(nb), dim3(256), 0, s, g);
   else
-    hipLaunchKernelGGL(sem::row_gemv_kernel<false>, grid, block, 0, s, a);
+    hipLaunchKernelGGL(sem::row_gemv_kernel<false>, dim3(nb), dim3(256), 0, s, g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("gemv_rows launch: ") + hipGetErrorString(e));
+  return SEM_OK;
+}
+
+int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, int64_t lda0, const double* x0,
+                   double* y0, int K1, const double* A1, int64_t lda1, const double* x1, double* y1, void* stream) {
+  if (M < 0 || K0 < 0 || K1 < 0 || lda0 < K0 || lda1 < K1) return sem::set_error(SEM_EINVAL, "gemv_rows2: bad sizes");
+  if (M == 0) return SEM_OK;
+  if (!A0 || !x0 || !y0 || !A1 || !x1 || !y1) return sem::set_error(SEM_EINVAL, "gemv_rows2: null argument");
+  const int nb = (M + sem::kRowsWG - 1) / sem::kRowsWG;
+  sem::RowGemv2Args g{{sem::RowGemvArgs{A0, x0, y0, lda0, alpha, beta, M, K0},
+                       sem::RowGemvArgs{A1, x1, y1, lda1, alpha, beta, M, K1}}, nb};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (sem::row_vec(g.p[0]) && sem::row_vec(g.p[1]))
+    hipLaunchKernelGGL(sem::row_gemv_kernel<true>, dim3(2 * nb), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(sem::row_gemv_kernel<false>, dim3(2 * nb), dim3(256), 0, s, g);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("gemv_rows2 launch: ") + hipGetErrorString(e));
   return SEM_OK;
 }
 

@@ -23,7 +23,8 @@ on shared lines.
 """
 import torch
 
-from .velocity_solve import VelocityJacobianSolver, fused_thomas_operators, fused_thomas_solve, pivot_inverse
+from .velocity_solve import (VelocityJacobianSolver, fused_thomas_operators, fused_thomas_solve, pivot_inverse,
+                             twisted_thomas_operators, twisted_thomas_solve)
 
 
 class StripLineSolver(VelocityJacobianSolver):
@@ -95,7 +96,10 @@ class StripLineSolver(VelocityJacobianSolver):
                              torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
             # the solve's operators: the fused block-Thomas sweep of the interior lines (one GEMV per line and
             # direction, as the whole-mesh sweep) and [X0 | X1] for the back substitution in one batched GEMV
-            th = fused_thomas_operators(Dinv, S_lo[1:n - 1] if n > 2 else None, Uh[:k - 1])
+            if self.sweep_form == "twisted" and k >= 3 and dev.type == "cuda":   # two-ended, as the whole mesh
+                th = ("twisted", twisted_thomas_operators(S_diag[1:n], S_up[1:n - 1], S_lo[1:n - 1]))
+            else:
+                th = ("single", fused_thomas_operators(Dinv, S_lo[1:n - 1] if n > 2 else None, Uh[:k - 1]))
             X01 = torch.cat((X0, X1), dim=2)
             del Dinv, Uh, X0, X1
             self._T = (th, X01)
@@ -124,8 +128,10 @@ class StripLineSolver(VelocityJacobianSolver):
             g[-1] -= B[-1]
 
     def _thomas(self, g):
-        """y = T^-1 g for the local interior lines (g: (k, m)): the fused block-Thomas sweep."""
-        return fused_thomas_solve(*self._T[0], g)
+        """y = T^-1 g for the local interior lines (g: (k, m)): the fused block-Thomas sweep, two-ended when the
+        strip has at least three interior lines."""
+        form, op = self._T[0]
+        return twisted_thomas_solve(op, g) if form == "twisted" else fused_thomas_solve(*op, g)
 
     def _iface_solve(self, g):
         """No host synchronisation under RCCL (the all-gather stays on the device): stream-capturable."""

@@ -213,6 +213,114 @@ def _gemv(A, x, y, alpha=1.0, beta=0.0):
     return y
 
 
+def _gemv2(p0, p1, alpha=1.0, beta=0.0):
+    """Two independent GEMVs (A, x, y) of equal row count in one launch (sem_gemv_rows2); torch elsewhere."""
+    (A0, x0, y0), (A1, x1, y1) = p0, p1
+    ok = lambda A, x, y: (A.is_cuda and A.dtype == torch.float64 and A.stride(1) == 1  # noqa: E731
+                          and x.stride(0) == 1 and y.stride(0) == 1)
+    if _SWEEP_GEMV == "hip" and A0.shape[0] == A1.shape[0] and ok(A0, x0, y0) and ok(A1, x1, y1):
+        import ctypes as C
+        from .. import _lib
+        lib = _lib.load()
+        v = C.c_void_p
+        _lib.check(lib.sem_gemv_rows2(A0.shape[0], alpha, beta, A0.shape[1], v(A0.data_ptr()), A0.stride(0),
+                                      v(x0.data_ptr()), v(y0.data_ptr()), A1.shape[1], v(A1.data_ptr()), A1.stride(0),
+                                      v(x1.data_ptr()), v(y1.data_ptr()),
+                                      v(torch.cuda.current_stream(A0.device).cuda_stream)))
+        return
+    _gemv(A0, x0, y0, alpha, beta)
+    _gemv(A1, x1, y1, alpha, beta)
+
+
+def twisted_thomas_operators(S_diag, S_up, S_lo, inv=None):
+    """Operators of the twisted ("burn at both ends") block-Thomas solve of a block-tridiagonal system with
+    lines 0..n-1 (n >= 3; diagonal S_diag, S_up[L]: row L <- L+1, S_lo[L]: row L+1 <- L): elimination from
+    line 0 down to k-1 and from line n-1 up to k+1 (k = n // 2), the two chains meeting at line k.
+      top     Dt_0 = S_diag[0], UhT_L = Dt_L^-1 S_up[L], Dt_{L+1} = S_diag[L+1] - S_lo[L] UhT_L
+      bottom  Et_{n-1} = S_diag[n-1], UhB_L = Et_L^-1 S_lo[L-1], Et_{L-1} = S_diag[L-1] - S_up[L-1] UhB_L
+      middle  M = S_diag[k] - S_lo[k-1] UhT_{k-1} - S_up[k] UhB_{k+1}
+    Fused forward operators as in fused_thomas_operators: FT_L = [Dt_L^-1 | -Dt_L^-1 S_lo[L-1]] (L = 1..k-1),
+    FB_L = [Et_L^-1 | -Et_L^-1 S_up[L]] (L = k+1..n-2), FM = [M^-1 | -M^-1 S_lo[k-1] | -M^-1 S_up[k]]; the
+    same 3 m^2 doubles per line as the one-ended sweep (plus m^2 for the middle) and the same pivot
+    inverses, but the two chains run side by side (twisted_thomas_solve): n + 1 dependent steps, not 2 n - 1."""
+    inv = inv or pivot_inverse
+    n, m = S_diag.shape[0], S_diag.shape[1]
+    if n < 3:
+        raise ValueError("the twisted sweep needs at least 3 lines")
+    k = n // 2
+    z = dict(dtype=S_diag.dtype, device=S_diag.device)
+    FT, UhT = torch.empty((k - 1, m, 2 * m), **z), torch.empty((k, m, m), **z)
+    FB, UhB = torch.empty((n - 2 - k, m, 2 * m), **z), torch.empty((n - 1 - k, m, m), **z)
+    Dt = S_diag[0]
+    for L in range(k):
+        if L > 0:
+            Dt = S_diag[L] - S_lo[L - 1] @ UhT[L - 1]
+        Di = inv(Dt)
+        if L == 0:
+            D0 = Di
+        else:
+            FT[L - 1, :, :m] = Di
+            FT[L - 1, :, m:] = -(Di @ S_lo[L - 1])
+        UhT[L] = Di @ S_up[L]
+    for L in range(n - 1, k, -1):
+        i = L - (k + 1)
+        Et = S_diag[L] if L == n - 1 else S_diag[L] - S_up[L] @ UhB[i + 1]
+        Ei = inv(Et)
+        if L == n - 1:
+            E0 = Ei
+        else:
+            FB[i, :, :m] = Ei
+            FB[i, :, m:] = -(Ei @ S_up[L])
+        UhB[i] = Ei @ S_lo[L - 1]
+    Mi = inv(S_diag[k] - S_lo[k - 1] @ UhT[k - 1] - S_up[k] @ UhB[0])
+    FM = torch.cat((Mi, -(Mi @ S_lo[k - 1]), -(Mi @ S_up[k])), dim=1)
+    return k, D0, E0, FT, FB, FM, UhT, UhB
+
+
+def twisted_thomas_solve(op, g):
+    """x = S^-1 g from twisted_thomas_operators (g: (n, m), not modified).  Work rows W[L] = [g_L | s_L | t_L]:
+    a top line's slot s_L holds z_{L-1}, a bottom line's holds w_{L+1}, the middle line k holds z_{k-1} and
+    w_{k+1} (s_k, t_k), so every forward GEMV reads one contiguous 2m (middle: 3m) vector and writes its result
+    straight into the slot of the next line of its chain; each step of the two chains is ONE launch
+    (sem_gemv_rows2), the back substitution updates the slots in place.  Stream-capturable."""
+    k, D0, E0, FT, FB, FM, UhT, UhB = op
+    n, m = g.shape[0], g.shape[1]
+    W = torch.empty((n, 3 * m), dtype=g.dtype, device=g.device)
+    W[:, :m] = g
+    top = lambda L: W[L + 1, m:2 * m]                                        # noqa: E731  z_L, then x_L
+    bot = lambda L: W[k, 2 * m:] if L == k + 1 else W[L - 1, m:2 * m]        # noqa: E731  w_L, then x_L
+    x_k = torch.empty(m, dtype=g.dtype, device=g.device)
+    # forward: step 0 (D0 g_0, E0 g_{n-1}), then the chains side by side
+    _gemv2((D0, g[0], top(0)), (E0, g[n - 1], bot(n - 1)))
+    steps_t, steps_b = list(range(1, k)), list(range(n - 2, k, -1))
+    for j in range(max(len(steps_t), len(steps_b))):
+        pt = (FT[steps_t[j] - 1], W[steps_t[j], :2 * m], top(steps_t[j])) if j < len(steps_t) else None
+        pb = (FB[steps_b[j] - (k + 1)], W[steps_b[j], :2 * m], bot(steps_b[j])) if j < len(steps_b) else None
+        if pt and pb:
+            _gemv2(pt, pb)
+        else:
+            _gemv(*(pt or pb))
+    _gemv(FM, W[k], x_k)
+    # back: x_L = z_L - UhT_L x_{L+1} (L = k-1 .. 0) beside x_L = w_L - UhB_L x_{L-1} (L = k+1 .. n-1)
+    steps_t, steps_b = list(range(k - 1, -1, -1)), list(range(k + 1, n))
+    xt = lambda L: x_k if L == k else top(L)                                 # noqa: E731
+    for j in range(max(len(steps_t), len(steps_b))):
+        Lt = steps_t[j] if j < len(steps_t) else None
+        Lb = steps_b[j] if j < len(steps_b) else None
+        pt = (UhT[Lt], xt(Lt + 1), top(Lt)) if Lt is not None else None
+        pb = (UhB[Lb - (k + 1)], x_k if Lb - 1 == k else bot(Lb - 1), bot(Lb)) if Lb is not None else None
+        if pt and pb:
+            _gemv2(pt, pb, alpha=-1.0, beta=1.0)
+        else:
+            _gemv(*(pt or pb), alpha=-1.0, beta=1.0)
+    x = torch.empty((n, m), dtype=g.dtype, device=g.device)   # sem_nested_solve reads x_B as a packed (n, m) array
+    x[:k] = W[1:k + 1, m:2 * m]
+    x[k] = x_k
+    x[k + 1] = W[k, 2 * m:]
+    x[k + 2:] = W[k + 1:n - 1, m:2 * m]
+    return x
+
+
 def fused_thomas_solve(D0, F, Uh, g):
     """x = S^-1 g from fused_thomas_operators (g: (n, m), not modified).  W[L] = [g_L | z_{L-1}]: the
     forward GEMV of line L reads one contiguous 2m vector and writes z_L straight into W[L+1]'s second
@@ -278,6 +386,10 @@ class VelocityJacobianSolver:
         # same work arrays, sem_nested_back_solve) or "full" (the ABI-10 path: y_I formed, then a second nested
         # solve of b_I - A_IB x_B through Xi)
         self.nested_back = os.environ.get("SEM_NESTED_BACK", "coupled")
+        # block-Thomas interface sweep on the GPU: "twisted" (two-ended: the chains from line 0 and from line N_ex
+        # meet in the middle, one launch per step of both, twisted_thomas_solve) or "single" (one-ended, the
+        # fused forward operators of fused_thomas_operators)
+        self.sweep_form = os.environ.get("SEM_SWEEP_FORM", "twisted")
 
     @contextlib.contextmanager
     def _phase(self, name):
@@ -681,6 +793,13 @@ class VelocityJacobianSolver:
             self._cr_factor(S_diag, S_up, S_lo)
             self.factored = True
             return
+        self._tw = None
+        if self.sweep_form == "twisted" and self.device.type == "cuda" and nex + 1 >= 3:
+            # two-ended block Thomas (round 4): the same operator bytes, half the dependent launches
+            self._tw = twisted_thomas_operators(S_diag, S_up, S_lo)
+            self._th = self.Dinv = self.Uh = self.S_lo = None
+            self.factored = True
+            return
         # block Thomas on the interface lines: Dt[0] = S_diag[0], Uh[L] = Dt[L]^-1 S_up[L],
         # Dt[L+1] = S_diag[L+1] - S_lo[L] Uh[L]; explicit (pivoted) inverses of the pivot blocks
         Dinv = torch.empty((nex + 1, m, m), dtype=torch.float64, device=self.device)
@@ -908,6 +1027,8 @@ class VelocityJacobianSolver:
         """The interface system S xB = g (overwrites g)."""
         if self.sweep == "cr":
             return self._cr_solve(g)
+        if getattr(self, "_tw", None) is not None:
+            return twisted_thomas_solve(self._tw, g)
         if getattr(self, "_th", None) is not None:
             return fused_thomas_solve(*self._th, g)
         # block Thomas with the pivot blocks' explicit inverses: 2 GEMVs per line forward, 1 back

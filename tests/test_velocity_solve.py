@@ -148,3 +148,39 @@ def test_edge_thomas_falls_back_to_dense_inverses():
     want = spla.spsolve(ns.Jvelo.tocsc(), np.hstack((bu.numpy(), bv.numpy())))
     got = np.hstack([t.numpy() for t in ch.solve(bu, bv)])
     assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
+
+
+@pytest.mark.parametrize("n,m", [(3, 5), (4, 7), (5, 4), (9, 6), (12, 3), (13, 8)])
+def test_twisted_thomas_matches_dense_solve(n, m):
+    """The two-ended block-Thomas sweep (twisted_thomas_operators / twisted_thomas_solve: chains from line 0 and
+    from line n-1 meeting at n // 2, odd and even line counts) against a dense solve of the assembled
+    block-tridiagonal system, and against the one-ended fused sweep."""
+    from sem_amd.solvers.velocity_solve import (fused_thomas_operators, fused_thomas_solve, twisted_thomas_operators,
+                                                twisted_thomas_solve)
+    g = torch.Generator().manual_seed(n * 100 + m)
+    f64 = torch.float64
+    Sd = torch.rand((n, m, m), dtype=f64, generator=g) - 0.5 + 3 * m * torch.eye(m, dtype=f64)
+    Su = torch.rand((n - 1, m, m), dtype=f64, generator=g) - 0.5
+    Sl = torch.rand((n - 1, m, m), dtype=f64, generator=g) - 0.5
+    A = torch.zeros((n * m, n * m), dtype=f64)
+    for L in range(n):
+        A[L * m:(L + 1) * m, L * m:(L + 1) * m] = Sd[L]
+        if L < n - 1:
+            A[L * m:(L + 1) * m, (L + 1) * m:(L + 2) * m] = Su[L]
+            A[(L + 1) * m:(L + 2) * m, L * m:(L + 1) * m] = Sl[L]
+    rhs = torch.rand((n, m), dtype=f64, generator=g) - 0.5
+    want = torch.linalg.solve(A, rhs.reshape(-1)).reshape(n, m)
+    got = twisted_thomas_solve(twisted_thomas_operators(Sd, Su, Sl), rhs)
+    assert (got - want).abs().max().item() <= 1e-12 * want.abs().max().item()
+    # the one-ended sweep's operators from the same blocks
+    Dinv = torch.empty_like(Sd)
+    Uh = torch.empty_like(Su)
+    Dt = Sd[0]
+    for L in range(n):
+        if L > 0:
+            Dt = Sd[L] - Sl[L - 1] @ Uh[L - 1]
+        Dinv[L] = torch.linalg.inv(Dt)
+        if L < n - 1:
+            Uh[L] = Dinv[L] @ Su[L]
+    one = fused_thomas_solve(*fused_thomas_operators(Dinv, Sl, Uh), rhs)
+    assert (got - one).abs().max().item() <= 1e-12 * want.abs().max().item()

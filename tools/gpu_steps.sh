@@ -64,6 +64,11 @@ for s in "$@"; do
         python tools/cfg5_ns_probe.py --update 0
       python tools/pmc_compact.py "$O/cfg5trace" && python tools/prof_summary.py "$O/cfg5trace" "" > "$O/cfg5trace/prof_summary.txt" ;;
     vsolve)     step vsolve 600 python tools/vsolve_probe.py --out "$O/vsolve.json" ;;
+    sweepab)    # interface sweep A/B: one-ended against two-ended block Thomas, one process each, alternated
+      for rep in 1 2; do for f in single twisted; do
+        SEM_SWEEP_FORM=$f TAILN=1 step sweepab_${f}_$rep 300 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 \
+          --out "$O/sweepab_${f}_$rep.json"
+      done; done ;;
     vsolveab)   # interface-sweep GEMV A/B: the library's streaming GEMV (default) against rocBLAS, one process each
       SEM_SWEEP_GEMV=torch TAILN=2 step vsolve_rocblas 600 python tools/vsolve_probe.py --ab-edge 0 --out "$O/vsolve_rocblas.json"
       TAILN=2 step vsolve_hip 600 python tools/vsolve_probe.py --ab-edge 1 --out "$O/vsolve_hip.json" ;;

@@ -60,7 +60,13 @@ def account(vs, back=None):
     else:
         b["edge Schur inverses x2"] = 2 * nbytes(SeT)
     b["aIB + aBI"] = nbytes(vs.aIB) + nbytes(vs.aBI)
-    if getattr(vs, "_th", None) is not None:
+    if getattr(vs, "_tw", None) is not None:   # two-ended sweep
+        k, D0, E0, FT, FB, FM, UhT, UhB = vs._tw
+        b["sweep FT_L + FB_L (m x 2m)"] = nbytes(FT) + nbytes(FB)
+        b["sweep FM (m x 3m, middle line)"] = nbytes(FM)
+        b["sweep UhT_L + UhB_L (m x m)"] = nbytes(UhT) + nbytes(UhB)
+        b["sweep D0 + E0"] = nbytes(D0) + nbytes(E0)
+    elif getattr(vs, "_th", None) is not None:
         D0, F, Uh = vs._th
         b["sweep F_L (m x 2m)"] = nbytes(F)
         b["sweep Uh_L (m x m)"] = nbytes(Uh)
@@ -104,7 +110,7 @@ def main():
     torch.cuda.synchronize(dev)
     out = {"config": f"velocity solve {args.ne}x{args.ne} P={args.P}", "N": N, "factor_s": time.perf_counter() - t0,
            "resident_GB": torch.cuda.memory_allocated(dev) / 1e9, "edge_thomas": bool(vs._edge_thomas),
-           "sweep": vs.sweep, "graph": getattr(vs, "_graph", None) is not None}
+           "sweep": vs.sweep, "sweep_form": vs.sweep_form, "graph": getattr(vs, "_graph", None) is not None}
     bu, bv = (ns._dev(r.uniform(-1, 1, N)) for _ in range(2))
 
     def timed():
