@@ -37,6 +37,8 @@ for s in "$@"; do
     batchedinv) step batchedinv 300 $PYT tests/test_batched_inverse.py tests/test_gpu_dense_inverse.py ;;
     smoke)      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)      step bench 600 python bench.py ;;
+    benchdrv)   step benchdrv 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;   # the driver's command
+    pmccd64)    tools/pmc_run.sh "$O/pmc_cd64" -- python tools/kbench.py --meshes 8:64 --reps 200 || exit 1 ;;
     inv)        step inv 300 python tools/inv_repro.py ;;
     nsbench)    step nsbench 300 python tools/nsbench.py ;;
     pivot)      step pivot 300 python tools/pivot_probe.py ;;
@@ -95,6 +97,12 @@ for s in "$@"; do
         SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_BAND_KP=$kp SEM_DIAG=$d \
           step bandlab_kp${kp}_d$d 120 python tools/kbench.py --meshes 8:64 --reps 1000
       done; done ;;
+    stamps)     # cfg2 per-wave phase stamps and per-tile realtime start/end (diagnostic build, struct-argument kernel)
+      for rep in 1 2; do
+        SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_BAND_KP=0 SEM_DIAG=8 SEM_DIAG_BUF=auto TAILN=30 \
+          step stamps_$rep 120 python tools/kbench.py --meshes 8:64 --stamps --nstamps 6 --stride 16 \
+          --roles X:0-1,Y:2-3 --tiles-x 65 --tiles-y 9
+      done ;;
     kbench)     TAILN=4 step kbench 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 1000 ;;
     bandtests)  step bandtests 600 $PYT tests/test_gpu_apply.py tests/test_gpu_partition.py ;;
     orderab)    # band tile order A/B: full tiles first (0) against the round-3 order (1), alternated, one process each
