@@ -37,6 +37,13 @@ for s in "$@"; do
     batchedinv) step batchedinv 300 $PYT tests/test_batched_inverse.py tests/test_gpu_dense_inverse.py ;;
     smoke)      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)      step bench 600 python bench.py ;;
+    benchgloo)  # the N > 1 bench path (strip partition, interface exchange, max-over-ranks timing) rehearsed with
+                # several ranks on one GPU over gloo (RCCL needs one GPU per rank); all-reduce and p2p exchanges
+      for nr in 2 4; do for ex in allreduce p2p; do
+        step benchgloo_${nr}_$ex 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $nr \
+          --master-addr 127.0.0.1 --master-port 2962$nr bench.py --gpus $nr --steps 20 --warmup 5 \
+          --dist-backend gloo --exchange $ex --cpu-seconds 0 --hbm-ne 0
+      done; done ;;
     benchdrv)   step benchdrv 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;   # the driver's command
     pmccd64)    tools/pmc_run.sh "$O/pmc_cd64" -- python tools/kbench.py --meshes 8:64 --reps 200 || exit 1 ;;
     inv)        step inv 300 python tools/inv_repro.py ;;
