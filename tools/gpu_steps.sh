@@ -119,6 +119,10 @@ for s in "$@"; do
     schurab)    TAILN=4 step schurab 900 python tools/schur_ab.py --out "$O/schur_ab.jsonl" ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
+    cfg4part)   # the element-partitioned coupled solve end to end at cfg4's size (48^2, P=8): 4 ranks on one GPU, gloo
+      step cfg4part 1000 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29613 tools/bous_cfg5_solve.py --backend gloo --ne 48 --P 8 --Ra 1e3 --out "$O/cfg4_part4_ra1e3.json" ;;
+    cfg4whole)  step cfg4whole 300 python tools/bous_cfg5_solve.py --ne 48 --P 8 --Ra 1e3 --out "$O/cfg4_whole_ra1e3.json" ;;
     cfg5part)   # rehearsal of cfg5's element-partitioned coupled solve: 4 ranks on one GPU over gloo, Ra = 1e3 from rest
       step cfg5part 1080 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
         --master-port 29611 tools/bous_cfg5_solve.py --backend gloo --Ra 1e3 --out "$O/cfg5_part4_ra1e3.json" ;;
