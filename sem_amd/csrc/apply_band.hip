@@ -483,7 +483,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // Diagnostics (SEM_DIAG bit 8): s_memtime phase stamps held in SGPRs, written at the very end
   // so that no diagnostic store sits in the vmcnt queue of the measured phases.
-  unsigned long long stv[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0, rt1 = 0;
+  unsigned long long stv[7] = {0, 0, 0, 0, 0, 0, 0}, rt0 = 0, rt1 = 0;  // stv[6]: epilogue values formed (slot 10)
   if (kDiag && !KP && a.stamps) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
 #define BSTAMP(k)                                                                      \
   do {                                                                                 \
@@ -684,6 +684,7 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
       zz[e] = finish_node<FULL>(a, ops[e], gx0 + r, gy0 + c, xv, z);
     }
   }
+  BSTAMP(6);
 #pragma unroll
   for (int e = 0; e < C::NE; ++e) {
     const int q = tid + e * C::THREADS;
@@ -695,9 +696,11 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1)::"memory");
     unsigned xcc_, hw_;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)" : "=s"(xcc_), "=s"(hw_));
-    if (lane == 0) {  // 16 slots per wave: 0-5 s_memtime phases, 6 tile, 7 hw id, 8-9 s_memrealtime start/end
+    if (lane == 0) {  // 16 slots per wave: 0-5 s_memtime phases, 6 tile, 7 hw id, 8-9 s_memrealtime start/end,
+                      // 10 epilogue values formed (before the stores)
       unsigned long long* o = a.stamps + (blockIdx.x * C::NW + w) * 16;
       for (int k = 0; k < 6; ++k) o[k] = stv[k];
+      o[10] = stv[6];
       o[6] = L;
       o[7] = (static_cast<unsigned long long>(hw_) << 8) | (xcc_ & 0xf);
       o[8] = rt0;

@@ -99,6 +99,10 @@ def main():
         for k in range(1, ns):
             d = st[:, k] - st[:, k - 1]
             print(f"  phase s{k-1}->s{k}: med {int(np.median(d)):7d}  p90 {int(np.percentile(d, 90)):7d}")
+        if a.stride >= 16 and (st[:, 10] > 0).any():   # band kernel slot 10: epilogue values formed, before the stores
+            d1, d2 = st[:, 10] - st[:, 4], st[:, 5] - st[:, 10]
+            print(f"  epilogue: s4->values formed med {int(np.median(d1))} p90 {int(np.percentile(d1, 90))}; "
+                  f"stores issued med {int(np.median(d2))} p90 {int(np.percentile(d2, 90))}")
         last = ns - 1
         # per-XCD view (each XCD has its own clock): dispatch ramp, wave span, active window
         xcc = st[:, 7] & 0xF
