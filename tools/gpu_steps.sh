@@ -98,6 +98,12 @@ for s in "$@"; do
       TAILN=40 step vsolvetr_window 120 python tools/trace_window.py "$O/vsolvetr" 20 cond_fwd_kernel 1 \
         --save "$O/vsolvetr/window_20_solves.csv"
       find "$O/vsolvetr" -name "*kernel_trace.csv" -delete ;;
+    vsolvepmc)  # FETCH_SIZE / WRITE_SIZE of the default velocity solve (one pass each, no tracing domains)
+      step vsolvepmc_fetch 600 timeout -s KILL 580 rocprofv3 --pmc FETCH_SIZE -d "$O/vsolvepmc1" -o pmc --output-format csv -- \
+        python tools/vsolve_probe.py --ab-edge 0 --ab-back 0
+      step vsolvepmc_write 600 timeout -s KILL 580 rocprofv3 --pmc WRITE_SIZE -d "$O/vsolvepmc2" -o pmc --output-format csv -- \
+        python tools/vsolve_probe.py --ab-edge 0 --ab-back 0
+      python tools/pmc_compact.py "$O/vsolvepmc1" && python tools/pmc_compact.py "$O/vsolvepmc2" ;;
     bandlab)    # cfg2 latency anatomy: diagnostic ablations (sem_amd/lib_diag) and the trivial-kernel floor
       step dispatch 120 tools/dispatch_bench
       for kp in 0 -1; do for d in 0 16 32 48 112; do
