@@ -371,6 +371,13 @@ int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, cons
 int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, int64_t lda0, const double* x0,
                    double* y0, int K1, const double* A1, int64_t lda1, const double* x1, double* y1, void* stream);
 
+/* ---- GMRES least-squares column (host) ------------------------------------ */
+/* Host memory, no device work (ABI 11): applies the Givens rotations 0..k-1 (cs, sn) to col[0..k+1], forms
+ * rotation k from (col[k], col[k+1]) into cs[k], sn[k], applies it to col and to the rotated right-hand side
+ * g[k], g[k+1] -- one Arnoldi step's update of the device GMRES (sem_amd/krylov.py), the host half of the
+ * Krylov solves that replace the reference's LGMRES (NavierStokes_Solver.py:197-229). */
+int sem_givens_column(double* col, double* cs, double* sn, double* g, int k);
+
 /* ---- small dense inverse (leaves of the sweep's pivot inverses) --------- */
 /* X = A^-1 for one n x n row-major block, n <= 64 (row r of A at A + r lda, of X at X + r ldx; device
  * memory; X must not overlap A): Gauss-Jordan elimination with partial pivoting in one workgroup (ABI 8).

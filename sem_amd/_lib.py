@@ -110,6 +110,7 @@ _SIGS = {
     "sem_block_gemv": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p), _i64p, C.c_void_p,
                                  C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p]),
     "sem_dense_inverse_small": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_void_p]),
+    "sem_givens_column": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "sem_gemv_rows2": (C.c_int, [C.c_int, C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
                                  C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sem_gemv_rows": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_int64, C.c_void_p, C.c_double,

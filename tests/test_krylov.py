@@ -155,3 +155,26 @@ def test_strip_solver_never_captures_over_host_collectives():
     vs = StripLineSolver(4, 4, 2, "cpu", [0, 2, 4], 0, dist=None, gather_device="cpu")
     vs.factored = True
     assert vs.capture() is False
+
+
+def test_givens_column_c_matches_python_loop():
+    """sem_givens_column (the library's host code) applies the same rotations in the same order as the Python loop
+    it replaced: equal results on a sequence of columns, to the last bit except through hypot (one rounding)."""
+    import sem_amd.krylov as K
+    rng = np.random.default_rng(3)
+    n = 60
+    cs_c, sn_c, g_c = np.zeros(n), np.zeros(n), np.zeros(n + 1)
+    cs_p, sn_p, g_p = np.zeros(n), np.zeros(n), np.zeros(n + 1)
+    g_c[0] = g_p[0] = 1.7
+    K.givens_column(np.ones(2), np.zeros(1), np.zeros(1), np.zeros(2), 0)   # loads the library once
+    saved = list(K._GIVENS)
+    for k in range(n):
+        col = rng.standard_normal(k + 2)
+        c1, c2 = col.copy(), col.copy()
+        K.givens_column(c1, cs_c, sn_c, g_c, k)
+        K._GIVENS[:] = [None]          # the interpreter fallback
+        K.givens_column(c2, cs_p, sn_p, g_p, k)
+        K._GIVENS[:] = saved
+        assert np.allclose(c1, c2, rtol=1e-14, atol=1e-15)
+    assert saved and saved[0] is not None   # the C path was the one under test
+    assert np.allclose(g_c, g_p, rtol=1e-13, atol=1e-300) and np.allclose(cs_c, cs_p, rtol=1e-14)

@@ -123,6 +123,8 @@ for s in "$@"; do
         SEM_BAND_ORDER=$o TAILN=2 step orderab_${o}_$rep 120 python tools/kbench.py --meshes 8:64,8:256 --reps 2000
       done; done ;;
     schurab)    TAILN=4 step schurab 900 python tools/schur_ab.py --out "$O/schur_ab.jsonl" ;;
+    schurmass)  TAILN=4 step schurmass 300 python tools/schur_ab.py --precond mass --out "$O/schur_mass.jsonl" ;;
+    krylovgpu)  step krylovgpu 300 $PYT tests/test_gpu_krylov.py tests/test_gpu_cfg4.py ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
                   --out "$O/cfg5_ra1e4.json" ;;
     cfg4part)   # the element-partitioned coupled solve end to end at cfg4's size (48^2, P=8): 4 ranks on one GPU, gloo
