@@ -19,6 +19,7 @@ rotations) runs on the host.  Vectors are torch tensors on any device, so the
 algorithm is unit-tested on CPU against SciPy.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -155,6 +156,11 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     Z = torch.empty((restart, N), dtype=dt, device=dev) if precond is not None else None
     total, matvecs = 0, 0
     self_reorth = [0]
+    # pipelined steps on one GPU (SEM_GMRES_PIPELINE=1; off by default until measured on MI355X): a pinned host
+    # buffer for each step's coefficients and norms, and the event that marks its copy
+    pipe = None
+    if sweeps is not None and os.environ.get("SEM_GMRES_PIPELINE", "0") == "1":
+        pipe = (torch.empty(restart + 3, dtype=torch.float64, pin_memory=True), torch.cuda.Event())
     r = b - matvec(x) if x0 is not None else b.clone()
     matvecs += x0 is not None
     beta = vnorm(r)
@@ -172,13 +178,17 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
         g = np.zeros(restart + 1)
         g[0] = beta
         k_done = 0
+        pending = None   # the next step's A M^-1 v_{k+1}, launched before this step's host synchronisation
         for k in range(restart):
-            zk = precond(V[k]) if precond is not None else V[k]
-            if Z is not None:
-                Z[k] = zk
-            w = matvec(zk)
+            if pending is None:
+                zk = precond(V[k]) if precond is not None else V[k]
+                if Z is not None:
+                    Z[k] = zk
+                w = matvec(zk)
+                matvecs += 1
+            else:
+                w, pending = pending, None
             w_in = w
-            matvecs += 1
             Vk = V[:k + 1]
             # CGS2 in three sweeps over the basis instead of four: the second pass's coefficients
             # V^T (w - V h) = (I - G) h come from the basis' Gram matrix G = V^T V, whose new row
@@ -198,7 +208,30 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
                 sweeps.update(k + 1, hh.contiguous(), w)
             else:
                 w = w - Vk.T @ hh
-            if inner is None:   # one device -> host transfer per step: coefficients, ||w|| after and before
+            spec = None
+            if pipe is not None:
+                # pipelined step (device, one GPU): the coefficients and norms go to pinned host memory, then
+                # v_{k+1} = w / ||w|| and the next matvec are queued BEFORE the host waits for that copy, so the
+                # GPU runs the next operator application while the host does this step's least-squares update;
+                # the speculation is dropped on convergence (one extra matvec) and redone after a
+                # reorthogonalisation (which changes w)
+                nw = torch.linalg.vector_norm(w)
+                pk = torch.cat((hh, nw[None], torch.linalg.vector_norm(w_in)[None]))
+                pipe[0][:k + 3].copy_(pk, non_blocking=True)
+                pipe[1].record()
+                if k + 1 < restart and total + 1 < maxiter:
+                    V[k + 1] = w / nw
+                    z1 = precond(V[k + 1]) if precond is not None else V[k + 1]
+                    if Z is not None:
+                        Z[k + 1] = z1
+                    spec = matvec(z1)
+                    matvecs += 1
+                pipe[1].synchronize()
+                cn = pipe[0][:k + 3].numpy().copy()
+                h0 = float(cn[-1])
+                col = cn[:-1]
+                hn = float(col[-1])
+            elif inner is None:   # one device -> host transfer per step: coefficients, ||w|| after and before
                 cn = _host64(torch.cat((hh, torch.linalg.vector_norm(w)[None], torch.linalg.vector_norm(w_in)[None])))
                 h0 = float(cn[-1])
                 col = cn[:-1]
@@ -222,6 +255,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
                 col[:k + 1] += _host64(h2)
                 col[k + 1] = hn
                 self_reorth[0] += 1
+                spec = None       # v_{k+1} and the speculative matvec came from the unreorthogonalised w
             givens_column(col, cs, sn, g, k)   # earlier rotations, the new one, the right-hand side
             H[:k + 2, k] = col
             total += 1
@@ -231,7 +265,10 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
                 callback(est)
             if est <= tol or hn == 0.0 or total >= maxiter:
                 break
-            V[k + 1] = w / hn
+            if spec is not None:
+                pending = spec    # V[k+1], Z[k+1] and A Z[k+1] are already on the device
+            else:
+                V[k + 1] = w / hn
         if basis_out is not None:
             basis_out.append(V[:k_done].clone())
         # x += Z y  with  H[:k,:k] y = g[:k]
