@@ -123,6 +123,11 @@ for s in "$@"; do
         SEM_BAND_ORDER=$o TAILN=2 step orderab_${o}_$rep 120 python tools/kbench.py --meshes 8:64,8:256 --reps 2000
       done; done ;;
     schurab)    TAILN=4 step schurab 900 python tools/schur_ab.py --out "$O/schur_ab.jsonl" ;;
+    schurpipe)  # device GMRES pipelined step A/B at cfg4's Ra = 1e6 block solve, one process each, alternated
+      for rep in 1 2; do for pp in 0 1; do
+        SEM_GMRES_PIPELINE=$pp TAILN=2 step schurpipe_${pp}_$rep 300 python tools/schur_ab.py --precond mass \
+          --out "$O/schurpipe_${pp}_$rep.jsonl"
+      done; done ;;
     schurmass)  TAILN=4 step schurmass 300 python tools/schur_ab.py --precond mass --out "$O/schur_mass.jsonl" ;;
     krylovgpu)  step krylovgpu 300 $PYT tests/test_gpu_krylov.py tests/test_gpu_cfg4.py ;;
     cfg5solve)  step cfg5solve 1000 python -u tools/bous_cfg5_solve.py --continuation 1e3 --Ra 1e4 \
