@@ -156,10 +156,11 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     Z = torch.empty((restart, N), dtype=dt, device=dev) if precond is not None else None
     total, matvecs = 0, 0
     self_reorth = [0]
-    # pipelined steps on one GPU (SEM_GMRES_PIPELINE=1; off by default until measured on MI355X): a pinned host
-    # buffer for each step's coefficients and norms, and the event that marks its copy
+    # pipelined steps on one GPU (SEM_GMRES_PIPELINE=0 turns them off; cfg4's Ra = 1e6 block solve 0.744 ->
+    # 0.715 s, profiles/r04/schur_ab/schurpipe_*.jsonl): a pinned host buffer for each step's coefficients and
+    # norms, and the event that marks its copy
     pipe = None
-    if sweeps is not None and os.environ.get("SEM_GMRES_PIPELINE", "0") == "1":
+    if sweeps is not None and os.environ.get("SEM_GMRES_PIPELINE", "1") != "0":
         pipe = (torch.empty(restart + 3, dtype=torch.float64, pin_memory=True), torch.cuda.Event())
     r = b - matvec(x) if x0 is not None else b.clone()
     matvecs += x0 is not None
