@@ -125,7 +125,7 @@ def givens_column(col, cs, sn, g, k):
 
 
 def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, precond=None, callback=None,
-          inner=None, basis_out=None):
+          inner=None, basis_out=None, linear_precond=True):
     """Right-preconditioned restarted GMRES.
 
     matvec(v) -> A v and precond(v) -> M^-1 v take and return 1-D tensors like b.
@@ -135,6 +135,9 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     sem_amd.parallel.DistributedInner, so every rank sees the same Hessenberg entries and takes the
     same path through the iteration.
     basis_out: a list that receives a copy of each cycle's orthonormal basis (tests).
+    linear_precond: precond is a fixed linear map (the solvers' mass diagonal, PCD and direct solves), so the
+    correction is M^-1 (V y) and the preconditioned basis Z = M^-1 V is not kept -- half the basis memory, and
+    twice the vectors within a memory budget; False keeps Z (flexible GMRES, for a varying preconditioner).
     """
     proj = inner if inner is not None else (lambda A, w: A @ w)
 
@@ -153,7 +156,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     G = torch.zeros((restart + 1, restart + 1), dtype=dt, device=dev)  # Gram matrix V^T V of the basis
     # the HIP sweeps read and write doubles: other dtypes take torch's GEMV route
     sweeps = _DeviceSweeps(V) if (inner is None and V.is_cuda and V.dtype == torch.float64) else None
-    Z = torch.empty((restart, N), dtype=dt, device=dev) if precond is not None else None
+    Z = torch.empty((restart, N), dtype=dt, device=dev) if (precond is not None and not linear_precond) else None
     total, matvecs = 0, 0
     self_reorth = [0]
     # pipelined steps on one GPU (SEM_GMRES_PIPELINE=0 turns them off; cfg4's Ra = 1e6 block solve 0.744 ->
@@ -267,16 +270,20 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             if est <= tol or hn == 0.0 or total >= maxiter:
                 break
             if spec is not None:
-                pending = spec    # V[k+1], Z[k+1] and A Z[k+1] are already on the device
+                pending = spec    # V[k+1] and A M^-1 V[k+1] (and Z[k+1]) are already on the device
             else:
                 V[k + 1] = w / hn
         if basis_out is not None:
             basis_out.append(V[:k_done].clone())
-        # x += Z y  with  H[:k,:k] y = g[:k]
+        # x += Z y (= M^-1 V y for a linear preconditioner)  with  H[:k,:k] y = g[:k]
         y = np.linalg.solve(np.triu(H[:k_done, :k_done]), np.asarray(g[:k_done])) if k_done else np.zeros(0)
         yt = torch.as_tensor(y, dtype=dt, device=dev)
-        basis = Z[:k_done] if Z is not None else V[:k_done]
-        x = x + basis.T @ yt
+        if Z is not None:
+            x = x + Z[:k_done].T @ yt
+        elif precond is not None:
+            x = x + precond(V[:k_done].T @ yt)
+        else:
+            x = x + V[:k_done].T @ yt
         r = b - matvec(x)
         matvecs += 1
         beta = vnorm(r)

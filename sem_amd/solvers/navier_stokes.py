@@ -488,6 +488,9 @@ class NavierStokesSolver:
         # 32 GB: unrestarted up to max_basis on cfg3/cfg4, restarted at 846 vectors on a whole-mesh cfg5
         # solver (N = 1537^2 = 2.36 M; 31.9 GB).  The velocity factor, the Schur graph's buffers and
         # the Hessenberg matrix come on top of this budget.
+        # restart within 16 bytes per DOF per vector (847 at cfg5): twice that (V only, as krylov.gmres keeps no
+        # M^-1 V for the linear mass-diagonal preconditioner) measured no faster at cfg5 -- fewer iterations in the
+        # long first solves, each dearer (profiles/r04/cfg5/cfg5_restart1694.json)
         restart = max(1, min(self.N, self._max_basis, int(32e9 // (16 * self.N))))
         if self._recycle_bytes and self._schur_recycle is None:
             cap = min(self.N, max(restart + 1, int(self._recycle_bytes // (16 * self.N))))
