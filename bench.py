@@ -14,8 +14,11 @@ rank holds one element-column strip and every step assembles the interface lines
 with the two neighbours), overlapped with the interior apply (--overlap 1: the
 strip's two interface positions are applied first, the exchange is started, the
 interior positions are applied while it runs).
-  --scaling weak   (default) a 64-element-column strip per rank of a (64 N) x 64 mesh
-  --scaling strong the 64 x 64 mesh (--ne) split into N strips (BASELINE.md's strong-scaling plan)
+  --scaling strong (default) the --ne x --ne mesh (64 x 64: BASELINE configs[1]) split into N strips -- north_star's
+                   "Ne x Ne, P=8 mesh at 1, 2, 4 and 8 GPUs" and BASELINE.md's strong-scaling plan; at N > 1 the
+                   line also carries `strong_hbm` (the 1024 x 1024 mesh split into N strips: the HBM regime) and
+                   `weak` (a 64-element-column strip per rank of a (64 N) x 64 mesh)
+  --scaling weak   the weak-scaling mesh as the headline instead
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N bench.py --gpus N ...
@@ -52,8 +55,10 @@ def parse():
     ap.add_argument("--hbm-ne", type=int, default=1024, help="HBM-regime mesh size (0 = skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the measured path); gloo only to rehearse N > 1 on a 1-GPU box")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: --ne x --ne elements per GPU; strong: --ne x --ne elements over all GPUs")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong: --ne x --ne elements over all GPUs; weak: --ne x --ne elements per GPU")
+    ap.add_argument("--extra-steps", type=int, default=100,
+                    help="N > 1: steps timed for the strong_hbm and weak extra keys (0 = skip them)")
     ap.add_argument("--overlap", type=int, default=1, help="N > 1: overlap the interface exchange with the interior")
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "p2p"],
                     help="interface assembly for N > 1: one RCCL all-reduce, or send/recv with the two neighbours")
@@ -246,40 +251,47 @@ def main():
     from sem_amd.parallel import StripApply, StripPartition
 
     P, ne, Pe = args.P, args.ne, args.Pe
+
+    def strip_case(nex, ney, d, steps, warmup, seed):
+        """Build this rank's strip of an nex x ney mesh and time `steps` partitioned applies (apply + interface
+        exchange).  Returns (seconds max-reduced over ranks, graph used, mesh, operands)."""
+        part = StripPartition(nex, world)
+        eb, ee = part.bounds[rank], part.bounds[rank + 1]
+        mesh = get_mesh(P, nex, ney, d, d, eb, ee, dev.index)
+        T, u, v = make_inputs(mesh, seed=seed)
+        y = torch.empty_like(T)
+        sides = _lib.SIDE_W | _lib.SIDE_E
+        kw = dict(c_stiff=1.0, c_gradx=Pe, cu=u, c_grady=Pe, cv=v, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides)
+        strip = StripApply(part, mesh, dist, kind=args.exchange, overlap=bool(args.overlap)) if world > 1 else None
+
+        def step():
+            if strip is None:
+                mesh.apply(T, y, **kw)
+            else:
+                strip(T, y, **kw)
+
+        # N > 1 over RCCL: the whole step (apply, pack, RCCL all-reduce or send/recv, unpack) is captured
+        # too -- RCCL collectives are stream-capturable -- so the per-step host cost (four launches and a
+        # collective call from Python) leaves the timed loop; gloo collectives are host-side and cannot be.
+        use_graph = bool(args.graph) and (world == 1 or args.dist_backend == "nccl")
+        try:
+            secs, _ = time_steps(step, steps, warmup, dev, use_graph=use_graph, dist=dist)
+        except RuntimeError as exc:  # capture refused: time the same steps eagerly
+            if not use_graph or world == 1:
+                raise
+            print(f"[bench] rank {rank}: hipGraph capture of the exchange failed ({exc}); timing eagerly",
+                  file=sys.stderr, flush=True)
+            use_graph = False
+            secs, _ = time_steps(step, steps, 0, dev, use_graph=False, dist=dist)
+        if dist is not None:
+            t = torch.tensor([secs], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            secs = float(t.item())
+        return secs, use_graph, mesh, (T, y, kw), (eb, ee)
+
     nex, ney = (ne * world, ne) if args.scaling == "weak" else (ne, ne)
     d = 1.0 / ne
-    part = StripPartition(nex, world)
-    eb, ee = part.bounds[rank], part.bounds[rank + 1]
-    mesh = get_mesh(P, nex, ney, d, d, eb, ee, dev.index)
-    T, u, v = make_inputs(mesh, seed=2024 + rank)
-    y = torch.empty_like(T)
-    sides = _lib.SIDE_W | _lib.SIDE_E
-    kw = dict(c_stiff=1.0, c_gradx=Pe, cu=u, c_grady=Pe, cv=v, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides)
-    strip = StripApply(part, mesh, dist, kind=args.exchange, overlap=bool(args.overlap)) if world > 1 else None
-
-    def step():
-        if strip is None:
-            mesh.apply(T, y, **kw)
-        else:
-            strip(T, y, **kw)
-
-    # N > 1 over RCCL: the whole step (apply, pack, RCCL all-reduce or send/recv, unpack) is captured
-    # too -- RCCL collectives are stream-capturable -- so the per-step host cost (four launches and a
-    # collective call from Python) leaves the timed loop; gloo collectives are host-side and cannot be.
-    use_graph = bool(args.graph) and (world == 1 or args.dist_backend == "nccl")
-    try:
-        secs, wall = time_steps(step, args.steps, args.warmup, dev, use_graph=use_graph, dist=dist)
-    except RuntimeError as exc:  # capture refused: time the same steps eagerly
-        if not use_graph or world == 1:
-            raise
-        print(f"[bench] rank {rank}: hipGraph capture of the exchange failed ({exc}); timing eagerly",
-              file=sys.stderr, flush=True)
-        use_graph = False
-        secs, wall = time_steps(step, args.steps, 0, dev, use_graph=False, dist=dist)
-    if dist is not None:
-        t = torch.tensor([secs], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        secs = float(t.item())
+    secs, use_graph, mesh, (T, y, kw), (eb, ee) = strip_case(nex, ney, d, args.steps, args.warmup, 2024 + rank)
     N_glob = (nex * P + 1) * (ney * P + 1)
     value = N_glob * args.steps / secs
     ms = secs / args.steps * 1e3
@@ -299,8 +311,18 @@ def main():
         kern_s = k_secs / args.steps
     g1000_us = graph_kernel_us(apply_only, dev)
     achieved = bytes_launch / kern_s / 1e9
-    workload = f"cd_matvec_{ne}x{ne}_P{P}"
-    traffic, traffic_kernel = load_pmc(workload, mesh.kernel_name())
+    workload = f"cd_matvec_{nex}x{ney}_P{P}"
+    # PMC traffic was measured on the whole-mesh kernel: a strip launch is another workload
+    traffic, traffic_kernel = load_pmc(workload, mesh.kernel_name()) if world == 1 else (None, None)
+
+    def regime(n_rank, latency=False):
+        mb = 32.0 * n_rank / 1e6
+        r = (f"HBM ({mb:.0f} MB moved per apply per GPU, beyond the 256 MB MALL)" if mb > 256 else
+             f"L2/MALL-resident ({mb:.1f} MB working set per GPU)")
+        if latency:
+            r += ("; latency-bound: the per-rank apply (a few us) is shorter than the interface exchange "
+                  "(small-message collective latency), so strong scaling of this mesh cannot be linear")
+        return r
     out = {
         "metric": BASELINE_METRIC,
         "work": "y = K T + Pe (u.Gx T + v.Gy T), Dirichlet identity rows on x=0,1: the Laplacian+convection "
@@ -319,7 +341,7 @@ def main():
                        + (", overlapped with the interior apply" if args.overlap else "")
                        + (" (RCCL)" if args.dist_backend == "nccl" else " (gloo rehearsal)")
                        if world > 1 else ""),
-                   "regime": "L2/MALL-resident (8.4 MB working set per GPU)", "hipgraph": use_graph},
+                   "regime": regime(n_loc, latency=world > 1 and 32.0 * n_loc < 256e6), "hipgraph": use_graph},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_kernel": traffic_kernel,
                      "kernel": mesh.kernel_name(), "bytes_per_launch": bytes_launch,
@@ -364,6 +386,27 @@ def main():
                                "frac": bb / kb / 1e9 / HBM_PEAK_GBS, "traffic": tb, "traffic_kernel": tbk,
                                "kernel_us": kb * 1e6}
         del Tb, ub, vb, yb
+
+    if world > 1 and args.extra_steps > 0:
+        # the other meshes per rank count (north_star: absolute numbers at 1, 2, 4 and 8 GPUs): the HBM-regime mesh
+        # split into N strips, and the weak-scaling mesh (or, with --scaling weak, the strong one)
+        def extra(nex_, ney_, d_, seed, latency):
+            es, eg, em, _, (eb_, ee_) = strip_case(nex_, ney_, d_, args.extra_steps, min(args.warmup, 10), seed)
+            Ng = (nex_ * P + 1) * (ney_ * P + 1)
+            r = {"global_mesh": f"{nex_}x{ney_}", "mesh_per_gpu": f"{ee_ - eb_}x{ney_} elements (rank 0)",
+                 "dofs_global": Ng, "value": Ng * args.extra_steps / es, "unit": "DOF-updates/s",
+                 "ms_per_step": es / args.extra_steps * 1e3, "steps": args.extra_steps, "hipgraph": eg,
+                 "regime": regime(em.n_local, latency),
+                 "rank0_bw_GBs": 32.0 * em.n_local / (es / args.extra_steps) / 1e9}
+            return r
+        if args.hbm_ne > 0:
+            out["strong_hbm"] = dict(extra(args.hbm_ne, args.hbm_ne, 1.0 / args.hbm_ne, 4048 + rank, False),
+                                     scaling="strong")
+            torch.cuda.empty_cache()
+        if args.scaling == "strong":
+            out["weak"] = dict(extra(ne * world, ne, d, 2024 + rank, True), scaling="weak")
+        else:
+            out["strong"] = dict(extra(ne, ne, d, 2024 + rank, True), scaling="strong")
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(P, ne, Pe, args.cpu_seconds)

@@ -1044,8 +1044,12 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   // element positions [pos0, pos1) of 0..ncols (ncols = the ghost position of the closing line)
   const bool ranged = g.pos1 > 0;
   const int pos0 = ranged ? g.pos0 : 0, pos1 = ranged ? g.pos1 : ncols + 1;
-  const int tiles_x = (pos1 - pos0 + TXE - 1) / TXE;
-  const int tiles_y = (h->ney + 1 + TYE - 1) / TYE;
+  // diagnostic bit 128 (diagnostic builds only; WRONG results on the closing line and column): the ghost tiles
+  // are not launched, so the grid is the full tiles alone (512 equal workgroups at cfg2, two per CU) -- the
+  // upper bound of what folding the closing line / column into the last full tiles could gain
+  const bool skip_ghost = kDiag && (g.diag & 128) && !ranged;
+  const int tiles_x = (pos1 - pos0 + TXE - 1) / TXE - (skip_ghost ? 1 : 0);
+  const int tiles_y = (h->ney + 1 + TYE - 1) / TYE - (skip_ghost ? 1 : 0);
   const long long nblk = static_cast<long long>(tiles_x) * tiles_y;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
   BandArgs b{};

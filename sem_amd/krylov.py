@@ -24,23 +24,30 @@ import os
 import numpy as np
 import torch
 
+from . import tracing
+from .tracing import phase
+
 
 class _DeviceSweeps:
     """The two basis passes of an Arnoldi step as HIP kernels (include/sem_ops.h: sem_basis_dot2,
     sem_basis_update): one HBM pass over the basis each, instead of torch's GEMV / skinny-GEMM
-    routes.  Used for device tensors without a distributed inner product."""
+    routes.  `segments`: the entries this rank owns (a partitioned vector's shared interface line is
+    counted on one rank only); dot2 runs over those ranges -- pointer offsets into V, a and b, no mask
+    -- and the update over the whole local vector."""
 
-    def __init__(self, V):
+    def __init__(self, V, segments=None):
         if V.dtype != torch.float64 or not V.is_cuda or V.stride(1) != 1:
             raise ValueError("the HIP basis sweeps need a float64 device basis with unit column stride")
         from . import _lib
         self.lib = _lib.load()
         self.check = _lib.check
         self.V, self.ldv = V, V.stride(0)
+        n = V.shape[1]
+        self.segments = [(0, n)] if segments is None else [(int(a), int(b)) for a, b in segments if b > a]
         rows = V.shape[0]
-        self.out = torch.empty((rows, 2), dtype=V.dtype, device=V.device)
-        self.work = torch.empty(max(1, self.lib.sem_basis_dot2_work_size(rows, V.shape[1])), dtype=V.dtype,
-                                device=V.device)
+        self.out = torch.empty((len(self.segments), rows, 2), dtype=V.dtype, device=V.device)
+        self.work = torch.empty(max(1, max(self.lib.sem_basis_dot2_work_size(rows, b - a) for a, b in self.segments)
+                                    if self.segments else 1), dtype=V.dtype, device=V.device)
 
     def _stream(self):
         return torch.cuda.current_stream(self.V.device).cuda_stream
@@ -51,12 +58,21 @@ class _DeviceSweeps:
             raise ValueError(f"{name} must be a contiguous float64 vector of {V.shape[1]} entries on {V.device}")
 
     def dot2(self, k, a, b):
-        """[V_j . a, V_j . b] for the first k rows -> (k, 2) view."""
+        """[V_j . a, V_j . b] over the owned entries for the first k rows -> (k, 2)."""
         self._vec(a, "a")
         self._vec(b, "b")
-        self.check(self.lib.sem_basis_dot2(self.V.data_ptr(), self.ldv, k, self.V.shape[1], a.data_ptr(),
-                                           b.data_ptr(), self.work.data_ptr(), self.out.data_ptr(), self._stream()))
-        return self.out[:k]
+        if not self.segments:
+            return torch.zeros((k, 2), dtype=self.V.dtype, device=self.V.device)
+        V, s = self.V, self._stream()
+        for i, (lo, hi) in enumerate(self.segments):
+            off = lo * V.element_size()
+            self.check(self.lib.sem_basis_dot2(V.data_ptr() + off, self.ldv, k, hi - lo, a.data_ptr() + off,
+                                               b.data_ptr() + off, self.work.data_ptr(), self.out[i].data_ptr(), s))
+        return self.out[0, :k] if len(self.segments) == 1 else self.out[:, :k].sum(0)
+
+    def sqnorm(self, w):
+        """w . w over the owned entries (0-d device tensor)."""
+        return _seg_sqnorm(w, self.segments)
 
     def update(self, k, c, w):
         """w -= V[:k]^T c, in place."""
@@ -67,13 +83,47 @@ class _DeviceSweeps:
                                              w.data_ptr(), self._stream()))
 
 
+def _seg_sqnorm(w, segments):
+    s = None
+    for a, b in segments:
+        p = torch.dot(w[a:b], w[a:b])
+        s = p if s is None else s + p
+    return s if s is not None else torch.zeros((), dtype=w.dtype, device=w.device)
+
+
+class _TorchSweeps:
+    """The same two passes through torch (CPU tensors, other dtypes): the CPU tests run the algorithm the
+    device runs, partitioned or not."""
+
+    def __init__(self, V, segments=None):
+        self.V = V
+        n = V.shape[1]
+        self.segments = [(0, n)] if segments is None else [(int(a), int(b)) for a, b in segments if b > a]
+
+    def dot2(self, k, a, b):
+        V = self.V
+        out = torch.zeros((k, 2), dtype=V.dtype, device=V.device)
+        for lo, hi in self.segments:
+            out += torch.stack((V[:k, lo:hi] @ a[lo:hi], V[:k, lo:hi] @ b[lo:hi]), dim=1)
+        return out
+
+    def update(self, k, c, w):
+        w -= self.V[:k].T @ c[:k]
+
+    def sqnorm(self, w):
+        return _seg_sqnorm(w, self.segments)
+
+
 REORTH_ETA = 1e-4   # a true extra orthogonalisation pass when ||w|| drops below this fraction
 
 
 class GMRESResult:
-    def __init__(self, x, info, iters, res_norm, matvecs, reorth=0):
+    """matvecs counts the operator applications the iteration used; `discarded` the speculative ones of the
+    pipelined step that were thrown away (on convergence or after a reorthogonalisation)."""
+
+    def __init__(self, x, info, iters, res_norm, matvecs, reorth=0, discarded=0):
         self.x, self.info, self.iters, self.res_norm, self.matvecs = x, info, iters, res_norm, matvecs
-        self.reorth = reorth
+        self.reorth, self.discarded = reorth, discarded
 
 
 def _sizes(N, restart, maxiter, inner, default_restart):
@@ -131,48 +181,61 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     matvec(v) -> A v and precond(v) -> M^-1 v take and return 1-D tensors like b.
     Converges when ||b - A x||_2 <= max(atol, rtol * ||b||_2) (SciPy's criterion).
     info = 0 on convergence, else the number of iterations performed (SciPy's convention).
-    inner(V, w) -> V @ w (k inner products) replaces the local products; a partitioned solve passes
-    sem_amd.parallel.DistributedInner, so every rank sees the same Hessenberg entries and takes the
-    same path through the iteration.
+    inner: the inner product of a partitioned vector.  sem_amd.parallel.DistributedInner (owned `segments` of
+    the local vector and a `reduce` all-reduce) keeps the partitioned solve on the HIP basis sweeps: per Arnoldi
+    step one all-reduce of both CGS2 coefficient sets with ||w||^2, one of ||w||^2 after the update, and the
+    pipelined step as on one GPU -- every rank sees the same Hessenberg entries and takes the same path through
+    the iteration.  Any other callable inner(V, w) -> V @ w takes torch's route (one collective per product).
     basis_out: a list that receives a copy of each cycle's orthonormal basis (tests).
     linear_precond: precond is a fixed linear map (the solvers' mass diagonal, PCD and direct solves), so the
     correction is M^-1 (V y) and the preconditioned basis Z = M^-1 V is not kept -- half the basis memory, and
     twice the vectors within a memory budget; False keeps Z (flexible GMRES, for a varying preconditioner).
     """
-    proj = inner if inner is not None else (lambda A, w: A @ w)
-
-    def vnorm(w):
-        if inner is None:
-            return torch.linalg.vector_norm(w).item()
-        return math.sqrt(max(proj(w.unsqueeze(0), w)[0].item(), 0.0))
-
     N = b.numel()
     dt, dev = b.dtype, b.device
     restart, maxiter = _sizes(N, restart, maxiter, inner, 100)
+    segments = getattr(inner, "segments", None) if inner is not None else None
+    red = getattr(inner, "reduce", None) if segments is not None else None
+    generic = inner is not None and segments is None      # an arbitrary inner(V, w) callable
+    proj = inner
     x = torch.zeros_like(b) if x0 is None else x0.clone()
-    bnorm = vnorm(b)
-    tol = max(atol, rtol * bnorm)
     V = torch.empty((restart + 1, N), dtype=dt, device=dev)
     G = torch.zeros((restart + 1, restart + 1), dtype=dt, device=dev)  # Gram matrix V^T V of the basis
-    # the HIP sweeps read and write doubles: other dtypes take torch's GEMV route
-    sweeps = _DeviceSweeps(V) if (inner is None and V.is_cuda and V.dtype == torch.float64) else None
+    sweeps = None
+    if not generic:   # the HIP sweeps read and write doubles: CPU tensors and other dtypes take torch's
+        sweeps = (_DeviceSweeps(V, segments) if (V.is_cuda and V.dtype == torch.float64)
+                  else _TorchSweeps(V, segments))
+
+    def dnorm(w):
+        """||w|| over every rank as a 0-d device tensor (no host synchronisation)."""
+        if red is None:
+            return torch.linalg.vector_norm(w)
+        return torch.sqrt(red(sweeps.sqnorm(w).reshape(1))[0].clamp_min(0.0))
+
+    def vnorm(w):
+        if generic:
+            return math.sqrt(max(proj(w.unsqueeze(0), w)[0].item(), 0.0))
+        return float(dnorm(w))
+
+    bnorm = vnorm(b)
+    tol = max(atol, rtol * bnorm)
     Z = torch.empty((restart, N), dtype=dt, device=dev) if (precond is not None and not linear_precond) else None
-    total, matvecs = 0, 0
+    total, matvecs, discarded = 0, 0, 0
     self_reorth = [0]
-    # pipelined steps on one GPU (SEM_GMRES_PIPELINE=0 turns them off; cfg4's Ra = 1e6 block solve 0.744 ->
-    # 0.715 s, profiles/r04/schur_ab/schurpipe_*.jsonl): a pinned host buffer for each step's coefficients and
-    # norms, and the event that marks its copy
+    # pipelined steps on the GPU, partitioned or not (SEM_GMRES_PIPELINE=0 turns them off; cfg4's Ra = 1e6 block
+    # solve 0.744 -> 0.715 s, profiles/r04/schur_ab/schurpipe_*.jsonl): a pinned host buffer for each step's
+    # coefficients and norms, and the event that marks its copy
     pipe = None
-    if sweeps is not None and os.environ.get("SEM_GMRES_PIPELINE", "1") != "0":
+    if isinstance(sweeps, _DeviceSweeps) and os.environ.get("SEM_GMRES_PIPELINE", "1") != "0":
         pipe = (torch.empty(restart + 3, dtype=torch.float64, pin_memory=True), torch.cuda.Event())
     r = b - matvec(x) if x0 is not None else b.clone()
     matvecs += x0 is not None
     beta = vnorm(r)
     while True:
         if beta <= tol:
-            return GMRESResult(x, 0, total, beta, matvecs, self_reorth[0])
+            return GMRESResult(x, 0, total, beta, matvecs, self_reorth[0], discarded)
         if total >= maxiter:
-            return GMRESResult(x, total, total, beta, matvecs, self_reorth[0])
+            return GMRESResult(x, total, total, beta, matvecs, self_reorth[0], discarded)
         V[0] = r / beta
         H = np.zeros((restart + 1, restart))
         # Givens rotations and the rotated right-hand side in float64 arrays: the O(k) rotation sweep of
@@ -185,22 +248,31 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
         pending = None   # the next step's A M^-1 v_{k+1}, launched before this step's host synchronisation
         for k in range(restart):
             if pending is None:
-                zk = precond(V[k]) if precond is not None else V[k]
-                if Z is not None:
-                    Z[k] = zk
-                w = matvec(zk)
+                with phase("krylov.matvec"):
+                    zk = precond(V[k]) if precond is not None else V[k]
+                    if Z is not None:
+                        Z[k] = zk
+                    w = matvec(zk)
                 matvecs += 1
             else:
                 w, pending = pending, None
             w_in = w
             Vk = V[:k + 1]
+            tok = tracing.begin("krylov.orthogonalise")
             # CGS2 in three sweeps over the basis instead of four: the second pass's coefficients
             # V^T (w - V h) = (I - G) h come from the basis' Gram matrix G = V^T V, whose new row
             # V^T v_k costs one GEMV per iteration.  (One GEMM over [w, v_k] would make it two
             # sweeps, but torch routes that skinny product to a GEMM 14x slower than two GEMVs.)
-            if sweeps is not None:           # one HIP pass: CGS pass 1 and the Gram row together
-                S = sweeps.dot2(k + 1, w.contiguous(), V[k])
-                h, gk = S[:, 0].clone(), S[:, 1].clone()
+            h0sq = None
+            if sweeps is not None:           # one pass: CGS pass 1 and the Gram row together
+                w = w.contiguous()
+                S = sweeps.dot2(k + 1, w, V[k])
+                if red is not None:          # ONE all-reduce: both coefficient sets and ||w||^2
+                    buf = torch.cat((S.reshape(-1), sweeps.sqnorm(w).reshape(1)))
+                    red(buf)
+                    h, gk, h0sq = buf[0:2 * k + 2:2], buf[1:2 * k + 2:2], buf[-1]
+                else:
+                    h, gk = S[:, 0].clone(), S[:, 1].clone()
             else:
                 h = proj(Vk, w)              # CGS pass 1
                 gk = proj(Vk, V[k])          # Gram row of the newest basis vector
@@ -213,30 +285,34 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             else:
                 w = w - Vk.T @ hh
             spec = None
+            if sweeps is not None:
+                nw = dnorm(w)
+                n0 = torch.linalg.vector_norm(w_in) if h0sq is None else torch.sqrt(h0sq.clamp_min(0.0))
+                pk = torch.cat((hh, nw[None], n0[None]))
+            tracing.end(tok)
             if pipe is not None:
-                # pipelined step (device, one GPU): the coefficients and norms go to pinned host memory, then
-                # v_{k+1} = w / ||w|| and the next matvec are queued BEFORE the host waits for that copy, so the
-                # GPU runs the next operator application while the host does this step's least-squares update;
-                # the speculation is dropped on convergence (one extra matvec) and redone after a
-                # reorthogonalisation (which changes w)
-                nw = torch.linalg.vector_norm(w)
-                pk = torch.cat((hh, nw[None], torch.linalg.vector_norm(w_in)[None]))
+                # pipelined step: the coefficients and norms go to pinned host memory, then v_{k+1} = w / ||w|| and
+                # the next matvec are queued BEFORE the host waits for that copy, so the GPU runs the next operator
+                # application while the host does this step's least-squares update; the speculation is dropped on
+                # convergence and redone after a reorthogonalisation (which changes w).  A zero ||w|| (exact
+                # breakdown) divides by one instead: the speculation is dropped there anyway.
                 pipe[0][:k + 3].copy_(pk, non_blocking=True)
                 pipe[1].record()
                 if k + 1 < restart and total + 1 < maxiter:
-                    V[k + 1] = w / nw
-                    z1 = precond(V[k + 1]) if precond is not None else V[k + 1]
-                    if Z is not None:
-                        Z[k + 1] = z1
-                    spec = matvec(z1)
+                    with phase("krylov.matvec"):
+                        V[k + 1] = w / torch.where(nw > 0, nw, torch.ones_like(nw))
+                        z1 = precond(V[k + 1]) if precond is not None else V[k + 1]
+                        if Z is not None:
+                            Z[k + 1] = z1
+                        spec = matvec(z1)
                     matvecs += 1
-                pipe[1].synchronize()
+                with phase("krylov.host_wait"):
+                    pipe[1].synchronize()
                 cn = pipe[0][:k + 3].numpy().copy()
-                h0 = float(cn[-1])
-                col = cn[:-1]
-                hn = float(col[-1])
-            elif inner is None:   # one device -> host transfer per step: coefficients, ||w|| after and before
-                cn = _host64(torch.cat((hh, torch.linalg.vector_norm(w)[None], torch.linalg.vector_norm(w_in)[None])))
+            elif sweeps is not None:   # one device -> host transfer per step: coefficients, ||w|| after and before
+                with phase("krylov.host_wait"):
+                    cn = _host64(pk)
+            if sweeps is not None:
                 h0 = float(cn[-1])
                 col = cn[:-1]
                 hn = float(col[-1])
@@ -250,16 +326,20 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
                 # severe cancellation: the Gram-matrix form of the second pass cannot see the rounding
                 # error of the first subtraction, so make one true extra pass (it fires only when
                 # ||w|| collapses by 1e4 or more)
-                h2 = sweeps.dot2(k + 1, w, V[k])[:, 0].clone() if sweeps is not None else proj(Vk, w)
                 if sweeps is not None:
+                    h2 = sweeps.dot2(k + 1, w, V[k])[:, 0].clone()
+                    if red is not None:
+                        red(h2)
                     sweeps.update(k + 1, h2.contiguous(), w)
                 else:
+                    h2 = proj(Vk, w)
                     w = w - Vk.T @ h2
                 hn = vnorm(w)
                 col[:k + 1] += _host64(h2)
                 col[k + 1] = hn
                 self_reorth[0] += 1
-                spec = None       # v_{k+1} and the speculative matvec came from the unreorthogonalised w
+                if spec is not None:   # v_{k+1} and the speculative matvec came from the unreorthogonalised w
+                    spec, matvecs, discarded = None, matvecs - 1, discarded + 1
             givens_column(col, cs, sn, g, k)   # earlier rotations, the new one, the right-hand side
             H[:k + 2, k] = col
             total += 1
@@ -268,6 +348,8 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
             if callback is not None:
                 callback(est)
             if est <= tol or hn == 0.0 or total >= maxiter:
+                if spec is not None:   # the speculation past convergence is not used
+                    matvecs, discarded = matvecs - 1, discarded + 1
                 break
             if spec is not None:
                 pending = spec    # V[k+1] and A M^-1 V[k+1] (and Z[k+1]) are already on the device

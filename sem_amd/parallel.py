@@ -178,22 +178,51 @@ class DistributedInner:
     """Inner products of strip-partitioned vectors for sem_amd.krylov.gmres(inner=...).
 
     A shared interface line is stored on both neighbouring ranks (with equal values after the
-    exchange); it is counted once, on the left-hand rank, and the per-rank partial products are
-    summed with one all-reduce (RCCL over xGMI under "nccl") per call: two per Arnoldi step for
-    CGS2, plus one per norm."""
+    exchange); it is counted once, on the left-hand rank.  The owned entries are contiguous ranges of
+    the local vector (`segments`: a rank > 0 skips its first NY entries), so krylov.gmres runs its
+    HIP basis sweeps on those ranges directly -- no mask, no temporary -- and sums the per-rank partial
+    products with `reduce` (one all-reduce, RCCL over xGMI under "nccl"): one per Arnoldi step for both
+    CGS2 coefficient sets and the norm before the update, one for the norm after it.
+    Called as inner(A, w) it is the plain k inner products (gmres_left, tests)."""
 
-    def __init__(self, part, mesh, dist, group=None):
+    def __init__(self, part, mesh, dist, group=None, segments=None, backend_device=None):
         self.dist, self.group = dist, group
-        rank = part.bounds.index(mesh.ex_begin if hasattr(mesh, "ex_begin") else mesh.eb)
-        self.own = torch.ones(mesh.n_local, dtype=torch.float64, device=mesh.device)
-        if rank > 0:
-            self.own[:mesh.NY] = 0.0
+        if segments is None:
+            rank = part.bounds.index(mesh.ex_begin if hasattr(mesh, "ex_begin") else mesh.eb)
+            segments = [(mesh.NY if rank > 0 else 0, mesh.n_local)]
+            n, dev = mesh.n_local, mesh.device
+        else:
+            n, dev = mesh
+        self.segments = [(int(a), int(b)) for a, b in segments]
+        self.n = n
+        self.own = torch.zeros(n, dtype=torch.float64, device=dev)
+        for a, b in self.segments:
+            self.own[a:b] = 1.0
+        if backend_device is None and dist is not None:
+            backend_device = ("cuda" if dist.get_backend(group) == "nccl" else "cpu")
+        self.bdev = torch.device(backend_device) if backend_device is not None else None
+        self.collectives = 0          # all-reduces issued (profiling: tools/strip_profile.py)
+
+    def reduce(self, t):
+        """Sum t (a device tensor) over the ranks, in place; returns t.  Under RCCL the collective stays on
+        the device (stream-ordered, no host synchronisation); under gloo it is staged through the host."""
+        if self.dist is None:
+            return t
+        self.collectives += 1
+        if self.bdev is None or t.device.type == self.bdev.type:
+            self.dist.all_reduce(t, group=self.group)
+            return t
+        tb = t.to(self.bdev)
+        self.dist.all_reduce(tb, group=self.group)
+        t.copy_(tb)
+        return t
 
     def __call__(self, A, w):
-        h = A @ (w * self.own)
-        if self.dist is not None:
-            self.dist.all_reduce(h, group=self.group)
-        return h
+        h = None
+        for a, b in self.segments:
+            p = A[:, a:b] @ w[a:b]
+            h = p if h is None else h + p
+        return self.reduce(h)
 
 
 class Partition:

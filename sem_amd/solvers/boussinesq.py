@@ -84,18 +84,14 @@ class BoussinesqCoupler:
             if (pcd is None) != (pns is None):
                 raise ValueError("partition both solvers or neither")
             if pns is not None:
-                own = torch.cat((pcd.inner.own, pns.inner.own, pns.inner.own, pns.inner.own))
-                dist, group = pns.dist, pns.group
-                bdev = pns.backend_device()
-
-                def inner(A, w, own=own):
-                    h = A @ (w * own)
-                    if dist.get_world_size(group) > 1:
-                        hb = h.to(bdev)
-                        dist.all_reduce(hb, group=group)
-                        h = hb.to(h.device)
-                    return h
-                self._inner = inner
+                # the owned ranges of [T | u | v | p]: each block's own strip range (a shared line counted once)
+                from ..parallel import DistributedInner
+                segs, off = [], 0
+                for blk in (pcd.inner, pns.inner, pns.inner, pns.inner):
+                    segs += [(off + a, off + b) for a, b in blk.segments]
+                    off += blk.n
+                self._inner = DistributedInner(None, (off, cd._mesh.device), pns.dist, pns.group, segments=segs,
+                                               backend_device=pns.backend_device())
         self.iterations = 0
         self.timing = {k: 0.0 for k in ("residuals", "jacobian_apply", "cd_update", "ns_update")}
         self.calls = {k: 0 for k in self.timing}

@@ -17,6 +17,7 @@ lines (sem_amd/solvers/velocity_solve.py, blocks written by the sem_velocity_blo
 instead of host SuperLU, and the Schur system runs the device GMRES.  No CSR matrix is formed.
 """
 import gc
+import os
 import time
 
 import numpy as np
@@ -26,6 +27,7 @@ from .. import SEM, _lib
 from ..device import get_mesh, no_gc
 from ..krylov import Recycle, gcro, gmres
 from ..operators import ConvectionTensor, SEMOperator
+from ..tracing import phase
 from .convection_diffusion import DirichletRows
 from .velocity_solve import VelocityJacobianSolver
 
@@ -318,6 +320,8 @@ class NavierStokesSolver:
         vs = StripLineSolver(self._P, self._N_ex, self._N_ey, m.device, p.part.bounds, p.rank, p.dist, group=p.group,
                              gather_device=p.backend_device())
         vs.factor_mesh(m, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
+        vs.set_operator(self._velocity_apply_lines, amax=lambda t: p.amax(t))
+        vs.check_refinement()       # every rank takes the same decision (norms max-reduced over the ranks)
         self._velo = vs
         if 'LU_suc' in self._iprint:
             print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec (element-partitioned)')
@@ -329,12 +333,17 @@ class NavierStokesSolver:
         m, part, NY = self._mesh, self._part, self._mesh.NY
         kw = self._ns_kw(pin_first=False)
         gu, gv = torch.empty_like(dp), torch.empty_like(dp)
-        m.ns_apply(None, None, dp, gu, gv, **kw)
-        part.assemble(gu, gv)
-        X = vs._solve_lines(torch.stack((gu.view(-1, NY), gv.view(-1, NY)), dim=1).reshape(-1, 2 * NY))
+        with phase("schur.grad_apply"):
+            m.ns_apply(None, None, dp, gu, gv, **kw)
+        with phase("schur.grad_assemble"):
+            part.assemble(gu, gv)
+        with phase("schur.velocity_solve"):
+            X = vs._solve_lines(torch.stack((gu.view(-1, NY), gv.view(-1, NY)), dim=1).reshape(-1, 2 * NY))
         rc = torch.empty_like(dp)
-        m.ns_apply(X[:, :NY].reshape(-1), X[:, NY:].reshape(-1), dp, rc=rc, c_div=-1.0, **kw)
-        part.assemble(rc)
+        with phase("schur.div_apply"):
+            m.ns_apply(X[:, :NY].reshape(-1), X[:, NY:].reshape(-1), dp, rc=rc, c_div=-1.0, **kw)
+        with phase("schur.div_assemble"):
+            part.assemble(rc)
         return rc
 
     def _get_update_strips(self, dres_u, dres_v, dres_cont, du0=None, dv0=None, dp0=None):
@@ -383,7 +392,8 @@ class NavierStokesSolver:
         if r.info != 0:
             raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {r.info} iterations')
         dp = r.x
-        self.schur_matvecs = count[0]
+        self.schur_matvecs = count[0] - r.discarded     # a dropped speculative matvec is not counted
+        self.schur_discarded = r.discarded
         b_u, b_v = torch.empty_like(dp), torch.empty_like(dp)
         m.ns_apply(None, None, dp, b_u, b_v, **kw)
         part.assemble(b_u, b_v)
@@ -406,13 +416,32 @@ class NavierStokesSolver:
         vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior,
                                     sweep=self._velocity_sweep)
         vs.factor_mesh(m, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
+        vs.set_operator(self._velocity_apply_lines)
+        vs.check_refinement()       # one refinement step per solve if the factor's backward error exceeds 1e-13
         if self._velocity_graph:
             vs.capture()
         self._velo = vs
         if 'LU_suc' in self._iprint:
             torch.cuda.synchronize(m.device)
-            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec (device static condensation)')
+            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec (device static condensation, '
+                  f'backward error {vs.refine_eta:.1e}{", refined" if vs.refine else ""})')
         return vs
+
+    def _velocity_apply_lines(self, X):
+        """J X for the velocity Jacobian of this linearisation on (NX, 2 NY) line arrays: the velocity rows of
+        _get_dresiduals at dp = 0 (NavierStokes_Solver.py:138-160; Dirichlet rows identity, as the factored
+        Jacobian's), assembled across strips on a partitioned solver.  The refinement step's operator."""
+        m, NY = self._mesh, self._mesh.NY
+        kw = dict(self._jac_kw, **self._ns_kw(pin_first=False))
+        if self._part is None:
+            Y = torch.empty_like(X)
+            m.ns_apply(X[:, :NY], X[:, NY:], None, Y[:, :NY], Y[:, NY:], None, **kw)
+            return Y
+        xu, xv = X[:, :NY].reshape(-1), X[:, NY:].reshape(-1)
+        ru, rv = torch.empty_like(xu), torch.empty_like(xv)
+        m.ns_apply(xu, xv, None, ru, rv, None, **kw)
+        self._part.assemble(ru, rv)
+        return torch.stack((ru.view(-1, NY), rv.view(-1, NY)), dim=1).reshape(-1, 2 * NY)
 
     def _pressure_laplacian(self):
         """A_p = K with the pinned pressure row as an identity row (the Neumann pressure Laplacian
@@ -500,10 +529,11 @@ class NavierStokesSolver:
         if r.info != 0:
             raise RuntimeError(f'NavierStokes LGMRES: Failed to converge in {r.info} iterations')
         dp = r.x
-        self.schur_matvecs = count[0]
+        self.schur_matvecs = count[0] - getattr(r, "discarded", 0)   # dropped speculations are not counted
+        self.schur_discarded = getattr(r, "discarded", 0)
         if 'LGMRES_suc' in self._iprint:
             res = (schur_mv(dp) - b_schur).abs().max().item()
-            print(f'NavierStokes GMRES: Converged in {count[0]} evaluations with max-norm {res}')
+            print(f'NavierStokes GMRES: Converged in {self.schur_matvecs} evaluations with max-norm {res}')
         b_u, b_v = torch.empty_like(dp), torch.empty_like(dp)
         m.ns_apply(None, None, dp, b_u, b_v, **self._ns_kw(pin_first=False))
         du, dv = vs.solve(ru - b_u, rv - b_v)
@@ -566,7 +596,10 @@ class _StripSchur:
         self.ns, self.vs = ns, vs
         m, part = ns._mesh, ns._part
         self._graph = None
-        if graph and m.device.type == "cuda" and part.backend_device().type == "cuda":
+        # SEM_STRIP_GRAPH=0 keeps the matvec eager (the capture of RCCL collectives is checked against
+        # the eager matvec on a probe vector, but no multi-GPU run has exercised it yet -- DESIGN.md section 7)
+        if (graph and m.device.type == "cuda" and part.backend_device().type == "cuda"
+                and os.environ.get("SEM_STRIP_GRAPH", "1") != "0"):
             self._capture()
 
     def _capture(self):

@@ -21,8 +21,11 @@ elimination to the two boundary lines, ONE all-gather of 2 m doubles per rank, t
 solve, local back substitution, interior back substitution.  x comes out on every rank's lines, equal
 on shared lines.
 """
+import os
+
 import torch
 
+from ..tracing import phase
 from .velocity_solve import (VelocityJacobianSolver, fused_thomas_operators, fused_thomas_solve, pivot_inverse,
                              twisted_thomas_operators, twisted_thomas_solve)
 
@@ -138,27 +141,31 @@ class StripLineSolver(VelocityJacobianSolver):
         if self.G == 1:
             return super()._iface_solve(g)
         n = self.nex
-        if self._T is not None:
-            y = self._thomas(g[1:n])
-            h = torch.stack((g[0] - self._S_up0 @ y[0], g[n] - self._S_lon @ y[-1]))
-        else:
-            y, h = None, torch.stack((g[0], g[1]))
-        H = torch.stack(self._all_gather(h))          # (G, 2, m): the boundary right-hand sides of every strip
-        rhs = torch.zeros((self.G + 1, self.m), dtype=torch.float64, device=self.device)
-        rhs[:-1] += H[:, 0]
-        rhs[1:] += H[:, 1]
-        xb = self._red._cr_solve(rhs)
+        with phase("strip.interior_sweep"):
+            if self._T is not None:
+                y = self._thomas(g[1:n])
+                h = torch.stack((g[0] - self._S_up0 @ y[0], g[n] - self._S_lon @ y[-1]))
+            else:
+                y, h = None, torch.stack((g[0], g[1]))
+        with phase("strip.allgather"):
+            H = torch.stack(self._all_gather(h))      # (G, 2, m): the boundary right-hand sides of every strip
+        with phase("strip.reduced_solve"):
+            rhs = torch.zeros((self.G + 1, self.m), dtype=torch.float64, device=self.device)
+            rhs[:-1] += H[:, 0]
+            rhs[1:] += H[:, 1]
+            xb = self._red._cr_solve(rhs)
         out = torch.empty_like(g)
         out[0], out[n] = xb[self.rank], xb[self.rank + 1]
-        if y is not None:   # y - X0 x0 - X1 x1 = y - [X0 | X1] [x0; x1], one batched GEMV
-            out[1:n] = y - torch.matmul(self._T[1], xb[self.rank:self.rank + 2].reshape(-1))
+        with phase("strip.back_substitution"):
+            if y is not None:   # y - X0 x0 - X1 x1 = y - [X0 | X1] [x0; x1], one batched GEMV
+                out[1:n] = y - torch.matmul(self._T[1], xb[self.rank:self.rank + 2].reshape(-1))
         return out
 
     def capture(self):
         """Graph capture of the solve: only when the reduced system's all-gather runs on the device (RCCL,
         capturable); under gloo the all-gather goes through the host, so the solve stays eager.
         Under RCCL the captured graph is checked against the eager solve before it is used."""
-        if self.G > 1 and self.gather_device.type != "cuda":
+        if self.G > 1 and (self.gather_device.type != "cuda" or os.environ.get("SEM_STRIP_GRAPH", "1") == "0"):
             return False
         captured = super().capture()       # a capture executes no collective: a failure desynchronises no rank
         if self.G == 1:

@@ -29,6 +29,7 @@ import time
 import torch
 
 from ..device import no_gc
+from ..tracing import phase
 
 GEMV_LDS_DOUBLES = 8192   # sem_block_gemv stages S m operand doubles in LDS (include/sem_ops.h)
 
@@ -390,6 +391,16 @@ class VelocityJacobianSolver:
         # meet in the middle, one launch per step of both, twisted_thomas_solve) or "single" (one-ended, the
         # fused forward operators of fused_thomas_operators)
         self.sweep_form = os.environ.get("SEM_SWEEP_FORM", "twisted")
+        # one step of iterative refinement x += J^-1 (b - J x), gated at factor time by the factor's measured
+        # backward error (check_refinement).  The nested condensation eliminates the element-
+        # column interiors first, with no pivoting across that split: where a column interior is far worse
+        # conditioned than J (kappa 2.0e6 against kappa(J) = 9.8e3 for the one-component Pe = 1000 operator on
+        # 2 x 2 elements, P = 6) the solve's backward error is ~1e-11 where SuperLU's pivoting gives ~4e-17
+        # (NavierStokes_Solver.py:184); one refinement step brings it to 3e-17 (tools/backward_error_probe.py)
+        self._apply = None
+        self._amax = None
+        self.refine = False
+        self.refine_eta = None
 
     @contextlib.contextmanager
     def _phase(self, name):
@@ -1055,27 +1066,67 @@ class VelocityJacobianSolver:
         v = C.c_void_p
         b1 = B.data_ptr() + 8 * m   # line e P + 1: first interior line of column e
         coupled = bool(d.XiB) and self.nested_back == "coupled"
-        if coupled:   # ABI 11: element and edge steps, then g from T and the edge values (no y_I formed)
-            _lib.check(lib.sem_nested_iface_rhs(C.byref(d), v(b1), P * m, v(B.data_ptr()), m,
-                                                v(self.aBI.data_ptr()), v(yI.data_ptr()), self.nI,
-                                                v(g.data_ptr()), st))
-        else:
-            _lib.check(lib.sem_nested_solve(C.byref(d), v(b1), P * m, None, None, v(yI.data_ptr()), self.nI, st))
-            _lib.check(lib.sem_interface_rhs(P, nex, m, v(B.data_ptr()), m, v(self.aBI.data_ptr()),
-                                             v(yI.data_ptr()), self.nI, v(g.data_ptr()), st))
-        self._own_rhs(g, B)
-        xB = self._iface_solve(g)
+        with phase("vsolve.nested_fwd"):
+            if coupled:   # ABI 11: element and edge steps, then g from T and the edge values (no y_I formed)
+                _lib.check(lib.sem_nested_iface_rhs(C.byref(d), v(b1), P * m, v(B.data_ptr()), m,
+                                                    v(self.aBI.data_ptr()), v(yI.data_ptr()), self.nI,
+                                                    v(g.data_ptr()), st))
+            else:
+                _lib.check(lib.sem_nested_solve(C.byref(d), v(b1), P * m, None, None, v(yI.data_ptr()), self.nI,
+                                                st))
+                _lib.check(lib.sem_interface_rhs(P, nex, m, v(B.data_ptr()), m, v(self.aBI.data_ptr()),
+                                                 v(yI.data_ptr()), self.nI, v(g.data_ptr()), st))
+            self._own_rhs(g, B)
+        with phase("vsolve.iface_solve"):
+            xB = self._iface_solve(g)
         out = torch.empty((NX, m), dtype=torch.float64, device=self.device)
         out[0::P] = xB
         # back substitution x_I = A_II^-1 (b_I - A_IB x_B): by default from the forward solve's work arrays and
         # Xi A_iB (ABI 11; nested_back = "full" re-solves with Xi, the ABI-10 path, for A/B)
         back = lib.sem_nested_back_solve if coupled else lib.sem_nested_solve
-        _lib.check(back(C.byref(d), v(b1), P * m, v(self.aIB.data_ptr()), v(xB.data_ptr()),
-                        v(out.data_ptr() + 8 * m), P * m, st))
+        with phase("vsolve.nested_back"):
+            _lib.check(back(C.byref(d), v(b1), P * m, v(self.aIB.data_ptr()), v(xB.data_ptr()),
+                            v(out.data_ptr() + 8 * m), P * m, st))
         return out
 
+    # ------------------------------------------------------------------ iterative refinement
+    def set_operator(self, apply_lines, amax=None):
+        """apply_lines(X) -> J X on (NX, m) line arrays (the matrix-free Jacobian apply of the solver that owns
+        this factor); amax(t) -> max |t| over every part (a partitioned solve reduces over the ranks)."""
+        self._apply = apply_lines
+        self._amax = amax if amax is not None else (lambda t: float(t.abs().max()))
+
+    def check_refinement(self, tau=None, seed=17):
+        """Measure the factor's normwise backward error eta = ||J x - b|| / (||J|| ||x|| + ||b||) (max norms) on a
+        seeded probe, ||J|| estimated from below by ||J s|| for a random sign vector s (so eta is over-estimated),
+        and turn on one refinement step per solve when eta > tau (SEM_REFINE_ETA, default 1e-13; 0 refines
+        always, inf never).  Every part of a partitioned solve takes the same decision (reduced norms).
+        Returns eta."""
+        if self._apply is None:
+            raise RuntimeError("set_operator() first")
+        if tau is None:
+            tau = float(os.environ.get("SEM_REFINE_ETA", "1e-13"))
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        b = torch.rand((self.NX, self.m), dtype=torch.float64, device=self.device, generator=g) * 2 - 1
+        sgn = torch.sign(torch.rand((self.NX, self.m), dtype=torch.float64, device=self.device, generator=g) - 0.5)
+        self.refine = False
+        x = self._solve_lines(b)
+        r = b - self._apply(x)
+        nJ = self._amax(self._apply(sgn))
+        eta = self._amax(r) / (nJ * self._amax(x) + self._amax(b))
+        self.refine_eta = eta
+        self.refine = eta > tau
+        return eta
+
     def _solve_lines(self, B):
-        """x = J^-1 b with b, x as (NX, 2 NY) line arrays (every line: u then v)."""
+        """x = J^-1 b with b, x as (NX, 2 NY) line arrays (every line: u then v); with `refine` set, one step of
+        iterative refinement on the matrix-free Jacobian apply."""
+        X = self._solve_lines_once(B)
+        if self.refine:
+            X = X + self._solve_lines_once(B - self._apply(X))
+        return X
+
+    def _solve_lines_once(self, B):
         P, nex, m, NX = self.P, self.nex, self.m, self.NX
         if (self.device.type == "cuda" and P > 1 and self.interior == "nested"
                 and getattr(self, "hip_nested", True)):

@@ -376,9 +376,6 @@ def _worker_cfg5_update(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.skipif(os.environ.get("SEM_SLOW_GPU_TESTS", "0") != "1",
-                    reason="several minutes with 4 ranks sharing one GPU over gloo: run by tools/gpu_steps.sh distcfg5 "
-                           "(SEM_SLOW_GPU_TESTS=1); the partitioned update itself is covered at small sizes above")
 def test_cfg5_element_partitioned_ns_update(gpu):
     """One cfg5 NS Newton update (_get_update) element-partitioned over 4 ranks on one GPU: it solves the
     partitioned Jacobian (the coupled maps above pin that to the whole-mesh device maps) to the reference's
@@ -396,4 +393,6 @@ def test_cfg5_element_partitioned_ns_update(gpu):
         assert p.exitcode == 0
     print(f"cfg5 partitioned NS update: {nmv} Schur matvecs, {secs:.1f} s, residual {err:.3e} (tol {tol:.3e}), "
           f"velocity error {verr:.2e}")
-    assert err <= 10 * tol and verr < 2e-5   # the cfg4 test's bar for the same stopping rule
+    # the reference's stopping rule itself, mtol sqrt(N) (NavierStokes_Solver.py:222-224), on the linearised residual
+    # of all three equations, and the step's velocities to the accuracy that rule implies (the cfg4 test's bar)
+    assert err <= tol and verr < 2e-5

@@ -178,3 +178,52 @@ def test_givens_column_c_matches_python_loop():
         assert np.allclose(c1, c2, rtol=1e-14, atol=1e-15)
     assert saved and saved[0] is not None   # the C path was the one under test
     assert np.allclose(g_c, g_p, rtol=1e-13, atol=1e-300) and np.allclose(cs_c, cs_p, rtol=1e-14)
+
+
+def test_flexible_path_with_a_varying_preconditioner():
+    """linear_precond=False keeps Z = M_k^-1 V (flexible GMRES), the only correct form when the
+    preconditioner changes between applications (an inner iterative solve).  With a preconditioner that varies
+    per call the flexible path meets the tolerance on the TRUE residual; the linear form (correction
+    M^-1 (V y)) is not meant for it.  With a fixed preconditioner both forms give SciPy's solution."""
+    rng = np.random.default_rng(11)
+    n = 160
+    A = np.diag(np.linspace(1, 80, n)) + 0.05 * rng.standard_normal((n, n))
+    b = rng.standard_normal(n)
+    At, bt = torch.from_numpy(A), torch.from_numpy(b)
+    d = torch.from_numpy(1.0 / np.diag(A).copy())
+    calls = [0]
+
+    def varying(v):                      # a different diagonal scaling on every call
+        calls[0] += 1
+        return d * v * (1.0 + 0.3 * np.sin(calls[0]))
+
+    r = gmres(lambda v: At @ v, bt, atol=1e-10, restart=60, maxiter=2000, precond=varying, linear_precond=False)
+    assert r.info == 0
+    assert np.linalg.norm(A @ r.x.numpy() - b) <= 1e-10 * 1.0001
+    ref, info = spla.gmres(A, b, atol=1e-11, rtol=0, restart=60, maxiter=200)
+    assert info == 0
+    for lin in (True, False):
+        rf = gmres(lambda v: At @ v, bt, atol=1e-10, restart=60, maxiter=2000, precond=lambda v: d * v,
+                   linear_precond=lin)
+        assert rf.info == 0 and np.abs(rf.x.numpy() - ref).max() < 1e-8
+
+
+def test_gmres_forced_reorthogonalisation_and_breakdown(monkeypatch):
+    """The reorthogonalisation branch on every step (REORTH_ETA > 1) gives the same solution as the default, and
+    an exact breakdown (b in a 3-dimensional invariant subspace) stops after 3 iterations with the exact answer."""
+    import sem_amd.krylov as K
+    rng = np.random.default_rng(2)
+    n = 120
+    A = torch.from_numpy(np.diag(np.linspace(1, 30, n)) + 0.02 * rng.standard_normal((n, n)))
+    b = torch.from_numpy(rng.standard_normal(n))
+    r0 = K.gmres(lambda v: A @ v, b, atol=1e-11, restart=80, maxiter=1000)
+    monkeypatch.setattr(K, "REORTH_ETA", 2.0)
+    r1 = K.gmres(lambda v: A @ v, b, atol=1e-11, restart=80, maxiter=1000)
+    assert r0.info == 0 and r1.info == 0 and r1.reorth >= r1.iters - 1 and r0.reorth == 0
+    assert abs(r0.iters - r1.iters) <= 1 and (r0.x - r1.x).abs().max().item() < 1e-9
+    monkeypatch.setattr(K, "REORTH_ETA", 1e-4)
+    D = torch.diag(torch.linspace(1, 5, n, dtype=torch.float64))
+    bb = torch.zeros(n, dtype=torch.float64)
+    bb[[3, 50, 90]] = torch.tensor([1.0, -2.0, 0.5], dtype=torch.float64)
+    rb = K.gmres(lambda v: D @ v, bb, atol=1e-12, restart=40, maxiter=100)
+    assert rb.iters == 3 and (D @ rb.x - bb).abs().max().item() < 1e-13

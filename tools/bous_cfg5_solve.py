@@ -40,6 +40,8 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group(args.backend)
     rank, world = dist.get_rank(), dist.get_world_size()
+    if args.backend == "gloo" and world > 1:   # rehearsal: the ranks share the box's 16-CPU share
+        torch.set_num_threads(max(1, 16 // world))
     import gc
 
     from sem_amd.solvers.boussinesq import BoussinesqCoupler, partitioned_coupler
@@ -77,7 +79,7 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
     if rank == 0:
-        out = {"config": f"cfg5 Boussinesq {args.mode} Ra={args.Ra:g}, {args.ne}x{args.ne} P={args.P}"
+        out = {"config": f"Boussinesq {args.mode} Ra={args.Ra:g}, {args.ne}x{args.ne} P={args.P}"
                          + (", element-partitioned" if world > 1 else ", whole mesh on one GPU"),
                "ranks": world, "backend": args.backend, "DOF": int(x.size), "stages": stages,
                "device": torch.cuda.get_device_name(dev)}

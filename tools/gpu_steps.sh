@@ -51,7 +51,7 @@ for s in "$@"; do
     pivot)      step pivot 300 python tools/pivot_probe.py ;;
     gemvprobe)  step gemvprobe 300 python tools/gemv_probe.py ;;
     dist)       step dist 900 $PYT tests/test_gpu_dist.py -k "not cfg5_element_partitioned_ns_update" ;;
-    distcfg5)   SEM_SLOW_GPU_TESTS=1 step distcfg5 720 ${PYT/--timeout 300/--timeout 680} -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
+    distcfg5)   step distcfg5 720 ${PYT/--timeout 300/--timeout 680} -s tests/test_gpu_dist.py -k cfg5_element_partitioned_ns_update ;;
     cfg5factor) SEM_PROFILE_FACTOR=1 step cfg5factor 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5factor_inv) SEM_PIVOT_INV=inv SEM_PROFILE_FACTOR=1 step cfg5factor_inv 900 python tools/cfg5_ns_probe.py --update 0 ;;
     cfg5ns)     SEM_PROFILE_FACTOR=1 step cfg5ns 900 python tools/cfg5_ns_probe.py ;;
@@ -154,6 +154,35 @@ for s in "$@"; do
       for c in 5 1 4 257 260; do
         SEM_BAND_CPOL=$c step bandab_c$c 300 python tools/kbench.py --meshes 8:1024 --reps 200
       done ;;
+    krylovdist) step krylovdist 900 $PYT tests/test_gpu_krylov.py tests/test_gpu_dist.py ;;
+    stripprof)  # where the partitioned Schur matvec's time goes (gloo rehearsal, 4 ranks) and
+                # one cfg5 strip as rank r of 8 alone on the GPU (loopback collectives), beside the whole-mesh matvec
+      step stripprof48 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29631 tools/strip_profile.py --mode rehearsal --ne 48 --P 8 --reps 5 --iters 40 \
+        --out "$O/strip_rehearsal48.jsonl"
+      step stripsolo128 900 python tools/strip_profile.py --mode solo --ne 128 --P 12 --G 8 --ranks 0,3 --reps 10 \
+        --whole 1 --out "$O/strip_solo128.jsonl" ;;
+    stripsolo)
+      step stripsolo128 900 python tools/strip_profile.py --mode solo --ne 128 --P 12 --G 8 --ranks 0,3 --reps 10 \
+        --whole 1 --out "$O/strip_solo128.jsonl" ;;
+    edgeprint)  TAILN=40 step edgeprint 300 $PYT -s tests/test_gpu_ns_velocity.py -k edge_sweep ;;
+    ghostab)    # VERDICT r4 item 7, the upper bound of folding the ghost tiles away: the 512 full tiles alone (diagnostic
+                # bit 128, wrong closing line / column) against all 585 tiles, alternated, in the driver's shape (one
+                # 20-apply graph) and amortised (1000-apply graph); then the SQ counter passes of both
+      for rep in 1 2 3; do for d in 0 128; do
+        SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_DIAG=$d TAILN=2 step ghostab_d${d}_r20_$rep 120 \
+          python tools/kbench.py --meshes 8:64 --reps 20
+        SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_DIAG=$d TAILN=2 step ghostab_d${d}_r1000_$rep 120 \
+          python tools/kbench.py --meshes 8:64 --reps 1000
+      done; done
+      for d in 0 128; do
+        SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_DIAG=$d tools/pmc_run.sh "$O/pmc_ghost_d$d" -- \
+          python tools/kbench.py --meshes 8:64 --reps 200 || exit 1
+      done ;;
+    stripprof128)
+      step stripprof128 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29632 tools/strip_profile.py --mode rehearsal --ne 128 --P 12 --reps 3 --iters 10 \
+        --out "$O/strip_rehearsal128.jsonl" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
