@@ -26,8 +26,8 @@ import os
 import torch
 
 from ..tracing import phase
-from .velocity_solve import (VelocityJacobianSolver, fused_thomas_operators, fused_thomas_solve, pivot_inverse,
-                             twisted_thomas_operators, twisted_thomas_solve)
+from .velocity_solve import (VelocityJacobianSolver, _gemv, fused_thomas_operators, fused_thomas_solve,
+                             pivot_inverse, twisted_thomas_operators, twisted_thomas_solve)
 
 
 class StripLineSolver(VelocityJacobianSolver):
@@ -43,6 +43,9 @@ class StripLineSolver(VelocityJacobianSolver):
         self.dist, self.group = dist, group
         self.gather_device = torch.device(gather_device) if gather_device is not None else self.device
         self.own_right = ee >= nex     # a shared right line belongs to the strip on its right
+        # the reduced system over the G + 1 strip-boundary lines: "rows" (default) keeps this rank's two block rows
+        # of its inverse (one GEMV per solve); "cr" factors and solves it whole on every rank (round 4, A/B)
+        self.reduced = os.environ.get("SEM_STRIP_REDUCED", "rows")
 
     # ------------------------------------------------------------------ factor
     def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
@@ -119,11 +122,57 @@ class StripLineSolver(VelocityJacobianSolver):
             Rd[j + 1] += Rj[1, 1]
             Ru[j], Rl[j] = Rj[0, 1], Rj[1, 0]
         del Rs
-        red = VelocityJacobianSolver(1, G, 1, dev)
-        red.m = m
-        red._cr_factor(Rd, Ru, Rl)
-        self._red = red
+        self._red = self._Z = None
+        if self.reduced == "cr":     # round-4 form: every rank factors and solves the whole reduced system
+            red = VelocityJacobianSolver(1, G, 1, dev)
+            red.m = m
+            red._cr_factor(Rd, Ru, Rl)
+            self._red = red
+        else:
+            self._Z = self._reduced_rows(Rd, Ru, Rl)
         self.factored = True
+
+    def _reduced_rows(self, Rd, Ru, Rl):
+        """Z = block rows r, r+1 of R^-1 for this rank r (2m x (G+1)m): the solve then needs x_r, x_{r+1} = Z h as ONE
+        streaming GEMV instead of a replicated solve of the whole reduced system (round 4: block cyclic reduction on
+        every rank, 3.9 ms per cfg5 matvec at G = 8 -- as long as the rest of the strip's solve,
+        tools/strip_profile.py).  R is eliminated from line 0 down to r - 1 and from line G up to r + 2, leaving
+        the 2 x 2 block system M of lines r, r+1:
+          top     Dt_0 = Rd[0],  Dt_j = Rd[j] - Rl[j-1] Dt_{j-1}^-1 Ru[j-1];  line r's right-hand side
+                  h_r + sum_{j<r} A_j h_j,  A_{r-1} = -Rl[r-1] Dt_{r-1}^-1,  A_j = A_{j+1} (-Rl[j] Dt_j^-1)
+          bottom  Et_G = Rd[G],  Et_j = Rd[j] - Ru[j] Et_{j+1}^-1 Rl[j];  line r+1's
+                  h_{r+1} + sum_{j>r+1} B_j h_j,  B_{r+2} = -Ru[r+1] Et_{r+2}^-1,  B_{j+1} = B_j (-Ru[j] Et_{j+1}^-1)
+          Z = M^-1 [A_0 .. A_{r-1} I 0 0 .. 0; 0 .. 0 0 I B_{r+2} .. B_G]
+        (Ru[j]: row j <- j+1, Rl[j]: row j+1 <- j.)  Factor cost: G pivot inverses and ~2G m^3 GEMMs."""
+        G, r, m = self.G, self.rank, self.m
+        inv = pivot_inverse
+        dev, f64 = self.device, torch.float64
+        Z = torch.zeros((2 * m, (G + 1) * m), dtype=f64, device=dev)
+        A, Dt_inv = [], None
+        for j in range(r):   # top chain: A_j appended as -Rl[j] Dt_j^-1 (products formed below)
+            D = Rd[j] if j == 0 else Rd[j] - Rl[j - 1] @ (Dt_inv @ Ru[j - 1])
+            Dt_inv = inv(D)
+            A.append(-(Rl[j] @ Dt_inv))
+        Mtop = Rd[r] if r == 0 else Rd[r] - Rl[r - 1] @ (Dt_inv @ Ru[r - 1])
+        B, Et_inv = {}, None
+        for j in range(G, r + 1, -1):   # bottom chain
+            E = Rd[j] if j == G else Rd[j] - Ru[j] @ (Et_inv @ Rl[j])
+            Et_inv = inv(E)
+            B[j] = -(Ru[j - 1] @ Et_inv)
+        Mbot = Rd[r + 1] if r + 1 == G else Rd[r + 1] - Ru[r + 1] @ (Et_inv @ Rl[r + 1])
+        M = torch.cat((torch.cat((Mtop, Ru[r]), dim=1), torch.cat((Rl[r], Mbot), dim=1)), dim=0)
+        Mi = inv(M)
+        Z[:, r * m:(r + 1) * m] = Mi[:, :m]
+        Z[:, (r + 1) * m:(r + 2) * m] = Mi[:, m:]
+        P = Mi[:, :m]
+        for j in range(r - 1, -1, -1):   # Z_j = Mi[:, :m] A_{r-1} ... A_j
+            P = P @ A[j]
+            Z[:, j * m:(j + 1) * m] = P
+        P = Mi[:, m:]
+        for j in range(r + 2, G + 1):    # Z_j = Mi[:, m:] B_{r+2} ... B_j
+            P = P @ B[j]
+            Z[:, j * m:(j + 1) * m] = P
+        return Z
 
     # ------------------------------------------------------------------ solve
     def _own_rhs(self, g, B):
@@ -149,16 +198,23 @@ class StripLineSolver(VelocityJacobianSolver):
                 y, h = None, torch.stack((g[0], g[1]))
         with phase("strip.allgather"):
             H = torch.stack(self._all_gather(h))      # (G, 2, m): the boundary right-hand sides of every strip
+        m = self.m
         with phase("strip.reduced_solve"):
-            rhs = torch.zeros((self.G + 1, self.m), dtype=torch.float64, device=self.device)
+            rhs = torch.zeros((self.G + 1, m), dtype=torch.float64, device=self.device)
             rhs[:-1] += H[:, 0]
             rhs[1:] += H[:, 1]
-            xb = self._red._cr_solve(rhs)
+            if self._Z is not None:    # x_r, x_{r+1} = Z h: one streaming GEMV over this rank's rows of R^-1
+                xb2 = torch.empty(2 * m, dtype=torch.float64, device=self.device)
+                _gemv(self._Z, rhs.reshape(-1), xb2)
+            else:
+                xb2 = self._red._cr_solve(rhs)[self.rank:self.rank + 2].reshape(-1)
         out = torch.empty_like(g)
-        out[0], out[n] = xb[self.rank], xb[self.rank + 1]
+        out[0], out[n] = xb2[:m], xb2[m:]
         with phase("strip.back_substitution"):
-            if y is not None:   # y - X0 x0 - X1 x1 = y - [X0 | X1] [x0; x1], one batched GEMV
-                out[1:n] = y - torch.matmul(self._T[1], xb[self.rank:self.rank + 2].reshape(-1))
+            if y is not None:   # y - X0 x0 - X1 x1 = y - [X0 | X1] [x0; x1]: one streaming GEMV over (k m) x 2m
+                X01 = self._T[1]
+                out[1:n] = y
+                _gemv(X01.view(-1, X01.shape[-1]), xb2, out[1:n].reshape(-1), alpha=-1.0, beta=1.0)
         return out
 
     def capture(self):

@@ -179,6 +179,10 @@ for s in "$@"; do
         SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_DIAG=$d tools/pmc_run.sh "$O/pmc_ghost_d$d" -- \
           python tools/kbench.py --meshes 8:64 --reps 200 || exit 1
       done ;;
+    stripsolotrace)  # kernel trace of one simulated cfg5 rank of 8 (factor + matvecs), per-kernel split of the strip solve
+      step stripsolotrace 600 rocprofv3 --kernel-trace --stats -d "$O/stripsolotrace" -o trace --output-format csv -- \
+        python tools/strip_profile.py --mode solo --ne 128 --P 12 --G 8 --ranks 3 --reps 10 --whole 0
+      find "$O/stripsolotrace" -name "*kernel_trace.csv" -size +20M -delete ;;
     stripprof128)
       step stripprof128 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
         --master-port 29632 tools/strip_profile.py --mode rehearsal --ne 128 --P 12 --reps 3 --iters 10 \
