@@ -27,7 +27,7 @@ import torch
 
 from ..tracing import phase
 from .velocity_solve import (VelocityJacobianSolver, _gemv, fused_thomas_operators, fused_thomas_solve,
-                             pivot_inverse, twisted_thomas_operators, twisted_thomas_solve)
+                             pivot_inverse, twisted_thomas_operators, twisted_thomas_solve, twisted_thomas_solve_mat)
 
 
 class StripLineSolver(VelocityJacobianSolver):
@@ -80,6 +80,20 @@ class StripLineSolver(VelocityJacobianSolver):
         if n == 1:
             R = torch.stack((torch.stack((S_diag[0], S_up[0])), torch.stack((S_lo[0], S_diag[1]))))
             self._T = None
+        elif self.sweep_form == "twisted" and n - 1 >= 3:
+            # two-ended sweep of the interior lines, as the whole mesh's; X0, X1 from the same factors (one set of
+            # pivot inverses: ADVICE r4 -- the one-ended factors were formed only for X0, X1 and doubled them)
+            k = n - 1
+            op = twisted_thomas_operators(S_diag[1:n], S_up[1:n - 1], S_lo[1:n - 1])
+            rhs = torch.zeros((k, m, 2 * m), dtype=f64, device=dev)
+            rhs[0, :, :m] = S_lo[0]
+            rhs[k - 1, :, m:] = S_up[n - 1]
+            X01 = twisted_thomas_solve_mat(op, rhs)
+            del rhs
+            X0, X1 = X01[..., :m], X01[..., m:]
+            R = torch.stack((torch.stack((S_diag[0] - S_up[0] @ X0[0], -(S_up[0] @ X1[0]))),
+                             torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
+            self._T = (("twisted", op), X01)
         else:
             k = n - 1                           # interior lines 1..n-1 -> rows 0..k-1 of T
             Dinv = torch.empty((k, m, m), dtype=f64, device=dev)
@@ -102,10 +116,7 @@ class StripLineSolver(VelocityJacobianSolver):
                              torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
             # the solve's operators: the fused block-Thomas sweep of the interior lines (one GEMV per line and
             # direction, as the whole-mesh sweep) and [X0 | X1] for the back substitution in one batched GEMV
-            if self.sweep_form == "twisted" and k >= 3 and dev.type == "cuda":   # two-ended, as the whole mesh
-                th = ("twisted", twisted_thomas_operators(S_diag[1:n], S_up[1:n - 1], S_lo[1:n - 1]))
-            else:
-                th = ("single", fused_thomas_operators(Dinv, S_lo[1:n - 1] if n > 2 else None, Uh[:k - 1]))
+            th = ("single", fused_thomas_operators(Dinv, S_lo[1:n - 1] if n > 2 else None, Uh[:k - 1]))
             X01 = torch.cat((X0, X1), dim=2)
             del Dinv, Uh, X0, X1
             self._T = (th, X01)

@@ -322,6 +322,29 @@ def twisted_thomas_solve(op, g):
     return x
 
 
+def twisted_thomas_solve_mat(op, g):
+    """X = S^-1 G for a block right-hand side G (n, m, c) from twisted_thomas_operators: the recurrences of
+    twisted_thomas_solve with GEMMs (the strip solve's coupling solutions X0, X1 from the same factors as its sweep,
+    strip_solve.StripLineSolver._sweep_factor; ADVICE r4: no second, one-ended set of pivot inverses)."""
+    k, D0, E0, FT, FB, FM, UhT, UhB = op
+    n, m = g.shape[0], g.shape[1]
+    z = [None] * n                    # z_L (top chain, L < k), w_L (bottom chain, L > k)
+    z[0] = D0 @ g[0]
+    for L in range(1, k):
+        z[L] = FT[L - 1, :, :m] @ g[L] + FT[L - 1, :, m:] @ z[L - 1]
+    z[n - 1] = E0 @ g[n - 1]
+    for L in range(n - 2, k, -1):
+        i = L - (k + 1)
+        z[L] = FB[i, :, :m] @ g[L] + FB[i, :, m:] @ z[L + 1]
+    x = torch.empty_like(g)
+    x[k] = FM[:, :m] @ g[k] + FM[:, m:2 * m] @ z[k - 1] + FM[:, 2 * m:] @ z[k + 1]
+    for L in range(k - 1, -1, -1):
+        x[L] = z[L] - UhT[L] @ x[L + 1]
+    for L in range(k + 1, n):
+        x[L] = z[L] - UhB[L - (k + 1)] @ x[L - 1]
+    return x
+
+
 def fused_thomas_solve(D0, F, Uh, g):
     """x = S^-1 g from fused_thomas_operators (g: (n, m), not modified).  W[L] = [g_L | z_{L-1}]: the
     forward GEMV of line L reads one contiguous 2m vector and writes z_L straight into W[L+1]'s second

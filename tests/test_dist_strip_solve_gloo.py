@@ -85,6 +85,7 @@ def _worker(rank, world, port, case, q):
     (2, (4, 4, 3, 300.0, 2, False)),    # two columns per strip: one interior interface line each
     (2, (3, 2, 4, 100.0, 2, True)),     # one column per strip: no interior line; block-LU edge inverses
     (3, (4, 7, 2, 700.0, 2, False)),    # uneven strips (3, 2, 2 columns)
+    (2, (3, 9, 2, 300.0, 2, False)),    # strips of 5 and 4 columns: the two-ended interior sweep, X0 / X1 from its factors
     (3, (5, 6, 3, 40.0, 1, False)),     # the one-component (CD) operator
     # cfg5's world size: 8 ranks over 11 columns (strips of 2, 2, 2, 1, 1, 1, 1, 1 columns:
     # uneven, one-column strips with no interior line), and the CD operator over 9 columns (2, 1 x 7)

@@ -172,6 +172,12 @@ def test_twisted_thomas_matches_dense_solve(n, m):
     want = torch.linalg.solve(A, rhs.reshape(-1)).reshape(n, m)
     got = twisted_thomas_solve(twisted_thomas_operators(Sd, Su, Sl), rhs)
     assert (got - want).abs().max().item() <= 1e-12 * want.abs().max().item()
+    # block right-hand sides (the strip solve's coupling solutions X0, X1 from the twisted factors)
+    from sem_amd.solvers.velocity_solve import twisted_thomas_solve_mat
+    Rm = torch.rand((n, m, 3), dtype=f64, generator=g) - 0.5
+    wantm = torch.linalg.solve(A, Rm.reshape(n * m, 3)).reshape(n, m, 3)
+    gotm = twisted_thomas_solve_mat(twisted_thomas_operators(Sd, Su, Sl), Rm)
+    assert (gotm - wantm).abs().max().item() <= 1e-12 * wantm.abs().max().item()
     # the one-ended sweep's operators from the same blocks
     Dinv = torch.empty_like(Sd)
     Uh = torch.empty_like(Su)

@@ -183,6 +183,15 @@ for s in "$@"; do
       step stripsolotrace 600 rocprofv3 --kernel-trace --stats -d "$O/stripsolotrace" -o trace --output-format csv -- \
         python tools/strip_profile.py --mode solo --ne 128 --P 12 --G 8 --ranks 3 --reps 10 --whole 0
       find "$O/stripsolotrace" -name "*kernel_trace.csv" -size +20M -delete ;;
+    cfg4a)      # BASELINE cfg4 end to end, part 1: Ra 1e3 -> 1e4 -> 1e5 -> 3e5 from rest, checkpointed
+      step cfg4a 1150 python -u tools/bous_solve.py --ne 48 --P 8 --continuation 1e3,1e4,1e5 --Ra 3e5 --iprint 2 \
+        --ckpt "$O/ckpt" --out "$O/cfg4_to3e5.json" ;;
+    cfg4b)      # part 2: Ra = 1e6 from the Ra = 3e5 state (ckpt/bous_48_300000.npy, copied into the tree)
+      step cfg4b 1150 python -u tools/bous_solve.py --ne 48 --P 8 --Ra 1e6 --x0 ckpt/bous_48_300000.npy --iprint 2 \
+        --ckpt "$O/ckpt" --out "$O/cfg4_ra1e6.json" ;;
+    cfg4c)      # part 3 (if part 2 hit its limit): Ra = 1e6 resumed from the last Newton checkpoint
+      step cfg4c 1150 python -u tools/bous_solve.py --ne 48 --P 8 --Ra 1e6 --x0 ckpt/bous_48_1e+06_newton.npy --resume 1 \
+        --iprint 2 --ckpt "$O/ckpt" --out "$O/cfg4_ra1e6_resumed.json" ;;
     stripprof128)
       step stripprof128 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
         --master-port 29632 tools/strip_profile.py --mode rehearsal --ne 128 --P 12 --reps 3 --iters 10 \
