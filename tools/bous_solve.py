@@ -48,6 +48,7 @@ def main():
                               schur_precond=args.schur_precond)
         if args.iprint >= 2:
             c.cd._progress = c.ns._progress = 500
+            c.ns._iprint = list(c.ns._iprint) + ["LU_suc"]   # factor times and the refinement gate's backward error
         def ckpt(xs, k, Ra=Ra):
             if args.ckpt:
                 os.makedirs(args.ckpt, exist_ok=True)
