@@ -131,7 +131,7 @@ enum sem_tune {
   SEM_TUNE_BAND_CPOL = 1, /* SEM_BAND_CPOL: cache policy of the band kernel's y stores / u,v loads */
   SEM_TUNE_BAND_KP = 2,   /* SEM_BAND_KP: -1 = struct-only kernel arguments, else preloaded      */
   SEM_TUNE_MARCH_WG = 3,  /* SEM_MARCH_WG: workgroups of the marching variant                     */
-  SEM_TUNE_MFMA_TILE = 4, /* SEM_MFMA_TILE: MFMA kernel tile                                      */
+  SEM_TUNE_MFMA_TILE = 4, /* SEM_MFMA_TILE: 0 = band-form MFMA kernel; 1, 2, 3 = element-block MFMA */
   SEM_TUNE_COL_TILE = 5,  /* SEM_COL_TILE: column kernel tile                                     */
   SEM_TUNE_NS_APPLY = 6,  /* SEM_NS_APPLY: 1 = sem_ns_apply's LDS-tile form instead of the band form
                            * (the one knob whose variants agree to rounding, not bitwise)           */

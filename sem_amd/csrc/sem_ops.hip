@@ -39,6 +39,8 @@ namespace sem {
 
 int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s);  // apply_band.hip
 std::string band_kernel_name(int P, long long n_local);
+int launch_apply_bmfma(const ApplyArgs& a, const sem_handle* h, hipStream_t s);  // apply_band.hip
+std::string bmfma_kernel_name(int P);
 
 static int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) return SEM_OK;
@@ -685,7 +687,7 @@ static int launch_apply_mfma_auto(const ApplyArgs& args, const sem_handle* h, hi
   const int force = tune(SEM_TUNE_MFMA_TILE);  // tuning knob (sem_set_tuning / SEM_MFMA_TILE, read once)
   if (force == 2 || (force == 0 && big_tiles >= 4 * 256)) return launch_apply_mfma<P, TL, TL, 4, true, false>(args, h, s);
   if (force == 1) return launch_apply_mfma<P, TS, TS, 2, false, false>(args, h, s);
-  return launch_apply_mfma<P, TS, TS, 4, false, true>(args, h, s);
+  return launch_apply_mfma<P, TS, TS, 4, false, true>(args, h, s);   // force 3: the round-4 default
 }
 
 // =========================================================================== column kernel
@@ -1134,7 +1136,11 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   if (d->dir_mode < SEM_DIR_NONE || d->dir_mode > SEM_DIR_REPLACE) return set_error(SEM_EINVAL, "bad dir_mode");
   if (d->dir_mode == SEM_DIR_REPLACE && !d->dir_val) return set_error(SEM_EINVAL, "SEM_DIR_REPLACE needs dir_val");
   if (d->algo < SEM_ALGO_AUTO || d->algo > SEM_ALGO_BAND) return set_error(SEM_EINVAL, "bad algo");
-  if (d->algo == SEM_ALGO_MFMA && h->P > 15) return set_error(SEM_EUNSUPPORTED, "MFMA path needs P <= 15");
+  // SEM_ALGO_MFMA: the band-form MFMA kernel (apply_bmfma, P <= 16; round 5); SEM_MFMA_TILE = 1, 2, 3 select the
+  // element-block MFMA kernel of rounds 1-4 (apply_tp_mfma, P <= 15) for A/B
+  const bool legacy_mfma = tune(SEM_TUNE_MFMA_TILE) != 0;
+  if (d->algo == SEM_ALGO_MFMA && legacy_mfma && h->P > 15)
+    return set_error(SEM_EUNSUPPORTED, "the element-block MFMA path needs P <= 15");
   const bool ranged = d->pos_end > 0;
   if (ranged && (d->pos_begin < 0 || d->pos_begin >= d->pos_end || d->pos_end > h->ex_end - h->ex_begin + 1))
     return set_error(SEM_EINVAL, "element-position range outside [0, ex_end - ex_begin + 1)");
@@ -1208,6 +1214,7 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   }
   const bool mfma = d->algo == SEM_ALGO_MFMA || d->algo == SEM_ALGO_AUTO;
   if (mfma && !fits32) return set_error(SEM_EUNSUPPORTED, "MFMA path needs n_local < 2^28");
+  if (d->algo == SEM_ALGO_MFMA && !legacy_mfma) return launch_apply_bmfma(a, h, s);
   if (mfma) {
     switch (h->P) {
 #define SEM_MCASE(PP) \
@@ -1240,6 +1247,8 @@ int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
     name = band_kernel_name(P, h->n_local);
   } else if (algo == SEM_ALGO_COLUMN || algo == SEM_ALGO_AUTO) {
     name = "sem::apply_tp_col<" + std::to_string(P) + ", 2, 64, 1>";
+  } else if (algo == SEM_ALGO_MFMA && tune(SEM_TUNE_MFMA_TILE) == 0) {
+    name = bmfma_kernel_name(P);
   } else if ((algo == SEM_ALGO_MFMA || algo == SEM_ALGO_AUTO) && P <= 15) {
     const int TL = std::max(1, 32 / P), TS = std::max(1, 16 / P);
     const long long big = static_cast<long long>((h->ex_end - h->ex_begin + TL - 1) / TL) * ((h->ney + TL - 1) / TL);

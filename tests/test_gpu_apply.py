@@ -70,7 +70,9 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
          (8, 17, 5), (9, 3, 4), (10, 2, 2), (11, 3, 1), (12, 5, 3), (13, 2, 3), (14, 1, 2), (15, 2, 2), (16, 3, 2)]
 
 
-ALGOS = [1, 2, 3, 4, "4dpp", "4m", "4mdpp", "4smem"]  # VALU two-phase, MFMA, column kernel, assembled band (+ DPP coefficient variant)
+# VALU two-phase, MFMA (band form, round 5), column kernel, assembled band (+ DPP coefficient variant), and the
+# element-block MFMA kernel of rounds 1-4 ("2eb": SEM_MFMA_TILE = 3)
+ALGOS = [1, 2, 3, 4, "4dpp", "4m", "4mdpp", "4smem", "2eb"]
 BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2", "4t5": "5", "4t6": "6", "4imm": "4",
                  "4m": "7", "4mdpp": "8", "4smem": "9"}  # 4m*: marching kernel (P = 8, 12; other P fall back to the band tile)  # SEM_TUNE_BAND_TILE values
 
@@ -78,6 +80,9 @@ BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2", "4t5": "5", "4t6": "6", "4
 def _algo(algo, tuning):
     """Select the kernel: an int is sem_apply_desc.algo; a band variant name also sets the band-tile knob."""
     from sem_amd import _lib
+    if algo == "2eb":
+        tuning(_lib.TUNE_MFMA_TILE, "3")
+        return 2
     if isinstance(algo, str):
         tuning(_lib.TUNE_BAND_TILE, BAND_VARIANTS[algo])
         return 4
@@ -87,8 +92,8 @@ def _algo(algo, tuning):
 @pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("P,nex,ney", CASES)
 def test_fused_apply_vs_oracle(gpu, P, nex, ney, algo, tuning):
-    if algo == 2 and P > 15:
-        pytest.skip("MFMA path covers P <= 15")
+    if algo == "2eb" and P > 15:
+        pytest.skip("the element-block MFMA kernel covers P <= 15")
     algo = _algo(algo, tuning)
     from sem_amd.device import get_mesh
     Lx, Ly = 1.3, 0.7

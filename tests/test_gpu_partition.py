@@ -16,8 +16,6 @@ def rel(a, b):
 @pytest.mark.parametrize("algo", [1, 2, 3, 4])
 @pytest.mark.parametrize("P,nex,ney,G", [(4, 6, 5, 2), (8, 9, 7, 3), (8, 64, 64, 8), (12, 5, 4, 5), (16, 4, 3, 2)])
 def test_strip_partition_matches_full_apply(gpu, P, nex, ney, G, algo):
-    if algo == 2 and P > 15:
-        pytest.skip("MFMA path covers P <= 15")
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     from sem_amd.parallel import StripPartition

@@ -42,7 +42,7 @@ for s in "$@"; do
       for nr in 2 4; do for ex in allreduce p2p; do
         step benchgloo_${nr}_$ex 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $nr \
           --master-addr 127.0.0.1 --master-port 2962$nr bench.py --gpus $nr --steps 20 --warmup 5 \
-          --dist-backend gloo --exchange $ex --cpu-seconds 0 --hbm-ne 0
+          --dist-backend gloo --exchange $ex --cpu-seconds 0 --extra-steps 20
       done; done ;;
     benchdrv)   step benchdrv 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;   # the driver's command
     pmccd64)    tools/pmc_run.sh "$O/pmc_cd64" -- python tools/kbench.py --meshes 8:64 --reps 200 || exit 1 ;;
@@ -192,6 +192,15 @@ for s in "$@"; do
     cfg4c)      # part 3 (if part 2 hit its limit): Ra = 1e6 resumed from the last Newton checkpoint
       step cfg4c 1150 python -u tools/bous_solve.py --ne 48 --P 8 --Ra 1e6 --x0 ckpt/bous_48_1e+06_newton.npy --resume 1 \
         --iprint 2 --ckpt "$O/ckpt" --out "$O/cfg4_ra1e6_resumed.json" ;;
+    bmfma)      # band-form MFMA kernel (round 5): parity, then A/B against the band VALU kernel and the element-block
+                # MFMA kernel of rounds 1-4 (SEM_MFMA_TILE=3), and the counter passes of the new kernel at cfg2
+      step bmfmatests 900 $PYT tests/test_gpu_apply.py tests/test_gpu_partition.py
+      for rep in 1 2; do
+        TAILN=4 step bmfma_ab_new_$rep 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 500 --algo 2
+        SEM_MFMA_TILE=3 TAILN=4 step bmfma_ab_eb_$rep 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 500 --algo 2
+        TAILN=4 step bmfma_ab_band_$rep 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 500 --algo 0
+      done
+      tools/pmc_run.sh "$O/pmc_bmfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1 ;;
     stripprof128)
       step stripprof128 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
         --master-port 29632 tools/strip_profile.py --mode rehearsal --ne 128 --P 12 --reps 3 --iters 10 \
