@@ -293,7 +293,7 @@ def _worker_strip_velocity(rank, world, port, q, case):
         want = spla.spsolve(ref.Jvelo.tocsc(), np.hstack((bu, bv)))
         xu, xv = vs.solve(d(bu), d(bv))
         err = max(np.abs(xu.cpu().numpy() - want[:ref.N][sl]).max(), np.abs(xv.cpu().numpy() - want[ref.N:][sl]).max())
-        q.put((rank, err / np.abs(want).max()))
+        q.put((rank, err / np.abs(want).max(), sl.start, xu.cpu().numpy(), xv.cpu().numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -310,8 +310,22 @@ def test_strip_velocity_solve_real_kernels(gpu, world, case):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, err in out:
+    for rank, err, *_ in out:
         assert err <= 1e-9, (rank, err)
+    # backward error of the assembled strip solution with the reference's own Jacobian: the
+    # forward error above is bounded by cond(J) times this
+    from velocity_blocks import oracle_velocity_jacobian
+    P, nex, ney, Re = case
+    ref, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    xu, xv = np.zeros(ref.N), np.zeros(ref.N)
+    for _, _, start, lu, lv in out:      # shared lines hold equal values on both ranks
+        xu[start:start + lu.size], xv[start:start + lv.size] = lu, lv
+    r = np.random.default_rng(3)
+    b = np.hstack((r.uniform(-1, 1, ref.N), r.uniform(-1, 1, ref.N)))
+    J, x = ref.Jvelo.tocsr(), np.hstack((xu, xv))
+    eta = np.abs(J @ x - b).max() / (abs(J).sum(axis=1).max() * np.abs(x).max() + np.abs(b).max())
+    print(f"strip solve over {world} ranks: backward error {eta:.1e}")
+    assert eta <= 1e-13, eta
 
 
 MTOL5 = 1e-13   # the couplers' mtol_internal (Boussinesq_SequentialCoupler.py:61-63)

@@ -201,6 +201,7 @@ for s in "$@"; do
         TAILN=4 step bmfma_ab_band_$rep 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 500 --algo 0
       done
       tools/pmc_run.sh "$O/pmc_bmfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1 ;;
+    gemvshapes) TAILN=4 step gemvshapes 300 python tools/gemv_shapes.py ;;
     stripprof128)
       step stripprof128 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
         --master-port 29632 tools/strip_profile.py --mode rehearsal --ne 128 --P 12 --reps 3 --iters 10 \

@@ -220,6 +220,53 @@ def rehearsal(args):
     dist.destroy_process_group()
 
 
+def graph_ms(fn, dev, reps):
+    fn()
+    torch.cuda.synchronize(dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        fn()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize(dev)
+        ts.append(a.elapsed_time(b))
+    del g
+    return float(np.median(ts))
+
+
+def graph_parts(vs, dev, reps):
+    """Device time of the strip solve's pieces, each captured and replayed alone."""
+    from sem_amd.solvers.velocity_solve import _gemv
+    m, n = vs.m, vs.nex
+    B = torch.rand((vs.NX, m), dtype=torch.float64, device=dev)
+    g = torch.rand((n + 1, m), dtype=torch.float64, device=dev)
+    out = {"solve_lines": graph_ms(lambda: vs._solve_lines(B), dev, reps),
+           "iface_solve": graph_ms(lambda: vs._iface_solve(g.clone()), dev, reps)}
+    if vs._T is not None:
+        out["interior_sweep"] = graph_ms(lambda: vs._thomas(g[1:n]), dev, reps)
+        X01 = vs._T[1]
+        xb2 = torch.rand(2 * m, dtype=torch.float64, device=dev)
+        yk = torch.rand((n - 1) * m, dtype=torch.float64, device=dev)
+        out["back_substitution_gemv"] = graph_ms(lambda: _gemv(X01.view(-1, X01.shape[-1]), xb2, yk, alpha=-1.0,
+                                                               beta=1.0), dev, reps)
+        out["back_substitution_GB"] = X01.numel() * 8 / 1e9
+    if getattr(vs, "_Z", None) is not None:
+        h = torch.rand(vs._Z.shape[1], dtype=torch.float64, device=dev)
+        x2 = torch.empty(2 * m, dtype=torch.float64, device=dev)
+        out["reduced_rows_gemv"] = graph_ms(lambda: _gemv(vs._Z, h, x2), dev, reps)
+        out["reduced_rows_GB"] = vs._Z.numel() * 8 / 1e9
+    return out
+
+
 def loopback_gather(fake):
     """StripLineSolver._all_gather for the loopback group: slot r is this rank's tensor; the other slots copy it,
     and the reduced-system blocks R of the other strips (4-D) get a boosted diagonal -- replicated R blocks would
@@ -287,6 +334,9 @@ def solo(args):
                 torch.cuda.synchronize(dev)
                 ts.append(a.elapsed_time(b))
             rec["graph_matvec_ms"] = float(np.median(ts))
+        # graph-replayed parts of the strip velocity solve (the eager phase split above includes Python launch
+        # gaps; these are device time of each piece alone)
+        rec["graph_parts_ms"] = graph_parts(vs, dev, args.reps)
         # Krylov step sweeps over the strip at several basis sizes (device time, one rank's share)
         ks = {}
         for k in (100, 300, 600):
