@@ -1273,6 +1273,7 @@ template <int P, bool FULL, bool GRAD>
 __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs a) {
   using C = BMCfg<P>;
   __shared__ double Ts[C::SL * C::PT];
+  __shared__ double ws[P + 1];   // GLL weights: one LDS read per node instead of a compare-select chain per weight
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lk = lane >> 4;
@@ -1322,6 +1323,7 @@ __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs 
       Ts[C::ts(rr, cc)] = (gy >= 0 && gy < NY) ? st[q] : 0.0;
     }
   }
+  if (tid <= P) ws[tid] = gll_w<P>(tid);
   // pointwise operands, issued after the staging stores (they land during the products)
   double pu[4], pv[4];
   NodeOps ops[4] = {};
@@ -1359,7 +1361,7 @@ __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs 
   constexpr double G00 = GllConst<P>::G[0], GPP = GllConst<P>::G[P * (P + 1) + P];
   const int lj = gyn % P, ne = gyn / P;
   const bool hasLy = lj == 0 && ne - 1 >= 0, hasRy = lj != 0 || ne < a.ney;
-  const double my = lj != 0 ? gll_w<P>(lj) : (hasLy ? wP : 0.0) + (hasRy ? w0 : 0.0);
+  const double my = lj != 0 ? ws[lj] : (hasLy ? wP : 0.0) + (hasRy ? w0 : 0.0);
   double zz[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -1367,7 +1369,7 @@ __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs 
     const double xv = Ts[C::ts(P + i, P + cb0 + lr)];
     const int li = i % P, me = gx / P;
     const bool hasLx = li == 0 && me - 1 >= a.ex_begin, hasRx = li != 0 || me < a.ex_end;
-    const double mx = li != 0 ? gll_w<P>(li) : (hasLx ? wP : 0.0) + (hasRx ? w0 : 0.0);
+    const double mx = li != 0 ? ws[li] : (hasLx ? wP : 0.0) + (hasRx ? w0 : 0.0);
     double XK = xk[r], XG = xg[r], YK = yk[r], YG = yg[r];
     if (li == 0) {   // a shared row without its left / right element: drop that element's diagonal term
       if (!hasLx) { XK = fma(-KPP, xv, XK); XG = fma(-GPP, xv, XG); }

@@ -201,6 +201,9 @@ for s in "$@"; do
         TAILN=4 step bmfma_ab_band_$rep 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 500 --algo 0
       done
       tools/pmc_run.sh "$O/pmc_bmfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1 ;;
+    bmfmapmc)   TAILN=4 step bmfma_apply 300 $PYT tests/test_gpu_apply.py tests/test_gpu_partition.py
+      TAILN=4 step bmfma_kb 300 python tools/kbench.py --meshes 8:64,12:128,8:1024 --reps 500 --algo 2
+      tools/pmc_run.sh "$O/pmc_bmfma64" -- python tools/kbench.py --meshes 8:64 --reps 200 --algo 2 || exit 1 ;;
     gemvshapes) TAILN=4 step gemvshapes 300 python tools/gemv_shapes.py ;;
     stripprof128)
       step stripprof128 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
