@@ -192,7 +192,8 @@ def rehearsal(args):
     vs = ns._strip_velocity_solver()
     torch.cuda.synchronize(dev)
     rec["factor_s"] = time.perf_counter() - t0
-    say(f"factor {rec['factor_s']:.2f} s")
+    rec["refine"], rec["refine_eta"] = bool(vs.refine), vs.refine_eta
+    say(f"factor {rec['factor_s']:.2f} s, backward error {vs.refine_eta:.1e}, refine {vs.refine}")
     for k in list(stats):
         stats[k][:] = [0, 0, 0.0]
     wall, tab = time_eager_matvecs(ns, vs, args.reps, dev)
@@ -309,6 +310,11 @@ def solo(args):
         torch.cuda.synchronize(dev)
         rec["factor_s"] = time.perf_counter() - t0
         rec["factor_gb_resident"] = torch.cuda.memory_allocated(dev) / 1e9
+        # the loopback group's stand-in reduced blocks make the refinement gate's probe meaningless (it measured a
+        # large backward error and switched refinement on, doubling every solve): time the plain solve, as a real
+        # partition whose gate passes runs it
+        rec["refine_eta_loopback"] = vs.refine_eta
+        vs.refine = False
         rec["twisted_interior"] = vs._T is not None and vs._T[0][0] == "twisted"
         fake.calls.clear()
         wall, tab = time_eager_matvecs(ns, vs, args.reps, dev)
