@@ -47,6 +47,10 @@ class StripLineSolver(VelocityJacobianSolver):
         # of its inverse (one GEMV per solve); "cr" factors and solves it whole on every rank (round 4, A/B)
         self.reduced = os.environ.get("SEM_STRIP_REDUCED", "rows")
 
+    def _probe_lines(self):
+        """This strip's lines eb P .. ee P among the mesh's nex P + 1 (refinement probes agree on shared lines)."""
+        return self.eb * self.P, self.ee * self.P + 1, self.nex_global * self.P + 1
+
     # ------------------------------------------------------------------ factor
     def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
         """Assemble the strip's condensed pieces on its strip handle (HIP) and factor."""

@@ -1129,9 +1129,14 @@ class VelocityJacobianSolver:
             raise RuntimeError("set_operator() first")
         if tau is None:
             tau = float(os.environ.get("SEM_REFINE_ETA", "1e-13"))
+        # probe vectors drawn over the GLOBAL lines and sliced: on a partition, a shared line's entries must be equal
+        # on both ranks (the strip solve's contract); per-rank draws made them differ and the residual of the
+        # inconsistent right-hand side read as a backward error of 1e-4 at cfg5 (a false refinement)
+        l0, l1, NXg = self._probe_lines()
         g = torch.Generator(device=self.device).manual_seed(seed)
-        b = torch.rand((self.NX, self.m), dtype=torch.float64, device=self.device, generator=g) * 2 - 1
-        sgn = torch.sign(torch.rand((self.NX, self.m), dtype=torch.float64, device=self.device, generator=g) - 0.5)
+        b = (torch.rand((NXg, self.m), dtype=torch.float64, device=self.device, generator=g) * 2 - 1)[l0:l1].contiguous()
+        sgn = torch.sign(torch.rand((NXg, self.m), dtype=torch.float64, device=self.device, generator=g)
+                         - 0.5)[l0:l1].contiguous()
         self.refine = False
         x = self._solve_lines(b)
         r = b - self._apply(x)
@@ -1140,6 +1145,10 @@ class VelocityJacobianSolver:
         self.refine_eta = eta
         self.refine = eta > tau
         return eta
+
+    def _probe_lines(self):
+        """(first, end, count) of this solver's lines among all lines of the mesh: the whole mesh here."""
+        return 0, self.NX, self.NX
 
     def _solve_lines(self, B):
         """x = J^-1 b with b, x as (NX, 2 NY) line arrays (every line: u then v); with `refine` set, one step of

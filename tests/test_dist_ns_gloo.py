@@ -73,6 +73,10 @@ def _worker(rank, world, port, case, q):
         ref.calc_jacobians(uo, vo)
         rhs = ref.dresiduals(0.1 * du, 0.1 * dv, 0.1 * dp)
         d = ns._get_update(*rhs)
+        if getattr(ns, "_velo", None) is not None and ns._velo.refine_eta is not None:
+            # the refinement gate's probe is consistent across ranks (shared lines equal): it measures the strip
+            # factor's real backward error (per-rank probes read 1e-4 at cfg5 and refined every solve)
+            errs["gate_eta"] = ns._velo.refine_eta
         want = ref.update(*rhs, mtol=1e-11)[:2]
         errs["update"] = max(np.abs(a - b).max() for a, b in zip(d[:2], want))
         # the update solves the oracle's linearised system to the Schur tolerance (mtol sqrt(N))
@@ -115,6 +119,8 @@ def test_partitioned_ns_solver_gloo(world, case):
         # LGMRES stop at the same residual bound, not at the same iterate
         assert e["update"] < (1e-9 if case[6] == "central" else 1e-8), (rank, e)
         assert e["update_res"] <= 10 * e["tol"], (rank, e)
+        if "gate_eta" in e:
+            assert e["gate_eta"] < 1e-13, (rank, e)
         if case[7]:
             assert e["newton"][0] == e["newton"][1], (rank, e)
             assert e["solve"] < 1e-8, (rank, e)

@@ -40,6 +40,7 @@ def _worker(rank, world, port, q, kind):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 16 // world))   # ranks share the box's CPU share: no OpenMP oversubscription
     try:
         from sem_amd.device import get_mesh
         from sem_amd.parallel import DistributedInner, StripPartition
@@ -90,6 +91,7 @@ def _worker_solver(rank, world, port, q, kind, overlap):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 16 // world))   # ranks share the box's CPU share: no OpenMP oversubscription
     try:
         from sem_amd.parallel import Partition
         from sem_amd.solvers import ConvectionDiffusionSolver
@@ -167,6 +169,7 @@ def _worker_ns(rank, world, port, q, kind):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 16 // world))   # ranks share the box's CPU share: no OpenMP oversubscription
     try:
         from sem_amd.parallel import Partition
         from sem_amd.solvers import NavierStokesSolver
@@ -219,6 +222,7 @@ def _worker_cfg5(rank, world, port, q):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 16 // world))   # ranks share the box's CPU share: no OpenMP oversubscription
     try:
         from sem_amd.solvers.boussinesq import partitioned_coupler
         c5 = CFG5
@@ -269,6 +273,7 @@ def _worker_strip_velocity(rank, world, port, q, case):
     sys.path[:0] = [os.path.dirname(here), here]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 16 // world))   # ranks share the box's CPU share: no OpenMP oversubscription
     try:
         from velocity_blocks import oracle_velocity_jacobian
         import scipy.sparse.linalg as spla
@@ -348,6 +353,7 @@ def _worker_cfg5_update(rank, world, port, q):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(max(1, 16 // world))   # ranks share the box's CPU share: no OpenMP oversubscription
     try:
         from sem_amd.parallel import Partition
         from sem_amd.solvers import NavierStokesSolver
