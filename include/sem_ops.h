@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 11
+#define SEM_ABI_VERSION 12
 
 enum sem_status {
   SEM_OK = 0,
@@ -136,7 +136,8 @@ enum sem_tune {
   SEM_TUNE_NS_APPLY = 6,  /* SEM_NS_APPLY: 1 = sem_ns_apply's LDS-tile form instead of the band form
                            * (the one knob whose variants agree to rounding, not bitwise)           */
   SEM_TUNE_EDGE_THOMAS = 7, /* SEM_EDGE_THOMAS: 1 = the ABI-9 runtime-width edge sweep of sem_nested_solve
-                             * instead of the templated one (A/B only; agrees to rounding)             */
+                             * instead of the templated one, 2 = the one-ended templated sweep even when
+                             * the two-ended factors are given (ABI 12; A/B only; agree to rounding)     */
   SEM_TUNE_BAND_ORDER = 8,  /* SEM_BAND_ORDER: 1 = the band kernel's full tiles before its ghost tiles in
                              * every XCD's share (measured slower; A/B only; bitwise identical) */
   SEM_TUNE_COUNT = 9
@@ -317,6 +318,15 @@ typedef struct sem_nested_desc {
    * columns edges n, n+1), and a work array Pw of nex * 2 * m doubles.  Used by sem_nested_iface_rhs. */
   const double* ABY;
   double* Pw;
+  /* ABI 12 (nullable; block-Thomas form only): the two-ended edge sweep.  The chain from edge 0 (Ed, El, Eu for
+   * k < edge_mid, as above) and the chain from edge N_ey (Edb[k] = inverse pivot block of the bottom chain for
+   * k > edge_mid, Es[k] = A_up[k] raw (edge k <- k+1), Eub[k-1] = Edb[k] A_lo[k-1] (edge k <- k-1)) run side by
+   * side and meet at edge_mid (1 <= edge_mid <= N_ey - 1), Edb[edge_mid] = the inverse of the meeting block:
+   * N_ey + 2 dependent block steps per column instead of 2 N_ey + 1.  Row-major blocks, as Ed / El / Eu. */
+  const double* Es;
+  const double* Edb;
+  const double* Eub;
+  int edge_mid;
 } sem_nested_desc;
 /* Column e's right-hand side at R + e ld_r (interior offsets o = (l-1) m + c N_y + gy), minus
  * aIB[e][l-1][s][.] xB[e+s][.] when aIB and xB are given (the back substitution r = b - A_IB x_B);

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.environ.get("SEM_LIBDIR") or os.path.join(_HERE, "lib"), "libsemops.so")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 (TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE, TUNE_NS_APPLY,
  TUNE_EDGE_THOMAS, TUNE_BAND_ORDER) = range(9)
@@ -51,7 +51,8 @@ class SemNestedDesc(C.Structure):
                 ("Xi", C.c_void_p), ("Aei", C.c_void_p), ("Yie", C.c_void_p), ("Se", C.c_void_p),
                 ("pi", C.c_void_p), ("pe", C.c_void_p), ("T", C.c_void_p), ("C", C.c_void_p), ("Ye", C.c_void_p),
                 ("Ed", C.c_void_p), ("El", C.c_void_p), ("Eu", C.c_void_p), ("XiB", C.c_void_p), ("AXB", C.c_void_p),
-                ("ABY", C.c_void_p), ("Pw", C.c_void_p)]
+                ("ABY", C.c_void_p), ("Pw", C.c_void_p), ("Es", C.c_void_p), ("Edb", C.c_void_p), ("Eub", C.c_void_p),
+                ("edge_mid", C.c_int)]
 
 
 class SemNsDesc(C.Structure):

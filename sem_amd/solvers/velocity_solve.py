@@ -527,6 +527,15 @@ class VelocityJacobianSolver:
             Et = [torch.empty(sh, **z) for sh in ((nex, ney + 1, ne1, ne1), (nex, ney, ne1, ne1), (nex, ney, ne1, ne1))]
             self._EtT = tuple(Et)                                   # row-major blocks (ABI 10)
             self._Ed, self._El, self._Eu = Et
+        # ABI 12: the two-ended edge sweep (chains from edge 0 and from edge N_ey meeting at edge mid): its bottom
+        # chain's factors beside the one-ended ones (which the torch path, the dense fallback and the top chain use)
+        self._edge_mid = (ney + 1) // 2
+        self._edge_twisted = (self._edge_thomas and self.device.type == "cuda" and ney + 1 >= 3
+                              and os.environ.get("SEM_EDGE_TWISTED", "1") != "0")
+        self._Etw = None
+        if self._edge_twisted:   # Es = A_up (raw), Edb[k >= mid] = bottom pivot inverses / M^-1, Eub[k-1] = UhB_k
+            self._Etw = tuple(torch.empty(sh, **z) for sh in ((nex, ney, ne1, ne1), (nex, ney + 1, ne1, ne1),
+                                                               (nex, ney, ne1, ne1)))
         if self.device.type == "cuda":
             T = [torch.empty(s[:-2] + (s[-1], s[-2]), **z) for s in shapes]
             if self._edge_thomas:
@@ -638,6 +647,9 @@ class VelocityJacobianSolver:
             self._edge_to_dense(c0)
         if self._edge_thomas:
             self._Ed[c0:c1], self._El[c0:c1], self._Eu[c0:c1] = fac[0], Sl, fac[1]
+            if self._edge_twisted:
+                with self._phase("edge_twisted"):
+                    self._twisted_edge_factor(Sd, Su, Sl, fac, Se_inv, c0, c1)
         else:
             self._Se_inv[c0:c1] = Se_inv
         with self._phase("coupling_pieces"):
@@ -685,6 +697,34 @@ class VelocityJacobianSolver:
             Cv[:, n, :, n, :] += C_GG.permute(1, 0, 2, 3)
             inv = self._group_perm()
             return Cg[:, inv][:, :, inv]
+
+    def _twisted_edge_factor(self, Sd, Su, Sl, fac, Se_inv, c0, c1):
+        """Bottom chain and meeting block of the two-ended edge sweep (ABI 12), for columns [c0, c1):
+          bottom  Db_{nb-1} = Sd_{nb-1}^-1,  UhB_k = Db_k Sl_{k-1},  Db_k = (Sd_k - Su_k UhB_{k+1})^-1   (k > mid)
+          middle  M^-1 = (Sd_mid - Sl_{mid-1} UhT_{mid-1} - Su_mid UhB_{mid+1})^-1
+        (the top chain's Dinv_k, UhT_k = Dinv_k Su_k for k < mid are the one-ended factors).  M^-1 is the (mid, mid)
+        block of S^-1, so the checked dense inverse the factorisation already built pins it: a column whose M^-1
+        misses that block (a pivot of the bottom chain lost accuracy) turns the two-ended sweep off."""
+        Dinv, Uh = fac
+        nb, mid, b = Sd.shape[1], self._edge_mid, Sd.shape[2]
+        inv = lambda A: torch.linalg.inv_ex(A)[0]  # noqa: E731
+        Es, Edb, Eub = self._Etw
+        Es[c0:c1] = Su
+        Db = inv(Sd[:, nb - 1])
+        Edb[c0:c1, nb - 1] = Db
+        for k in range(nb - 1, mid, -1):
+            if k < nb - 1:
+                Db = inv(Sd[:, k] - Su[:, k] @ Eub[c0:c1, k])          # Eub[:, k] holds UhB_{k+1}
+                Edb[c0:c1, k] = Db
+            Eub[c0:c1, k - 1] = Db @ Sl[:, k - 1]                      # UhB_k
+        M = Sd[:, mid] - Sl[:, mid - 1] @ Uh[:, mid - 1] - Su[:, mid] @ Eub[c0:c1, mid]
+        Mi = inv(M)
+        Edb[c0:c1, mid] = Mi
+        want = Se_inv.view(Se_inv.shape[0], nb, b, nb, b)[:, mid, :, mid, :]
+        err = ((Mi - want).abs().amax(dim=(1, 2)) / want.abs().amax(dim=(1, 2)).clamp(min=1e-300)).max().item()
+        if not err <= 1e-9:
+            self._edge_twisted = False
+            self._Etw = None
 
     def _blocktri_inverse(self, Sd, Su, Sl, factors=False):
         """Dense inverse of block-tridiagonal matrices (batched over columns): diagonal blocks Sd (cc, nb, b, b),
@@ -750,7 +790,8 @@ class VelocityJacobianSolver:
         if self._hipT is not None:
             self._hipT = self._hipT[:3] + (SeT,)
         self._edge_thomas = False
-        self._Ed = self._El = self._Eu = self._EtT = None
+        self._edge_twisted = False
+        self._Ed = self._El = self._Eu = self._EtT = self._Etw = None
 
     @staticmethod
     def _blocktri_dense(Sd, Su, Sl):
@@ -1048,9 +1089,11 @@ class VelocityJacobianSolver:
                     raise RuntimeError("nested solve: edge offsets differ from the block-Thomas sweep's layout")
             q = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
             hb = self._hipB if getattr(self, "_hipB", None) is not None else (None, None, None)
+            tw = self._Etw if (self._edge_thomas and getattr(self, "_edge_twisted", False)) else (None, None, None)
             self._nd = _lib.SemNestedDesc(P, nex, ney, self.ncomp, self.NY, p(XiT), p(AeiT), p(YieT), q(SeT),
                                           p(self._pi), p(self._pe), p(T), p(Cw), p(Ye), *(q(t) for t in Et),
-                                          *(q(t) for t in hb), p(Pw))
+                                          *(q(t) for t in hb), p(Pw), *(q(t) for t in tw),
+                                          self._edge_mid if tw[0] is not None else 0)
         return self._nd
 
     def _own_rhs(self, g, B):

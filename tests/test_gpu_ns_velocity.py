@@ -255,16 +255,22 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
     J = ref.Jvelo.tocsr()
     lib = _lib.load()
 
-    def both(refine):
+    def both(refine, knob=1):
         ch.refine = refine
         x_new = torch.cat(ch.solve(bu, bv))
-        _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 1))
+        _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, knob))
         try:
             x_old = torch.cat(ch.solve(bu, bv))
         finally:
             _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
         return x_new, x_old
 
+    # ABI 12: the default sweep is the two-ended one wherever N_ey + 1 >= 3; knob 2 forces the one-ended templated sweep
+    assert ch._edge_twisted == (ney + 1 >= 3)
+    x_tw, x_one = both(False, knob=2)
+    e_tw, e_one = _eta(J, x_tw, bb), _eta(J, x_one, bb)
+    print(f"two-ended edge sweep {e_tw:.1e}, one-ended {e_one:.1e}")
+    assert max(e_tw, e_one) <= 4 * min(e_tw, e_one) + 1e-15
     x_new, x_old = both(False)
     e_new, e_old, e_lu = _eta(J, x_new, bb), _eta(J, x_old, bb), _eta(J, spla.spsolve(J.tocsc(), bb), bb)
     f_new, f_old = both(True)

@@ -179,6 +179,9 @@ for s in "$@"; do
         SEM_LIBDIR=$PWD/sem_amd/lib_diag SEM_ALLOW_DIAG=1 SEM_DIAG=$d tools/pmc_run.sh "$O/pmc_ghost_d$d" -- \
           python tools/kbench.py --meshes 8:64 --reps 200 || exit 1
       done ;;
+    stripsolocr)  # the round-4 reduced solve (block CR replicated on every rank) in the same solo measurement
+      SEM_STRIP_REDUCED=cr step stripsolocr 900 python tools/strip_profile.py --mode solo --ne 128 --P 12 --G 8 --ranks 3 \
+        --reps 10 --whole 0 --out "$O/strip_solo128_cr.jsonl" ;;
     stripsolotrace)  # kernel trace of one simulated cfg5 rank of 8 (factor + matvecs), per-kernel split of the strip solve
       step stripsolotrace 600 rocprofv3 --kernel-trace --stats -d "$O/stripsolotrace" -o trace --output-format csv -- \
         python tools/strip_profile.py --mode solo --ne 128 --P 12 --G 8 --ranks 3 --reps 10 --whole 0
