@@ -404,6 +404,9 @@ class VelocityJacobianSolver:
         # ABI-9 form: O(N_ey ne1^2) doubles per column read per solve instead of the n_e^2 of the dense
         # inverse -- 1.5 MB instead of 64 MB per cfg5 column); "dense" keeps the dense inverse
         self.edge_solve = "auto"
+        # ABI 12 two-ended edge sweep: "auto" on the GPU (the kernel's form), True also on the CPU (the torch form,
+        # for tests), False never
+        self.edge_two_ended = "auto"
         self._edge_thomas = False
         # HIP nested solves: "coupled" (ABI 11: the interface right-hand side from the forward element step's
         # T = Xi b_i and the edge values, sem_nested_iface_rhs; the back substitution T -= Xi A_iB x_B from the
@@ -528,14 +531,21 @@ class VelocityJacobianSolver:
             self._EtT = tuple(Et)                                   # row-major blocks (ABI 10)
             self._Ed, self._El, self._Eu = Et
         # ABI 12: the two-ended edge sweep (chains from edge 0 and from edge N_ey meeting at edge mid): its bottom
-        # chain's factors beside the one-ended ones (which the torch path, the dense fallback and the top chain use)
-        self._edge_mid = (ney + 1) // 2
-        self._edge_twisted = (self._edge_thomas and self.device.type == "cuda" and ney + 1 >= 3
-                              and os.environ.get("SEM_EDGE_TWISTED", "1") != "0")
+        # chain's factors beside the one-ended ones (which the dense fallback and the top chain use).  The meeting
+        # edge is chosen from a window around the middle after the last chunk (_twisted_edge_select)
+        nb = ney + 1
+        self._edge_mid = nb // 2
+        two = self.edge_two_ended
+        self._edge_twisted = (self._edge_thomas and nb >= 3 and os.environ.get("SEM_EDGE_TWISTED", "1") != "0"
+                              and (two is True or (two == "auto" and self.device.type == "cuda")))
         self._Etw = None
-        if self._edge_twisted:   # Es = A_up (raw), Edb[k >= mid] = bottom pivot inverses / M^-1, Eub[k-1] = UhB_k
+        if self._edge_twisted:   # Es = A_up (raw), Edb[k > mid] = bottom pivot inverses, Edb[mid] = M^-1, Eub[k-1] = UhB_k
             self._Etw = tuple(torch.empty(sh, **z) for sh in ((nex, ney, ne1, ne1), (nex, ney + 1, ne1, ne1),
                                                                (nex, ney, ne1, ne1)))
+            w = max(1, nb // 8)
+            self._tw_cand = list(range(max(1, self._edge_mid - w), min(nb - 2, self._edge_mid + w) + 1))
+            self._tw_Mi = torch.empty((nex, len(self._tw_cand), ne1, ne1), **z)
+            self._tw_ratio = torch.zeros(len(self._tw_cand), dtype=torch.float64)
         if self.device.type == "cuda":
             T = [torch.empty(s[:-2] + (s[-1], s[-2]), **z) for s in shapes]
             if self._edge_thomas:
@@ -594,6 +604,7 @@ class VelocityJacobianSolver:
                 S_up[c0:c1] -= C[:, :m, m:]
                 S_lo[c0:c1] -= C[:, m:, :m]
                 del C
+        self._twisted_edge_select()
         self._nested_finish()
         self.W = None
         self.aBI, self.aIB = aBI, aIB
@@ -699,32 +710,86 @@ class VelocityJacobianSolver:
             return Cg[:, inv][:, :, inv]
 
     def _twisted_edge_factor(self, Sd, Su, Sl, fac, Se_inv, c0, c1):
-        """Bottom chain and meeting block of the two-ended edge sweep (ABI 12), for columns [c0, c1):
-          bottom  Db_{nb-1} = Sd_{nb-1}^-1,  UhB_k = Db_k Sl_{k-1},  Db_k = (Sd_k - Su_k UhB_{k+1})^-1   (k > mid)
-          middle  M^-1 = (Sd_mid - Sl_{mid-1} UhT_{mid-1} - Su_mid UhB_{mid+1})^-1
-        (the top chain's Dinv_k, UhT_k = Dinv_k Su_k for k < mid are the one-ended factors).  M^-1 is the (mid, mid)
-        block of S^-1, so the checked dense inverse the factorisation already built pins it: a column whose M^-1
-        misses that block (a pivot of the bottom chain lost accuracy) turns the two-ended sweep off."""
+        """Bottom chain and candidate meeting blocks of the two-ended edge sweep (ABI 12), for columns [c0, c1):
+          bottom  Db_{nb-1} = Sd_{nb-1}^-1,  UhB_k = Db_k Sl_{k-1},  Db_k = (Sd_k - Su_k UhB_{k+1})^-1   (k > t)
+          middle  M_t^-1 = (Sd_t - Sl_{t-1} UhT_{t-1} - Su_t UhB_{t+1})^-1
+        (the top chain's Dinv_k, UhT_k = Dinv_k Su_k for k < t are the one-ended factors), for every candidate
+        meeting edge t of the window.  Block elimination without pivoting across blocks amplifies rounding by its
+        multipliers: a chain that runs into a nearly singular Schur complement (P = 16, 2 x 6 elements, Re = 300:
+        ||Db_4|| = 600 from the bottom, <= 10 from the top) gives a two-ended sweep 50x the one-ended backward
+        error if it meets there.  So each candidate is scored, per column, by its largest back-substitution
+        multiplier max(max_{k<t} ||UhT_k||, max_{k>t} ||UhB_k||) over the one-ended sweep's max_k ||UhT_k||, and
+        _twisted_edge_select keeps the best (the max over columns).  M_t^-1 is the (t, t) block of S^-1, so the
+        checked dense inverse pins it too: a candidate that misses it by 1e-9 is excluded."""
         Dinv, Uh = fac
-        nb, mid, b = Sd.shape[1], self._edge_mid, Sd.shape[2]
+        nb, b = Sd.shape[1], Sd.shape[2]
+        cand = self._tw_cand
         inv = lambda A: torch.linalg.inv_ex(A)[0]  # noqa: E731
+        nrm = lambda A: A.abs().sum(-1).amax(-1)   # noqa: E731  infinity norm per column
         Es, Edb, Eub = self._Etw
         Es[c0:c1] = Su
         Db = inv(Sd[:, nb - 1])
         Edb[c0:c1, nb - 1] = Db
-        for k in range(nb - 1, mid, -1):
+        for k in range(nb - 1, cand[0], -1):
             if k < nb - 1:
                 Db = inv(Sd[:, k] - Su[:, k] @ Eub[c0:c1, k])          # Eub[:, k] holds UhB_{k+1}
                 Edb[c0:c1, k] = Db
             Eub[c0:c1, k - 1] = Db @ Sl[:, k - 1]                      # UhB_k
-        M = Sd[:, mid] - Sl[:, mid - 1] @ Uh[:, mid - 1] - Su[:, mid] @ Eub[c0:c1, mid]
-        Mi = inv(M)
-        Edb[c0:c1, mid] = Mi
-        want = Se_inv.view(Se_inv.shape[0], nb, b, nb, b)[:, mid, :, mid, :]
-        err = ((Mi - want).abs().amax(dim=(1, 2)) / want.abs().amax(dim=(1, 2)).clamp(min=1e-300)).max().item()
-        if not err <= 1e-9:
-            self._edge_twisted = False
-            self._Etw = None
+        top = nrm(Uh.transpose(0, 1)).cummax(0).values                 # top[j] = max_{k<=j} ||UhT_k||   (nb-1, cc)
+        ub = nrm(Eub[c0:c1, cand[0]:].transpose(0, 1))                 # ||UhB_k||, k = cand[0]+1 .. nb-1
+        bot = ub.flip(0).cummax(0).values.flip(0)                      # bot[i] = max_{k >= cand[0]+1+i} ||UhB_k||
+        one = top[-1].clamp(min=1e-300)
+        Sv = Se_inv.view(Se_inv.shape[0], nb, b, nb, b)
+        for i, t in enumerate(cand):
+            Mi = inv(Sd[:, t] - Sl[:, t - 1] @ Uh[:, t - 1] - Su[:, t] @ Eub[c0:c1, t])
+            self._tw_Mi[c0:c1, i] = Mi
+            want = Sv[:, t, :, t, :]
+            err = ((Mi - want).abs().amax(dim=(1, 2)) / want.abs().amax(dim=(1, 2)).clamp(min=1e-300)).max().item()
+            score = (torch.maximum(top[t - 1], bot[t - cand[0]]) / one).max().item()
+            if not err <= 1e-9:
+                score = float("inf")
+            self._tw_ratio[i] = max(self._tw_ratio[i].item(), score)
+
+    def _twisted_edge_select(self, slack=1.25, worst=2.0):
+        """Meeting edge of the two-ended edge sweep, after the last chunk: among the candidates scoring within
+        `slack` of the best, the one closest to the middle (fewest dependent steps); none at all (the one-ended
+        sweep) when the best multiplier ratio exceeds `worst`."""
+        if not self._edge_twisted:
+            return
+        r = self._tw_ratio
+        best = r.min().item()
+        if not best <= worst:
+            self._edge_twisted, self._Etw = False, None
+        else:
+            nb = self.ney + 1
+            ok = [i for i, t in enumerate(self._tw_cand) if r[i].item() <= slack * best]
+            i = min(ok, key=lambda i: (max(self._tw_cand[i], nb - 1 - self._tw_cand[i]), self._tw_cand[i]))
+            self._edge_mid = self._tw_cand[i]
+            self._Etw[1][:, self._edge_mid] = self._tw_Mi[:, i]
+        self._tw_score = best
+        self._tw_Mi = None
+
+    def _edge_twisted_solve(self, Re, cols=slice(None)):
+        """S_e^-1 Re by the two-ended sweep (the torch form of cond_edge_twisted_kernel): chains from edge 0 and
+        from edge N_ey, the meeting block at edge mid, back substitution outwards."""
+        Ed, El, Eu = self._Ed[cols], self._El[cols], self._Eu[cols]
+        Es, Edb, Eub = (t[cols] for t in self._Etw)
+        nex, nb, b = Ed.shape[0], Ed.shape[1], Ed.shape[2]
+        t = self._edge_mid
+        R = Re.view(nex, nb, b, -1)
+        Z = torch.empty_like(R)
+        Z[:, 0] = Ed[:, 0] @ R[:, 0]
+        for k in range(1, t):
+            Z[:, k] = Ed[:, k] @ (R[:, k] - El[:, k - 1] @ Z[:, k - 1])
+        Z[:, nb - 1] = Edb[:, nb - 1] @ R[:, nb - 1]
+        for k in range(nb - 2, t, -1):
+            Z[:, k] = Edb[:, k] @ (R[:, k] - Es[:, k] @ Z[:, k + 1])
+        Z[:, t] = Edb[:, t] @ (R[:, t] - El[:, t - 1] @ Z[:, t - 1] - Es[:, t] @ Z[:, t + 1])
+        for k in range(t - 1, -1, -1):
+            Z[:, k] -= Eu[:, k] @ Z[:, k + 1]
+        for k in range(t + 1, nb):
+            Z[:, k] -= Eub[:, k - 1] @ Z[:, k - 1]
+        return Z.view(Re.shape)
 
     def _blocktri_inverse(self, Sd, Su, Sl, factors=False):
         """Dense inverse of block-tridiagonal matrices (batched over columns): diagonal blocks Sd (cc, nb, b, b),
@@ -1045,7 +1110,10 @@ class VelocityJacobianSolver:
         Rv = Re.view(nex, ney + 1, ne1, k)
         Rv[:, :-1] -= Cn[:, :, :ne1]
         Rv[:, 1:] -= Cn[:, :, ne1:]
-        Ye = self._edge_thomas_solve(Re, cols) if self._edge_thomas else self._Se_inv[cols] @ Re  # (nex, n_e, k)
+        if self._edge_thomas:
+            Ye = (self._edge_twisted_solve if self._edge_twisted else self._edge_thomas_solve)(Re, cols)
+        else:
+            Ye = self._Se_inv[cols] @ Re                                # (nex, n_e, k)
         Yv = Ye.view(nex, ney + 1, ne1, k)
         Yi = Ti - self._Yie[cols] @ torch.cat((Yv[:, :-1], Yv[:, 1:]), dim=2)
         Y = torch.empty_like(R)

@@ -265,8 +265,10 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
             _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
         return x_new, x_old
 
-    # ABI 12: the default sweep is the two-ended one wherever N_ey + 1 >= 3; knob 2 forces the one-ended templated sweep
-    assert ch._edge_twisted == (ney + 1 >= 3)
+    # ABI 12: the default sweep is the two-ended one wherever N_ey + 1 >= 3 and a meeting edge whose multipliers are
+    # within 2x of the one-ended sweep's exists (VelocityJacobianSolver._twisted_edge_factor: P = 16, 2 x 6 elements
+    # meets at edge 4, not 3); knob 2 forces the one-ended templated sweep
+    assert ch._edge_twisted == (ney + 1 >= 3 and ch._tw_score <= 2.0)
     x_tw, x_one = both(False, knob=2)
     e_tw, e_one = _eta(J, x_tw, bb), _eta(J, x_one, bb)
     print(f"two-ended edge sweep {e_tw:.1e}, one-ended {e_one:.1e}")

@@ -190,3 +190,47 @@ def test_twisted_thomas_matches_dense_solve(n, m):
             Uh[L] = Dinv[L] @ Su[L]
     one = fused_thomas_solve(*fused_thomas_operators(Dinv, Sl, Uh), rhs)
     assert (got - one).abs().max().item() <= 1e-12 * want.abs().max().item()
+
+
+@pytest.mark.parametrize("P,nex,ney,Re,mid", [(16, 2, 6, 300.0, 4), (5, 4, 7, 400.0, None), (4, 3, 2, 100.0, 1),
+                                              (12, 2, 12, 1000.0, None)])
+def test_two_ended_edge_sweep(P, nex, ney, Re, mid):
+    """ABI 12's two-ended edge sweep in its torch form (the kernel's arithmetic): solves the Jacobian as the one-ended
+    sweep does.  The meeting edge is chosen by the back-substitution multipliers: at P = 16, 2 x 6 elements,
+    Re = 300 the chain from the bottom meets a nearly singular Schur complement at edge 4 (||Db_4|| ~ 600), so meeting
+    at the middle edge 3 would multiply rounding by ~200x the one-ended sweep's; the selection meets at 4 and the
+    backward error stays the one-ended one's."""
+    ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex + ney)
+    pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
+    r = np.random.default_rng(9)
+    bu, bv = (torch.as_tensor(r.uniform(-1, 1, ns.N)) for _ in range(2))
+    b = np.hstack((bu.numpy(), bv.numpy()))
+    J = ns.Jvelo
+
+    def run(two):
+        ch = VelocityJacobianSolver(P, nex, ney, "cpu")
+        cond = ch.condense_dense(pcs["AII"])
+
+        def fill(blocks, cols):
+            c0, c1 = cols
+            for k in ("D", "aIB", "aBI", "E", "F"):
+                blocks[k].copy_(pcs[k])
+            for k, v in cond.items():
+                blocks[k].copy_(v[c0:c1])
+
+        ch.edge_dense_max, ch.edge_solve, ch.edge_two_ended = 0, "thomas", two
+        ch.factor_condensed(fill, chunk_cols=1)
+        x = np.hstack([t.numpy() for t in ch.solve(bu, bv)])
+        return ch, x, np.abs(J @ x - b).max() / (abs(J).sum(1).max() * np.abs(x).max() + np.abs(b).max())
+
+    one, x1, e1 = run(False)
+    two, x2, e2 = run(True)
+    assert not one._edge_twisted and two._edge_twisted
+    assert two._edge_mid in two._tw_cand and two._tw_score <= 2.0
+    if mid is not None:
+        assert two._edge_mid == mid
+    if (P, ney) == (16, 6):
+        assert two._tw_ratio[two._tw_cand.index(3)] > 100     # the middle edge: the bottom chain's large pivot
+    want = spla.spsolve(J.tocsc(), b)
+    assert np.abs(x2 - want).max() <= 1e-10 * np.abs(want).max()
+    assert e2 <= 4 * e1 + 1e-15

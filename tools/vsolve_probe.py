@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--solves", type=int, default=20)
     ap.add_argument("--out", default="")
     ap.add_argument("--ab-edge", type=int, default=1, help="also time the ABI-9 runtime-width edge sweep")
+    ap.add_argument("--ab-oneended", type=int, default=0,
+                    help="also time the one-ended edge sweep (EDGE_THOMAS = 2) against the two-ended one (ABI 12)")
     ap.add_argument("--ab-back", type=int, default=1,
                     help="also time the ABI-10 back substitution (a second nested solve through Xi)")
     args = ap.parse_args()
@@ -136,6 +138,17 @@ def main():
         _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
         vs.capture()
         out["abi9_edge_sweep_solve_ms_median"] = float(np.median(ts_rt))
+    one_ended = args.ab_oneended and getattr(vs, "_edge_twisted", False)
+    out["edge_twisted"] = bool(getattr(vs, "_edge_twisted", False))
+    if one_ended:
+        from sem_amd import _lib
+        lib = _lib.load()
+        _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 2))
+        vs.capture()
+        ts_oe, xu_oe, xv_oe = timed()
+        _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
+        vs.capture()
+        out["one_ended_edge_solve_ms_median"] = float(np.median(ts_oe))
     if args.ab_back and getattr(vs, "_hipB", None) is not None:
         vs.nested_back = "full"
         vs.capture()
@@ -154,6 +167,9 @@ def main():
     if args.ab_edge and vs._edge_thomas:
         out["abi9_vs_templated_rel_diff"] = float(max((xu - xu_rt).abs().max(), (xv - xv_rt).abs().max())
                                                   / max(xu.abs().max(), xv.abs().max()))
+    if one_ended:
+        out["one_ended_vs_two_ended_rel_diff"] = float(max((xu - xu_oe).abs().max(), (xv - xv_oe).abs().max())
+                                                       / max(xu.abs().max(), xv.abs().max()))
     ju, jv, _ = ns._get_dresiduals(xu, xv, torch.zeros_like(xu))
     out["rel_residual"] = float(max((ju - bu).abs().max(), (jv - bv).abs().max()) / max(bu.abs().max(), bv.abs().max()))
     acc = account(vs)
