@@ -407,6 +407,8 @@ class VelocityJacobianSolver:
         # ABI 12 two-ended edge sweep: "auto" on the GPU (the kernel's form), True also on the CPU (the torch form,
         # for tests), False never
         self.edge_two_ended = "auto"
+        if os.environ.get("SEM_EDGE_TWISTED") == "force":   # tests: block-Thomas edge solves, two-ended, on any device
+            self.edge_dense_max, self.edge_solve, self.edge_two_ended = 0, "thomas", True
         self._edge_thomas = False
         # HIP nested solves: "coupled" (ABI 11: the interface right-hand side from the forward element step's
         # T = Xi b_i and the edge values, sem_nested_iface_rhs; the back substitution T -= Xi A_iB x_B from the
@@ -530,22 +532,25 @@ class VelocityJacobianSolver:
             Et = [torch.empty(sh, **z) for sh in ((nex, ney + 1, ne1, ne1), (nex, ney, ne1, ne1), (nex, ney, ne1, ne1))]
             self._EtT = tuple(Et)                                   # row-major blocks (ABI 10)
             self._Ed, self._El, self._Eu = Et
-        # ABI 12: the two-ended edge sweep (chains from edge 0 and from edge N_ey meeting at edge mid): its bottom
-        # chain's factors beside the one-ended ones (which the dense fallback and the top chain use).  The meeting
-        # edge is chosen from a window around the middle after the last chunk (_twisted_edge_select)
+        # ABI 12: the two-ended edge sweep (chains from edge 0 and from edge N_ey meeting at edge t): its bottom
+        # chain's factors beside the one-ended ones (which the dense fallback and the top chain use), and the meeting
+        # block of three candidate edges t; check_refinement's probe picks the sweep (_select_edge_sweep).  Until
+        # then, and without a probe, the solve runs the one-ended sweep.
         nb = ney + 1
-        self._edge_mid = nb // 2
+        mid = nb // 2
+        env = os.environ.get("SEM_EDGE_TWISTED", "1")   # "0": never; "force": see __init__
         two = self.edge_two_ended
-        self._edge_twisted = (self._edge_thomas and nb >= 3 and os.environ.get("SEM_EDGE_TWISTED", "1") != "0"
-                              and (two is True or (two == "auto" and self.device.type == "cuda")))
+        self._edge_mid, self._edge_twisted, self._tw_done = 0, False, False
+        self._tw_ready = (self._edge_thomas and nb >= 3 and env != "0"
+                          and (two is True or (two == "auto" and self.device.type == "cuda")))
         self._Etw = None
-        if self._edge_twisted:   # Es = A_up (raw), Edb[k > mid] = bottom pivot inverses, Edb[mid] = M^-1, Eub[k-1] = UhB_k
+        if self._tw_ready:   # Es = A_up (raw), Edb[k > t] = bottom pivot inverses, Edb[t] = M_t^-1, Eub[k-1] = UhB_k
             self._Etw = tuple(torch.empty(sh, **z) for sh in ((nex, ney, ne1, ne1), (nex, ney + 1, ne1, ne1),
                                                                (nex, ney, ne1, ne1)))
-            w = max(1, nb // 8)
-            self._tw_cand = list(range(max(1, self._edge_mid - w), min(nb - 2, self._edge_mid + w) + 1))
+            self._tw_cand = list(dict.fromkeys(t for t in (mid, mid + 1, mid - 1) if 1 <= t <= nb - 2))
+            # M_t^-1 of every candidate, and the bottom pivot inverse Db_t that slot t of Edb holds otherwise
             self._tw_Mi = torch.empty((nex, len(self._tw_cand), ne1, ne1), **z)
-            self._tw_ratio = torch.zeros(len(self._tw_cand), dtype=torch.float64)
+            self._tw_Db = torch.empty((nex, len(self._tw_cand), ne1, ne1), **z)
         if self.device.type == "cuda":
             T = [torch.empty(s[:-2] + (s[-1], s[-2]), **z) for s in shapes]
             if self._edge_thomas:
@@ -604,7 +609,6 @@ class VelocityJacobianSolver:
                 S_up[c0:c1] -= C[:, :m, m:]
                 S_lo[c0:c1] -= C[:, m:, :m]
                 del C
-        self._twisted_edge_select()
         self._nested_finish()
         self.W = None
         self.aBI, self.aIB = aBI, aIB
@@ -658,9 +662,9 @@ class VelocityJacobianSolver:
             self._edge_to_dense(c0)
         if self._edge_thomas:
             self._Ed[c0:c1], self._El[c0:c1], self._Eu[c0:c1] = fac[0], Sl, fac[1]
-            if self._edge_twisted:
+            if self._tw_ready:
                 with self._phase("edge_twisted"):
-                    self._twisted_edge_factor(Sd, Su, Sl, fac, Se_inv, c0, c1)
+                    self._twisted_edge_factor(Sd, Su, Sl, fac, c0, c1)
         else:
             self._Se_inv[c0:c1] = Se_inv
         with self._phase("coupling_pieces"):
@@ -709,65 +713,71 @@ class VelocityJacobianSolver:
             inv = self._group_perm()
             return Cg[:, inv][:, :, inv]
 
-    def _twisted_edge_factor(self, Sd, Su, Sl, fac, Se_inv, c0, c1):
+    def _twisted_edge_factor(self, Sd, Su, Sl, fac, c0, c1):
         """Bottom chain and candidate meeting blocks of the two-ended edge sweep (ABI 12), for columns [c0, c1):
           bottom  Db_{nb-1} = Sd_{nb-1}^-1,  UhB_k = Db_k Sl_{k-1},  Db_k = (Sd_k - Su_k UhB_{k+1})^-1   (k > t)
           middle  M_t^-1 = (Sd_t - Sl_{t-1} UhT_{t-1} - Su_t UhB_{t+1})^-1
-        (the top chain's Dinv_k, UhT_k = Dinv_k Su_k for k < t are the one-ended factors), for every candidate
-        meeting edge t of the window.  Block elimination without pivoting across blocks amplifies rounding by its
-        multipliers: a chain that runs into a nearly singular Schur complement (P = 16, 2 x 6 elements, Re = 300:
-        ||Db_4|| = 600 from the bottom, <= 10 from the top) gives a two-ended sweep 50x the one-ended backward
-        error if it meets there.  So each candidate is scored, per column, by its largest back-substitution
-        multiplier max(max_{k<t} ||UhT_k||, max_{k>t} ||UhB_k||) over the one-ended sweep's max_k ||UhT_k||, and
-        _twisted_edge_select keeps the best (the max over columns).  M_t^-1 is the (t, t) block of S^-1, so the
-        checked dense inverse pins it too: a candidate that misses it by 1e-9 is excluded."""
+        (the top chain's Dinv_k, UhT_k = Dinv_k Su_k for k < t are the one-ended factors), for each candidate
+        meeting edge t (the middle edge and its two neighbours)."""
         Dinv, Uh = fac
-        nb, b = Sd.shape[1], Sd.shape[2]
-        cand = self._tw_cand
+        nb = Sd.shape[1]
+        lo = min(self._tw_cand)
         inv = lambda A: torch.linalg.inv_ex(A)[0]  # noqa: E731
-        nrm = lambda A: A.abs().sum(-1).amax(-1)   # noqa: E731  infinity norm per column
         Es, Edb, Eub = self._Etw
         Es[c0:c1] = Su
         Db = inv(Sd[:, nb - 1])
         Edb[c0:c1, nb - 1] = Db
-        for k in range(nb - 1, cand[0], -1):
+        for k in range(nb - 1, lo, -1):
             if k < nb - 1:
                 Db = inv(Sd[:, k] - Su[:, k] @ Eub[c0:c1, k])          # Eub[:, k] holds UhB_{k+1}
                 Edb[c0:c1, k] = Db
             Eub[c0:c1, k - 1] = Db @ Sl[:, k - 1]                      # UhB_k
-        top = nrm(Uh.transpose(0, 1)).cummax(0).values                 # top[j] = max_{k<=j} ||UhT_k||   (nb-1, cc)
-        ub = nrm(Eub[c0:c1, cand[0]:].transpose(0, 1))                 # ||UhB_k||, k = cand[0]+1 .. nb-1
-        bot = ub.flip(0).cummax(0).values.flip(0)                      # bot[i] = max_{k >= cand[0]+1+i} ||UhB_k||
-        one = top[-1].clamp(min=1e-300)
-        Sv = Se_inv.view(Se_inv.shape[0], nb, b, nb, b)
-        for i, t in enumerate(cand):
-            Mi = inv(Sd[:, t] - Sl[:, t - 1] @ Uh[:, t - 1] - Su[:, t] @ Eub[c0:c1, t])
-            self._tw_Mi[c0:c1, i] = Mi
-            want = Sv[:, t, :, t, :]
-            err = ((Mi - want).abs().amax(dim=(1, 2)) / want.abs().amax(dim=(1, 2)).clamp(min=1e-300)).max().item()
-            score = (torch.maximum(top[t - 1], bot[t - cand[0]]) / one).max().item()
-            if not err <= 1e-9:
-                score = float("inf")
-            self._tw_ratio[i] = max(self._tw_ratio[i].item(), score)
+        for i, t in enumerate(self._tw_cand):
+            self._tw_Mi[c0:c1, i] = inv(Sd[:, t] - Sl[:, t - 1] @ Uh[:, t - 1] - Su[:, t] @ Eub[c0:c1, t])
+            self._tw_Db[c0:c1, i] = Edb[c0:c1, t]                      # (unset for t = lo: no chain meets below it)
 
-    def _twisted_edge_select(self, slack=1.25, worst=2.0):
-        """Meeting edge of the two-ended edge sweep, after the last chunk: among the candidates scoring within
-        `slack` of the best, the one closest to the middle (fewest dependent steps); none at all (the one-ended
-        sweep) when the best multiplier ratio exceeds `worst`."""
-        if not self._edge_twisted:
-            return
-        r = self._tw_ratio
-        best = r.min().item()
-        if not best <= worst:
-            self._edge_twisted, self._Etw = False, None
+    def _set_edge_sweep(self, t):
+        """Edge sweep of the following solves: two-ended meeting at candidate edge t, or one-ended (t None)."""
+        Edb = self._Etw[1]
+        for i, c in enumerate(self._tw_cand):
+            Edb[:, c] = self._tw_Db[:, i]
+        if t is not None:
+            Edb[:, t] = self._tw_Mi[:, self._tw_cand.index(t)]
+        self._edge_twisted, self._edge_mid = t is not None, (0 if t is None else t)
+        self._nd = None                                                 # the descriptor carries the sweep
+
+    def _select_edge_sweep(self, probe, slack=2.0):
+        """Block elimination without inter-block pivoting multiplies rounding by its multipliers, and the two chains
+        of a two-ended sweep meet different Schur complements: at P = 16, 2 x 6 elements, Re = 300 the chain from the
+        bottom meets a nearly singular one at edge 4 (||Db_4|| = 600; <= 10 from the top), and meeting at the middle
+        edge 3 gave 180x the one-ended sweep's backward error.  Neither the multipliers nor a random edge-level probe
+        predict the solve's error reliably (the edge right-hand sides of a solve are structured), so the candidates are
+        judged by the solver's own probe: the first of (middle, middle + 1, middle - 1) whose probe backward error is
+        within `slack` of the one-ended sweep's is kept, else the one-ended sweep.  Returns the kept sweep's eta.
+        Every rank of a partition takes the same decisions (the probe's norms are reduced over the ranks)."""
+        if getattr(self, "_tw_done", False):   # judged at an earlier probe: keep that sweep
+            return probe()
+        self._tw_done = True
+        ready = getattr(self, "_tw_ready", False) and self._Etw is not None
+        ready = self._amax(torch.tensor([0.0 if ready else 1.0], dtype=torch.float64, device=self.device)) == 0.0
+        if ready:
+            self._set_edge_sweep(None)
+        eta1 = probe()
+        self._tw_eta = {"one-ended": eta1}
+        best = None
+        if ready:
+            for t in self._tw_cand:
+                self._set_edge_sweep(t)
+                eta = probe()
+                self._tw_eta[t] = eta
+                if eta <= slack * eta1 + 1e-16:
+                    best = (t, eta)
+                    break
+            self._set_edge_sweep(None if best is None else best[0])
+            self._tw_Mi = self._tw_Db = None
         else:
-            nb = self.ney + 1
-            ok = [i for i, t in enumerate(self._tw_cand) if r[i].item() <= slack * best]
-            i = min(ok, key=lambda i: (max(self._tw_cand[i], nb - 1 - self._tw_cand[i]), self._tw_cand[i]))
-            self._edge_mid = self._tw_cand[i]
-            self._Etw[1][:, self._edge_mid] = self._tw_Mi[:, i]
-        self._tw_score = best
-        self._tw_Mi = None
+            self._edge_twisted, self._edge_mid = False, 0
+        return eta1 if best is None else best[1]
 
     def _edge_twisted_solve(self, Re, cols=slice(None)):
         """S_e^-1 Re by the two-ended sweep (the torch form of cond_edge_twisted_kernel): chains from edge 0 and
@@ -855,7 +865,7 @@ class VelocityJacobianSolver:
         if self._hipT is not None:
             self._hipT = self._hipT[:3] + (SeT,)
         self._edge_thomas = False
-        self._edge_twisted = False
+        self._edge_twisted = self._tw_ready = False
         self._Ed = self._El = self._Eu = self._EtT = self._Etw = None
 
     @staticmethod
@@ -1142,9 +1152,10 @@ class VelocityJacobianSolver:
             nex, ney, P, m = self.nex, self.ney, self.P, self.m
             ni, ne1 = self._pi.shape[1], self._ne1
             z = dict(dtype=torch.float64, device=self.device)
-            self._work = (torch.empty(nex * ney * ni, **z), torch.empty(nex * ney * 2 * ne1, **z),
-                          torch.empty(nex * (ney + 1) * ne1, **z), torch.empty((nex, self.nI), **z),
-                          torch.empty((nex + 1, m), **z), torch.empty(nex * 2 * m, **z))
+            if getattr(self, "_work", None) is None:   # kept when only the descriptor is rebuilt (_set_edge_sweep)
+                self._work = (torch.empty(nex * ney * ni, **z), torch.empty(nex * ney * 2 * ne1, **z),
+                              torch.empty(nex * (ney + 1) * ne1, **z), torch.empty((nex, self.nI), **z),
+                              torch.empty((nex + 1, m), **z), torch.empty(nex * 2 * m, **z))
             T, Cw, Ye, _, _, Pw = self._work
             p = lambda t: t.data_ptr()  # noqa: E731
             XiT, AeiT, YieT, SeT = self._hipT
@@ -1249,10 +1260,13 @@ class VelocityJacobianSolver:
         sgn = torch.sign(torch.rand((NXg, self.m), dtype=torch.float64, device=self.device, generator=g)
                          - 0.5)[l0:l1].contiguous()
         self.refine = False
-        x = self._solve_lines(b)
-        r = b - self._apply(x)
-        nJ = self._amax(self._apply(sgn))
-        eta = self._amax(r) / (nJ * self._amax(x) + self._amax(b))
+        nJ, nb = self._amax(self._apply(sgn)), self._amax(b)
+
+        def probe():
+            x = self._solve_lines(b)
+            return self._amax(b - self._apply(x)) / (nJ * self._amax(x) + nb)
+
+        eta = self._select_edge_sweep(probe)
         self.refine_eta = eta
         self.refine = eta > tau
         return eta

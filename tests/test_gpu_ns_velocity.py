@@ -255,29 +255,39 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
     J = ref.Jvelo.tocsr()
     lib = _lib.load()
 
-    def both(refine, knob=1):
+    def both(refine, knob=1, first=0):
         ch.refine = refine
-        x_new = torch.cat(ch.solve(bu, bv))
-        _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, knob))
+        out = []
         try:
-            x_old = torch.cat(ch.solve(bu, bv))
+            for k in (first, knob):
+                _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, k))
+                out.append(torch.cat(ch.solve(bu, bv)))
         finally:
             _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
-        return x_new, x_old
+        return out
 
-    # ABI 12: the default sweep is the two-ended one wherever N_ey + 1 >= 3 and a meeting edge whose multipliers are
-    # within 2x of the one-ended sweep's exists (VelocityJacobianSolver._twisted_edge_factor: P = 16, 2 x 6 elements
-    # meets at edge 4, not 3); knob 2 forces the one-ended templated sweep
-    assert ch._edge_twisted == (ney + 1 >= 3 and ch._tw_score <= 2.0)
+    # ABI 12: the factor's probe (check_refinement) picks the edge sweep: two-ended, meeting at the first of the middle
+    # edge and its neighbours whose probe backward error is within 2x of the one-ended sweep's, else one-ended
+    # (VelocityJacobianSolver._select_edge_sweep: P = 16, 2 x 6 elements meets at edge 4, not 3); knob 2 forces the
+    # one-ended templated sweep
+    assert not ch._edge_twisted
+    eta0 = ch.check_refinement()
+    print(f"edge sweep probe {ch._tw_eta}: meeting edge {ch._edge_mid}")
+    if ney + 1 >= 3:
+        assert ch._edge_twisted == any(k != "one-ended" and v <= 2 * ch._tw_eta["one-ended"] + 1e-16
+                                       for k, v in ch._tw_eta.items())
     x_tw, x_one = both(False, knob=2)
     e_tw, e_one = _eta(J, x_tw, bb), _eta(J, x_one, bb)
     print(f"two-ended edge sweep {e_tw:.1e}, one-ended {e_one:.1e}")
-    assert max(e_tw, e_one) <= 4 * min(e_tw, e_one) + 1e-15
-    x_new, x_old = both(False)
+    assert e_tw <= 4 * e_one + 1e-15
+    # the one-ended templated sweep (knob 2) against the ABI-9 sweep (knob 1): one factor, one elimination order
+    x_new, x_old = both(False, first=2)
     e_new, e_old, e_lu = _eta(J, x_new, bb), _eta(J, x_old, bb), _eta(J, spla.spsolve(J.tocsc(), bb), bb)
-    f_new, f_old = both(True)
+    f_new, f_old = both(True, first=2)
     g_new, g_old = _eta(J, f_new, bb), _eta(J, f_old, bb)
-    eta = ch.check_refinement()
+    mid = ch._edge_mid
+    eta = ch.check_refinement()                                    # a second probe keeps the chosen sweep
+    assert ch._edge_mid == mid
     x_s = torch.cat(ch.solve(bu, bv))
     e_s = _eta(J, x_s, bb)
     print(f"velocity pair, block width {ch._ne1}: backward error templated {e_new:.1e} / ABI-9 {e_old:.1e} / SuperLU "
