@@ -276,10 +276,22 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
     if ney + 1 >= 3:
         assert ch._edge_twisted == any(k != "one-ended" and v <= 2 * ch._tw_eta["one-ended"] + 1e-16
                                        for k, v in ch._tw_eta.items())
-    x_tw, x_one = both(False, knob=2)
-    e_tw, e_one = _eta(J, x_tw, bb), _eta(J, x_one, bb)
-    print(f"two-ended edge sweep {e_tw:.1e}, one-ended {e_one:.1e}")
-    assert e_tw <= 4 * e_one + 1e-15
+    # two elimination orders: on one right-hand side their backward errors differ by 0.3x - 7x either way (CPU, 20
+    # draws per mesh), so the bar is over 16 draws: the worst two-ended error within 2x of the worst one-ended one
+    e_tw, e_one = [], []
+    for sd in range(16):
+        rr = np.random.default_rng(100 + sd)
+        cu, cv = ns._dev(rr.uniform(-1, 1, ns.N)), ns._dev(rr.uniform(-1, 1, ns.N))
+        cb = np.hstack((cu.cpu().numpy(), cv.cpu().numpy()))
+        try:
+            for k, acc in ((0, e_tw), (2, e_one)):
+                _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, k))
+                acc.append(_eta(J, torch.cat(ch.solve(cu, cv)), cb))
+        finally:
+            _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
+    print(f"over 16 right-hand sides: two-ended edge sweep worst {max(e_tw):.1e} median {np.median(e_tw):.1e}, "
+          f"one-ended worst {max(e_one):.1e} median {np.median(e_one):.1e}")
+    assert max(e_tw) <= 2 * max(e_one) + 1e-15
     # the one-ended templated sweep (knob 2) against the ABI-9 sweep (knob 1): one factor, one elimination order
     x_new, x_old = both(False, first=2)
     e_new, e_old, e_lu = _eta(J, x_new, bb), _eta(J, x_old, bb), _eta(J, spla.spsolve(J.tocsc(), bb), bb)
