@@ -267,15 +267,16 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
         return out
 
     # ABI 12: the factor's probe (check_refinement) picks the edge sweep: two-ended, meeting at the first of the middle
-    # edge and its neighbours whose probe backward error is within 2x of the one-ended sweep's, else one-ended
+    # edge and its neighbours whose worst backward error over 4 probes is within 1.5x of the one-ended sweep's worst
+    # (or below 1e-15), else one-ended
     # (VelocityJacobianSolver._select_edge_sweep: P = 16, 2 x 6 elements meets at edge 4, not 3); knob 2 forces the
     # one-ended templated sweep
     assert not ch._edge_twisted
     eta0 = ch.check_refinement()
     print(f"edge sweep probe {ch._tw_eta}: meeting edge {ch._edge_mid}")
     if ney + 1 >= 3:
-        assert ch._edge_twisted == any(k != "one-ended" and v <= 2 * ch._tw_eta["one-ended"] + 1e-16
-                                       for k, v in ch._tw_eta.items())
+        bar = max(1.5 * ch._tw_eta["one-ended"], 1e-15)
+        assert ch._edge_twisted == any(k != "one-ended" and v <= bar for k, v in ch._tw_eta.items())
     # two elimination orders: on one right-hand side their backward errors differ by 0.3x - 7x either way (CPU, 20
     # draws per mesh), so the bar is over 16 draws: the worst two-ended error within 2x of the worst one-ended one
     e_tw, e_one = [], []

@@ -197,7 +197,8 @@ def test_twisted_thomas_matches_dense_solve(n, m):
 def test_two_ended_edge_sweep(P, nex, ney, Re, mid):
     """ABI 12's two-ended edge sweep in its torch form (the kernel's arithmetic) solves the Jacobian as the one-ended
     sweep does.  The sweep is chosen by the solver's backward-error probe (check_refinement): the first of the
-    middle edge and its two neighbours whose probe error is within 2x of the one-ended sweep's.  At P = 16,
+    middle edge and its two neighbours whose worst error over 4 probe right-hand sides is within 1.5x of the
+    one-ended sweep's worst (or below 1e-15).  At P = 16,
     2 x 6 elements, Re = 300 the chain from the bottom meets a nearly singular Schur complement at edge 4
     (||Db_4|| ~ 600): meeting at the middle edge 3 multiplies the error ~100x, so the probe moves the meeting to
     edge 4.  (12, 2, 5): edge 2 has the smallest multipliers yet 10x the error on solve right-hand sides -- the
@@ -238,7 +239,7 @@ def test_two_ended_edge_sweep(P, nex, ney, Re, mid):
     one, x1, e1 = run(False)
     two, x2, e2 = run(True)
     print(f"probe eta {two._tw_eta}, meeting edge {two._edge_mid}; solve eta {e2:.1e} (one-ended {e1:.1e})")
-    assert not one._edge_twisted and two._tw_eta["one-ended"] == one.refine_eta
+    assert not one._edge_twisted and two._tw_eta["one-ended"] >= one.refine_eta   # worst of 4 probes vs probe 0
     assert two._edge_twisted == (mid is not None or two._edge_mid != 0)
     if mid is not None:
         assert two._edge_twisted and two._edge_mid == mid
