@@ -764,7 +764,9 @@ class VelocityJacobianSolver:
         ready = self._amax(torch.tensor([0.0 if ready else 1.0], dtype=torch.float64, device=self.device)) == 0.0
         if not ready:
             self._edge_twisted, self._edge_mid = False, 0
-            return probe(0)
+            eta = probe(0)
+            self._tw_eta = {"one-ended": eta}
+            return eta
         self._set_edge_sweep(None)
         eta1 = max(probe(k) for k in range(nprobe))
         bar = max(slack * eta1, floor)
