@@ -226,7 +226,11 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
     # solve 0.744 -> 0.715 s, profiles/r04/schur_ab/schurpipe_*.jsonl): a pinned host buffer for each step's
     # coefficients and norms, and the event that marks its copy
     pipe = None
-    if isinstance(sweeps, _DeviceSweeps) and os.environ.get("SEM_GMRES_PIPELINE", "1") != "0":
+    # a host-staged reduce (gloo rehearsals of the partitioned solve) synchronises the host with the device at every
+    # collective, the matvec's own included: nothing can run behind the host's wait, so no speculation there
+    bdev = getattr(inner, "bdev", None) if red is not None else None
+    staged = bdev is not None and bdev.type != dev.type
+    if isinstance(sweeps, _DeviceSweeps) and not staged and os.environ.get("SEM_GMRES_PIPELINE", "1") != "0":
         pipe = (torch.empty(restart + 3, dtype=torch.float64, pin_memory=True), torch.cuda.Event())
     r = b - matvec(x) if x0 is not None else b.clone()
     matvecs += x0 is not None
