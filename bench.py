@@ -110,9 +110,22 @@ def time_steps(step, steps, warmup, dev, use_graph, dist=None):
     if use_graph and steps > 0:
         batch = min(steps, GRAPH_BATCH)
         reps, rem = divmod(steps, batch)
-        plan.append((capture(step, batch, dev), reps))
-        if rem:
-            plan.append((capture(step, rem, dev), 1))
+        try:
+            plan.append((capture(step, batch, dev), reps))
+            if rem:
+                plan.append((capture(step, rem, dev), 1))
+        except RuntimeError as exc:   # capture refused (a collective the library cannot capture): eager steps
+            if dist is None:
+                raise
+            print(f"[bench] hipGraph capture failed ({exc}); timing eagerly", file=sys.stderr, flush=True)
+            plan = []
+        if dist is not None:
+            # a capture executes no collective, so a rank whose capture failed would otherwise run a different
+            # number of collectives than the others: every rank replays only if every rank captured
+            ok = torch.tensor([1.0 if plan else 0.0], device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() < 1.0:
+                plan = []
         for g, _ in plan:
             g.replay()
         torch.cuda.synchronize(dev)
@@ -134,7 +147,7 @@ def time_steps(step, steps, warmup, dev, use_graph, dist=None):
     wall = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-    return e0.elapsed_time(e1) / 1e3, wall
+    return e0.elapsed_time(e1) / 1e3, bool(plan)
 
 
 def graph_kernel_us(fn, dev, launches=1000, trials=5):
@@ -274,15 +287,8 @@ def main():
         # too -- RCCL collectives are stream-capturable -- so the per-step host cost (four launches and a
         # collective call from Python) leaves the timed loop; gloo collectives are host-side and cannot be.
         use_graph = bool(args.graph) and (world == 1 or args.dist_backend == "nccl")
-        try:
-            secs, _ = time_steps(step, steps, warmup, dev, use_graph=use_graph, dist=dist)
-        except RuntimeError as exc:  # capture refused: time the same steps eagerly
-            if not use_graph or world == 1:
-                raise
-            print(f"[bench] rank {rank}: hipGraph capture of the exchange failed ({exc}); timing eagerly",
-                  file=sys.stderr, flush=True)
-            use_graph = False
-            secs, _ = time_steps(step, steps, 0, dev, use_graph=False, dist=dist)
+        # a refused capture (every rank agrees first) times the same steps eagerly
+        secs, use_graph = time_steps(step, steps, warmup, dev, use_graph=use_graph, dist=dist)
         if dist is not None:
             t = torch.tensor([secs], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
