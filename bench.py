@@ -53,6 +53,8 @@ def parse():
                     help="capture steps in hipGraphs (N=1, and N>1 over RCCL: apply + pack + all-reduce + unpack)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--hbm-ne", type=int, default=1024, help="HBM-regime mesh size (0 = skip)")
+    ap.add_argument("--weak-ne", type=int, default=512,
+                    help="HBM-regime weak scaling: (weak_ne N) x weak_ne elements over N GPUs, SURVEY 8(d) (0 = skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the measured path); gloo only to rehearse N > 1 on a 1-GPU box")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
@@ -393,9 +395,10 @@ def main():
                                "kernel_us": kb * 1e6}
         del Tb, ub, vb, yb
 
-    if world > 1 and args.extra_steps > 0:
+    if args.extra_steps > 0:
         # the other meshes per rank count (north_star: absolute numbers at 1, 2, 4 and 8 GPUs): the HBM-regime mesh
-        # split into N strips, and the weak-scaling mesh (or, with --scaling weak, the strong one)
+        # split into N strips, the weak-scaling mesh (or, with --scaling weak, the strong one), and the HBM-regime
+        # weak-scaling mesh of SURVEY 8(d) (weak_ne^2 elements per GPU; at N = 1 its baseline)
         def extra(nex_, ney_, d_, seed, latency):
             es, eg, em, _, (eb_, ee_) = strip_case(nex_, ney_, d_, args.extra_steps, min(args.warmup, 10), seed)
             Ng = (nex_ * P + 1) * (ney_ * P + 1)
@@ -405,14 +408,18 @@ def main():
                  "regime": regime(em.n_local, latency),
                  "rank0_bw_GBs": 32.0 * em.n_local / (es / args.extra_steps) / 1e9}
             return r
-        if args.hbm_ne > 0:
+        if world > 1 and args.hbm_ne > 0:
             out["strong_hbm"] = dict(extra(args.hbm_ne, args.hbm_ne, 1.0 / args.hbm_ne, 4048 + rank, False),
                                      scaling="strong")
             torch.cuda.empty_cache()
-        if args.scaling == "strong":
+        if world > 1 and args.scaling == "strong":
             out["weak"] = dict(extra(ne * world, ne, d, 2024 + rank, True), scaling="weak")
-        else:
+        elif world > 1:
             out["strong"] = dict(extra(ne, ne, d, 2024 + rank, True), scaling="strong")
+        if args.weak_ne > 0:
+            wn = args.weak_ne
+            out["weak_hbm"] = dict(extra(wn * world, wn, 1.0 / wn, 6072 + rank, False), scaling="weak")
+            torch.cuda.empty_cache()
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(P, ne, Pe, args.cpu_seconds)
