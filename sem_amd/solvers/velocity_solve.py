@@ -405,10 +405,12 @@ class VelocityJacobianSolver:
         # inverse -- 1.5 MB instead of 64 MB per cfg5 column); "dense" keeps the dense inverse
         self.edge_solve = "auto"
         # ABI 12 two-ended edge sweep: "auto" on the GPU (the kernel's form), True also on the CPU (the torch form,
-        # for tests), False never
-        self.edge_two_ended = "auto"
-        if os.environ.get("SEM_EDGE_TWISTED") == "force":   # tests: block-Thomas edge solves, two-ended, on any device
-            self.edge_dense_max, self.edge_solve, self.edge_two_ended = 0, "thomas", True
+        # for tests), False never.  Opt-in (SEM_EDGE_TWISTED=1): with it on, cfg5's coupled JNK solve at Ra = 1e4
+        # diverged where the one-ended sweep reproduces round 4's converged run
+        env = os.environ.get("SEM_EDGE_TWISTED", "0")
+        self.edge_two_ended = {"1": "auto", "force": True}.get(env, False)
+        if env == "force":   # tests: block-Thomas edge solves, two-ended, on any device
+            self.edge_dense_max, self.edge_solve = 0, "thomas"
         self._edge_thomas = False
         # HIP nested solves: "coupled" (ABI 11: the interface right-hand side from the forward element step's
         # T = Xi b_i and the edge values, sem_nested_iface_rhs; the back substitution T -= Xi A_iB x_B from the
@@ -538,10 +540,9 @@ class VelocityJacobianSolver:
         # then, and without a probe, the solve runs the one-ended sweep.
         nb = ney + 1
         mid = nb // 2
-        env = os.environ.get("SEM_EDGE_TWISTED", "1")   # "0": never; "force": see __init__
         two = self.edge_two_ended
         self._edge_mid, self._edge_twisted, self._tw_done = 0, False, False
-        self._tw_ready = (self._edge_thomas and nb >= 3 and env != "0"
+        self._tw_ready = (self._edge_thomas and nb >= 3
                           and (two is True or (two == "auto" and self.device.type == "cuda")))
         self._Etw = None
         if self._tw_ready:   # Es = A_up (raw), Edb[k > t] = bottom pivot inverses, Edb[t] = M_t^-1, Eub[k-1] = UhB_k

@@ -245,7 +245,7 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
     kw = dict(juu=ns._Jac_u_u._coeffs()[4], juv=ns._Jac_u_v._coeffs()[4], jvu=ns._Jac_v_u._coeffs()[4],
               jvv=ns._Jac_v_v._coeffs()[4], dir_mask=ns._dir.mask, dir_sides=ns._dir.sides, **ns._sys_kw(ns._Sys))
     ch = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
-    ch.edge_dense_max, ch.edge_solve = 0, "auto"
+    ch.edge_dense_max, ch.edge_solve, ch.edge_two_ended = 0, "auto", "auto"   # the two-ended sweep is opt-in
     ch.factor_mesh(ns._mesh, budget_bytes=1, **kw)
     assert ch._edge_thomas
     ch.set_operator(ns._velocity_apply_lines)

@@ -79,9 +79,9 @@ for s in "$@"; do
           --out "$O/sweepab_${f}_$rep.json"
       done; done ;;
     edgetw)     # two-ended edge sweep (ABI 12) against the one-ended one (EDGE_THOMAS = 2): cfg2-size and 128^2 P=12
-      TAILN=2 step edgetw_48 300 python tools/vsolve_probe.py --ne 48 --P 8 --ab-edge 0 --ab-back 0 --ab-oneended 1 \
+      SEM_EDGE_TWISTED=1 TAILN=2 step edgetw_48 300 python tools/vsolve_probe.py --ne 48 --P 8 --ab-edge 0 --ab-back 0 --ab-oneended 1 \
         --solves 50 --out "$O/edgetw_48.json"
-      TAILN=2 step edgetw_128 600 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 --ab-oneended 1 \
+      SEM_EDGE_TWISTED=1 TAILN=2 step edgetw_128 600 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 --ab-oneended 1 \
         --out "$O/edgetw_128.json" ;;
     vsolveab)   # interface-sweep GEMV A/B: the library's streaming GEMV (default) against rocBLAS, one process each
       SEM_SWEEP_GEMV=torch TAILN=2 step vsolve_rocblas 600 python tools/vsolve_probe.py --ab-edge 0 --out "$O/vsolve_rocblas.json"
