@@ -1254,8 +1254,9 @@ class VelocityJacobianSolver:
         """Measure the factor's normwise backward error eta = ||J x - b|| / (||J|| ||x|| + ||b||) (max norms) on a
         seeded probe, ||J|| estimated from below by ||J s|| for a random sign vector s (so eta is over-estimated),
         and turn on one refinement step per solve when eta > tau (SEM_REFINE_ETA, default 1e-13; 0 refines
-        always, inf never).  Every part of a partitioned solve takes the same decision (reduced norms).
-        Returns eta."""
+        always, inf never).  With the opt-in two-ended edge sweep factored, the same probe first picks the edge
+        sweep (_select_edge_sweep) and eta is the kept sweep's.  Every part of a partitioned solve takes the same
+        decisions (reduced norms).  Returns eta."""
         if self._apply is None:
             raise RuntimeError("set_operator() first")
         if tau is None:
