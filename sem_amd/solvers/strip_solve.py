@@ -26,7 +26,7 @@ import os
 import torch
 
 from ..tracing import phase
-from .velocity_solve import (VelocityJacobianSolver, _gemv, fused_thomas_operators, fused_thomas_solve,
+from .velocity_solve import (VelocityJacobianSolver, _gemv, _gemv2, fused_thomas_operators, fused_thomas_solve,
                              pivot_inverse, twisted_thomas_operators, twisted_thomas_solve, twisted_thomas_solve_mat)
 
 
@@ -208,7 +208,8 @@ class StripLineSolver(VelocityJacobianSolver):
         with phase("strip.interior_sweep"):
             if self._T is not None:
                 y = self._thomas(g[1:n])
-                h = torch.stack((g[0] - self._S_up0 @ y[0], g[n] - self._S_lon @ y[-1]))
+                h = torch.stack((g[0], g[n]))   # the boundary lines' right-hand sides: one dual streaming GEMV
+                _gemv2((self._S_up0, y[0], h[0]), (self._S_lon, y[-1], h[1]), alpha=-1.0, beta=1.0)
             else:
                 y, h = None, torch.stack((g[0], g[1]))
         with phase("strip.allgather"):
