@@ -137,7 +137,20 @@ struct RowGemv2Args {
   int nb0;
 };
 
-template <bool VEC>
+// A's rows are read once per call: NT = true loads them non-temporally (gfx950 `nt`), so they do not evict x
+// (read by every workgroup) from L2 (SEM_GEMV_CPOL=1; results bitwise identical: only the load policy differs).
+using dvec2 = double __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ double2 load_a2(const double* p) {
+  if constexpr (NT) {
+    const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p));
+    return make_double2(v.x, v.y);
+  } else {
+    return *reinterpret_cast<const double2*>(p);
+  }
+}
+
+template <bool VEC, bool NT = false>
 __global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemv2Args g) {
   __shared__ double part[4][kRowsWG];
   const bool second = static_cast<int>(blockIdx.x) >= g.nb0;
@@ -161,7 +174,7 @@ __global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemv2Args g) {
       for (int t = 0; t < kSweepUnroll; ++t) {
         xv[t] = *reinterpret_cast<const double2*>(a.x + 2 * (u + 64 * t));
 #pragma unroll
-        for (int i = 0; i < kRowsWG; ++i) av[t][i] = *reinterpret_cast<const double2*>(rows[i] + 2 * (u + 64 * t));
+        for (int i = 0; i < kRowsWG; ++i) av[t][i] = load_a2<NT>(rows[i] + 2 * (u + 64 * t));
       }
 #pragma unroll
       for (int t = 0; t < kSweepUnroll; ++t)
@@ -175,7 +188,7 @@ __global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemv2Args g) {
       const double2 xv = *reinterpret_cast<const double2*>(a.x + 2 * u);
 #pragma unroll
       for (int i = 0; i < kRowsWG; ++i) {
-        const double2 av = *reinterpret_cast<const double2*>(rows[i] + 2 * u);
+        const double2 av = load_a2<NT>(rows[i] + 2 * u);
         acc[i][0] = fma(av.x, xv.x, acc[i][0]);
         acc[i][1] = fma(av.y, xv.y, acc[i][1]);
       }
@@ -233,7 +246,10 @@ int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, cons
   sem::RowGemv2Args g{{sem::RowGemvArgs{A, x, y, lda, alpha, beta, M, K}, sem::RowGemvArgs{}}, nb};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (sem::row_vec(g.p[0]))
-    hipLaunchKernelGGL(sem::row_gemv_kernel<true>, dim3(nb), dim3(256), 0, s, g);
+    if (sem::tune(SEM_TUNE_GEMV_CPOL) == 1)
+      hipLaunchKernelGGL((sem::row_gemv_kernel<true, true>), dim3(nb), dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((sem::row_gemv_kernel<true, false>), dim3(nb), dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL(sem::row_gemv_kernel<false>, dim3(nb), dim3(256), 0, s, g);
   hipError_t e = hipGetLastError();
@@ -251,7 +267,10 @@ int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, i
                        sem::RowGemvArgs{A1, x1, y1, lda1, alpha, beta, M, K1}}, nb};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (sem::row_vec(g.p[0]) && sem::row_vec(g.p[1]))
-    hipLaunchKernelGGL(sem::row_gemv_kernel<true>, dim3(2 * nb), dim3(256), 0, s, g);
+    if (sem::tune(SEM_TUNE_GEMV_CPOL) == 1)
+      hipLaunchKernelGGL((sem::row_gemv_kernel<true, true>), dim3(2 * nb), dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((sem::row_gemv_kernel<true, false>), dim3(2 * nb), dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL(sem::row_gemv_kernel<false>, dim3(2 * nb), dim3(256), 0, s, g);
   hipError_t e = hipGetLastError();

@@ -48,6 +48,7 @@ Tuning& tuning() {
     r.v[SEM_TUNE_NS_APPLY] = env_int("SEM_NS_APPLY");
     r.v[SEM_TUNE_EDGE_THOMAS] = env_int("SEM_EDGE_THOMAS");
     r.v[SEM_TUNE_BAND_ORDER] = env_int("SEM_BAND_ORDER");
+    r.v[SEM_TUNE_GEMV_CPOL] = env_int("SEM_GEMV_CPOL");
     return r;
   }();
   return t;
