@@ -140,8 +140,8 @@ enum sem_tune {
                              * the two-ended factors are given (ABI 12; A/B only; agree to rounding)     */
   SEM_TUNE_BAND_ORDER = 8,  /* SEM_BAND_ORDER: 1 = the band kernel's full tiles before its ghost tiles in
                              * every XCD's share (measured slower; A/B only; bitwise identical) */
-  SEM_TUNE_GEMV_CPOL = 9,   /* SEM_GEMV_CPOL: 1 = sem_gemv_rows / rows2 load the operator non-temporally
-                               (bitwise-identical results)                                              */
+  SEM_TUNE_GEMV_CPOL = 9,   /* SEM_GEMV_CPOL: 2 = sem_gemv_rows / rows2 load the operator with plain loads
+                               instead of the default non-temporal ones (bitwise-identical results)       */
   SEM_TUNE_COUNT = 10
 };
 

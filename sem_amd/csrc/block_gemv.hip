@@ -137,8 +137,10 @@ struct RowGemv2Args {
   int nb0;
 };
 
-// A's rows are read once per call: NT = true loads them non-temporally (gfx950 `nt`), so they do not evict x
-// (read by every workgroup) from L2 (SEM_GEMV_CPOL=1; results bitwise identical: only the load policy differs).
+// A's rows are read once per call: NT = true (the default; SEM_GEMV_CPOL=2 for plain loads) loads them
+// non-temporally (gfx950 `nt`), so they do not evict x (read by every workgroup) from L2.  Results are bitwise
+// identical; alternated A/B at cfg5 (profiles/r05/gemv_cpol/): the velocity solve 8.045 -> 8.018 ms, the strip
+// solve's reduced-rows GEMV 5.6 -> 5.75 TB/s, its back-substitution GEMV 6.0 -> 6.25 TB/s.
 using dvec2 = double __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ double2 load_a2(const double* p) {
@@ -246,7 +248,7 @@ int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, cons
   sem::RowGemv2Args g{{sem::RowGemvArgs{A, x, y, lda, alpha, beta, M, K}, sem::RowGemvArgs{}}, nb};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (sem::row_vec(g.p[0]))
-    if (sem::tune(SEM_TUNE_GEMV_CPOL) == 1)
+    if (sem::tune(SEM_TUNE_GEMV_CPOL) != 2)
       hipLaunchKernelGGL((sem::row_gemv_kernel<true, true>), dim3(nb), dim3(256), 0, s, g);
     else
       hipLaunchKernelGGL((sem::row_gemv_kernel<true, false>), dim3(nb), dim3(256), 0, s, g);
@@ -267,7 +269,7 @@ int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, i
                        sem::RowGemvArgs{A1, x1, y1, lda1, alpha, beta, M, K1}}, nb};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (sem::row_vec(g.p[0]) && sem::row_vec(g.p[1]))
-    if (sem::tune(SEM_TUNE_GEMV_CPOL) == 1)
+    if (sem::tune(SEM_TUNE_GEMV_CPOL) != 2)
       hipLaunchKernelGGL((sem::row_gemv_kernel<true, true>), dim3(2 * nb), dim3(256), 0, s, g);
     else
       hipLaunchKernelGGL((sem::row_gemv_kernel<true, false>), dim3(2 * nb), dim3(256), 0, s, g);

@@ -83,9 +83,9 @@ for s in "$@"; do
         --solves 50 --out "$O/edgetw_48.json"
       SEM_EDGE_TWISTED=1 TAILN=2 step edgetw_128 600 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 --ab-oneended 1 \
         --out "$O/edgetw_128.json" ;;
-    gemvcpol)   # streaming GEMV operator loads plain (0) against non-temporal (1): shapes alone, then the cfg5 velocity
-                # solve, one process per setting, alternated (bitwise-identical results; only the load policy differs)
-      for rep in 1 2; do for c in 0 1; do
+    gemvcpol)   # streaming GEMV operator loads plain (2) against non-temporal (0, the default): shapes alone, then the
+                # cfg5 velocity solve, one process per setting, alternated (bitwise-identical results)
+      for rep in 1 2; do for c in 2 0; do
         SEM_GEMV_CPOL=$c TAILN=3 step gemvcpol_${c}_$rep 300 python tools/gemv_shapes.py
         SEM_GEMV_CPOL=$c TAILN=1 step vsolvecpol_${c}_$rep 300 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 \
           --solves 30 --out "$O/vsolvecpol_${c}_$rep.json"
