@@ -142,7 +142,11 @@ enum sem_tune {
                              * every XCD's share (measured slower; A/B only; bitwise identical) */
   SEM_TUNE_GEMV_CPOL = 9,   /* SEM_GEMV_CPOL: 2 = sem_gemv_rows / rows2 load the operator with plain loads
                                instead of the default non-temporal ones (bitwise-identical results)       */
-  SEM_TUNE_COUNT = 10
+  SEM_TUNE_BASIS_CPOL = 10,  /* SEM_BASIS_CPOL: 1 = sem_basis_dot2 / update read the basis non-temporally
+                                (bitwise-identical results)                                             */
+  SEM_TUNE_COND_CPOL = 11,   /* SEM_COND_CPOL: 1 = the nested solve's element step reads its factors
+                                non-temporally (bitwise-identical results)                              */
+  SEM_TUNE_COUNT = 12
 };
 
 /* ---- library ------------------------------------------------------------ */

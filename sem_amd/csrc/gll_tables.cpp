@@ -49,6 +49,8 @@ Tuning& tuning() {
     r.v[SEM_TUNE_EDGE_THOMAS] = env_int("SEM_EDGE_THOMAS");
     r.v[SEM_TUNE_BAND_ORDER] = env_int("SEM_BAND_ORDER");
     r.v[SEM_TUNE_GEMV_CPOL] = env_int("SEM_GEMV_CPOL");
+    r.v[SEM_TUNE_BASIS_CPOL] = env_int("SEM_BASIS_CPOL");
+    r.v[SEM_TUNE_COND_CPOL] = env_int("SEM_COND_CPOL");
     return r;
   }();
   return t;

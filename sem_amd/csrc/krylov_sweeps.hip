@@ -25,6 +25,16 @@ namespace sem {
 // then sums the chunks in order: results are bitwise reproducible.
 constexpr int kDotThreads = 256, kDotPer = 8, kDotCols = kDotThreads * kDotPer, kDotRows = 16;
 
+// Basis loads: NT = true reads V non-temporally (gfx950 `nt`; SEM_BASIS_CPOL=1); bitwise-identical results.
+template <bool NT>
+__device__ __forceinline__ double ldv_(const double* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(kDotThreads) void basis_dot2_kernel(const double* __restrict__ V, int64_t ldv, int k,
                                                                  int64_t n, int nchunks, const double* __restrict__ a,
                                                                  const double* __restrict__ b,
@@ -46,7 +56,7 @@ __global__ __launch_bounds__(kDotThreads) void basis_dot2_kernel(const double* _
 #pragma unroll
     for (int q = 0; q < kDotPer; ++q) {
       const int64_t i = lo + t + q * kDotThreads;
-      vv[q] = i < n ? row[i] : 0.0;
+      vv[q] = i < n ? ldv_<NT>(row + i) : 0.0;
     }
     double pa0 = 0.0, pb0 = 0.0, pa1 = 0.0, pb1 = 0.0;
 #pragma unroll
@@ -88,6 +98,7 @@ __global__ void basis_dot2_finish(const double* __restrict__ work, int k, int nc
 // w[i] -= sum_j c[j] V[j][i]: one thread per column, rows streamed in order (coalesced per row);
 // the coefficients are staged through LDS in blocks.
 constexpr int kUpdThreads = 256, kUpdStage = 512;
+template <bool NT>
 __global__ __launch_bounds__(kUpdThreads) void basis_update_kernel(const double* __restrict__ V, int64_t ldv, int k,
                                                                    int64_t n, const double* __restrict__ c,
                                                                    double* __restrict__ w) {
@@ -103,10 +114,10 @@ __global__ __launch_bounds__(kUpdThreads) void basis_update_kernel(const double*
       const double* p = V + static_cast<int64_t>(j0) * ldv + i;
       int j = 0;
       for (; j + 1 < m; j += 2) {  // two independent chains for load-level parallelism
-        s0 = fma(cs[j], p[static_cast<int64_t>(j) * ldv], s0);
-        s1 = fma(cs[j + 1], p[static_cast<int64_t>(j + 1) * ldv], s1);
+        s0 = fma(cs[j], ldv_<NT>(p + static_cast<int64_t>(j) * ldv), s0);
+        s1 = fma(cs[j + 1], ldv_<NT>(p + static_cast<int64_t>(j + 1) * ldv), s1);
       }
-      if (j < m) s0 = fma(cs[j], p[static_cast<int64_t>(j) * ldv], s0);
+      if (j < m) s0 = fma(cs[j], ldv_<NT>(p + static_cast<int64_t>(j) * ldv), s0);
     }
   }
   if (i < n) w[i] = w[i] - (s0 + s1);
@@ -136,8 +147,12 @@ int sem_basis_dot2(const double* V, int64_t ldv, int k, int64_t n, const double*
   if (groups > 65535) return sem::set_error(SEM_EINVAL, "basis_dot2: too many basis vectors");
   auto s = reinterpret_cast<hipStream_t>(stream);
   const int nch = dot2_chunks(n);
-  hipLaunchKernelGGL(sem::basis_dot2_kernel, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n, nch, a, b,
-                     work);
+  if (sem::tune(SEM_TUNE_BASIS_CPOL) == 1)
+    hipLaunchKernelGGL(sem::basis_dot2_kernel<true>, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n,
+                       nch, a, b, work);
+  else
+    hipLaunchKernelGGL(sem::basis_dot2_kernel<false>, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n,
+                       nch, a, b, work);
   hipLaunchKernelGGL(sem::basis_dot2_finish, dim3((2 * k + 255) / 256), dim3(256), 0, s, work, k, nch, out);
   return sem::hip_check_k(hipGetLastError(), "basis_dot2 launch");
 }
@@ -148,8 +163,13 @@ int sem_basis_update(const double* V, int64_t ldv, int k, int64_t n, const doubl
   if (!V || !c || !w) return sem::set_error(SEM_EINVAL, "basis_update: null argument");
   const int64_t blocks = (n + sem::kUpdThreads - 1) / sem::kUpdThreads;
   if (blocks > 0x7fffffffLL) return sem::set_error(SEM_EINVAL, "basis_update: vector too long");
-  hipLaunchKernelGGL(sem::basis_update_kernel, dim3(static_cast<unsigned>(blocks)), dim3(sem::kUpdThreads), 0,
-                     reinterpret_cast<hipStream_t>(stream), V, ldv, k, n, c, w);
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  if (sem::tune(SEM_TUNE_BASIS_CPOL) == 1)
+    hipLaunchKernelGGL(sem::basis_update_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(sem::kUpdThreads), 0,
+                       s, V, ldv, k, n, c, w);
+  else
+    hipLaunchKernelGGL(sem::basis_update_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(sem::kUpdThreads), 0,
+                       s, V, ldv, k, n, c, w);
   return sem::hip_check_k(hipGetLastError(), "basis_update launch");
 }
 

@@ -71,19 +71,29 @@ __device__ __forceinline__ double rhs(const CondArgs& a, int e, int64_t o) {
 // wavefront multiple) over the column split t / RP, and the splits' partial sums meet in `part`
 // (LDS) in split order.  More rows: each thread owns rows t, t + 256, ... over all columns.
 // out(row, value) stores.
-template <typename Out>
+// NT: the factor block is read once per solve -- load it non-temporally (gfx950 `nt`; SEM_COND_CPOL=1).  The
+// load policy only: results are bitwise identical.
+template <bool NT>
+__device__ __forceinline__ double ldm(const double* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+template <bool NT = false, typename Out>
 __device__ __forceinline__ void colmajor_gemv(const double* __restrict__ M, int rows, int cols, const double* x,
                                               double* part, Out out) {
   auto dot = [&](int i, int cb, int ce) {
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
     int j = cb;
     for (; j + 3 < ce; j += 4) {
-      acc0 = fma(M[static_cast<int64_t>(j) * rows + i], x[j], acc0);
-      acc1 = fma(M[static_cast<int64_t>(j + 1) * rows + i], x[j + 1], acc1);
-      acc2 = fma(M[static_cast<int64_t>(j + 2) * rows + i], x[j + 2], acc2);
-      acc3 = fma(M[static_cast<int64_t>(j + 3) * rows + i], x[j + 3], acc3);
+      acc0 = fma(ldm<NT>(M + static_cast<int64_t>(j) * rows + i), x[j], acc0);
+      acc1 = fma(ldm<NT>(M + static_cast<int64_t>(j + 1) * rows + i), x[j + 1], acc1);
+      acc2 = fma(ldm<NT>(M + static_cast<int64_t>(j + 2) * rows + i), x[j + 2], acc2);
+      acc3 = fma(ldm<NT>(M + static_cast<int64_t>(j + 3) * rows + i), x[j + 3], acc3);
     }
-    for (; j < ce; ++j) acc0 = fma(M[static_cast<int64_t>(j) * rows + i], x[j], acc0);
+    for (; j < ce; ++j) acc0 = fma(ldm<NT>(M + static_cast<int64_t>(j) * rows + i), x[j], acc0);
     return (acc0 + acc1) + (acc2 + acc3);
   };
   const int t = threadIdx.x;
@@ -112,6 +122,7 @@ __device__ __forceinline__ void colmajor_gemv(const double* __restrict__ M, int 
 __host__ __device__ constexpr int part_size() { return kCondThreads; }
 
 // K1: T = Xi r_i, C = Aei T for element (e, n) = (blockIdx.x / ney, blockIdx.x % ney).
+template <bool NT>
 __global__ __launch_bounds__(kCondThreads) void cond_fwd_kernel(const CondArgs a) {
   extern __shared__ double lds[];
   double* part = lds;                     // part_size()
@@ -123,14 +134,21 @@ __global__ __launch_bounds__(kCondThreads) void cond_fwd_kernel(const CondArgs a
   __syncthreads();
   const double* Xi = a.Xi + static_cast<int64_t>(el) * a.ni * a.ni;
   double* T = a.T + static_cast<int64_t>(el) * a.ni;
-  colmajor_gemv(Xi, a.ni, a.ni, x, part, [&](int r, double v) {
+  colmajor_gemv<NT>(Xi, a.ni, a.ni, x, part, [&](int r, double v) {
     T[r] = v;
     t[r] = v;
   });
   __syncthreads();
   const double* Aei = a.Aei + static_cast<int64_t>(el) * 2 * a.ne1 * a.ni;
   double* C = a.C + static_cast<int64_t>(el) * 2 * a.ne1;
-  colmajor_gemv(Aei, 2 * a.ne1, a.ni, t, part, [&](int r, double v) { C[r] = v; });
+  colmajor_gemv<NT>(Aei, 2 * a.ne1, a.ni, t, part, [&](int r, double v) { C[r] = v; });
+}
+
+static void launch_cond_fwd(const CondArgs& a, unsigned elems, size_t lds, hipStream_t s) {
+  if (tune(SEM_TUNE_COND_CPOL) == 1)
+    hipLaunchKernelGGL(cond_fwd_kernel<true>, dim3(elems), dim3(kCondThreads), lds, s, a);
+  else
+    hipLaunchKernelGGL(cond_fwd_kernel<false>, dim3(elems), dim3(kCondThreads), lds, s, a);
 }
 
 // K1 of the back substitution (ABI 11): r_i = b_i - A_iB x_B, so Xi r_i = Xi b_i - XiB x_B|n and
@@ -837,8 +855,7 @@ int sem_nested_solve(const sem_nested_desc* d, const double* R, int64_t ld_r, co
   if (int st = sem::nested_args(d, R, ld_r, aIB, xB, Y, ld_y, a)) return st;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t part = sem::part_size() * sizeof(double);
-  hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(static_cast<unsigned>(a.nex) * a.ney), dim3(sem::kCondThreads),
-                     part + 2 * a.ni * sizeof(double), s, a);
+  sem::launch_cond_fwd(a, static_cast<unsigned>(a.nex) * a.ney, part + 2 * a.ni * sizeof(double), s);
   if (int st = sem::launch_check("nested_solve fwd")) return st;
   return sem::nested_edge_back(a, s);
 }
@@ -867,7 +884,7 @@ int sem_nested_iface_rhs(const sem_nested_desc* d, const double* R, int64_t ld_r
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned elems = static_cast<unsigned>(a.nex) * a.ney;
   const size_t part = sem::part_size() * sizeof(double);
-  hipLaunchKernelGGL(sem::cond_fwd_kernel, dim3(elems), dim3(sem::kCondThreads), part + 2 * a.ni * sizeof(double), s, a);
+  sem::launch_cond_fwd(a, elems, part + 2 * a.ni * sizeof(double), s);
   if (int st = sem::launch_check("nested_iface_rhs fwd")) return st;
   if (int st = sem::nested_edge(a, s)) return st;
   hipLaunchKernelGGL(sem::cond_iface_part_kernel, dim3(elems), dim3(sem::kCondThreads),

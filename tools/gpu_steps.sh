@@ -90,6 +90,16 @@ for s in "$@"; do
         SEM_GEMV_CPOL=$c TAILN=1 step vsolvecpol_${c}_$rep 300 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 \
           --solves 30 --out "$O/vsolvecpol_${c}_$rep.json"
       done; done ;;
+    cpolab)     # non-temporal loads (1) against plain (0), one process per setting, alternated (bitwise-identical results):
+                # the Krylov basis passes (sweep_bench at the 64^2 CD size and at cfg4's Ra = 1e6 block solve) and the
+                # nested solve's element step (the cfg5 velocity solve)
+      for rep in 1 2; do for c in 0 1; do
+        SEM_BASIS_CPOL=$c TAILN=4 step sweepcpol_${c}_$rep 300 python tools/sweep_bench.py
+        SEM_BASIS_CPOL=$c TAILN=2 step schurcpol_${c}_$rep 300 python tools/schur_ab.py --precond mass \
+          --out "$O/schurcpol_${c}_$rep.jsonl"
+        SEM_COND_CPOL=$c TAILN=1 step condcpol_${c}_$rep 300 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 \
+          --solves 30 --out "$O/condcpol_${c}_$rep.json"
+      done; done ;;
     vsolveab)   # interface-sweep GEMV A/B: the library's streaming GEMV (default) against rocBLAS, one process each
       SEM_SWEEP_GEMV=torch TAILN=2 step vsolve_rocblas 600 python tools/vsolve_probe.py --ab-edge 0 --out "$O/vsolve_rocblas.json"
       TAILN=2 step vsolve_hip 600 python tools/vsolve_probe.py --ab-edge 1 --out "$O/vsolve_hip.json" ;;
