@@ -142,10 +142,11 @@ enum sem_tune {
                              * every XCD's share (measured slower; A/B only; bitwise identical) */
   SEM_TUNE_GEMV_CPOL = 9,   /* SEM_GEMV_CPOL: 2 = sem_gemv_rows / rows2 load the operator with plain loads
                                instead of the default non-temporal ones (bitwise-identical results)       */
-  SEM_TUNE_BASIS_CPOL = 10,  /* SEM_BASIS_CPOL: 1 = sem_basis_dot2 / update read the basis non-temporally
-                                (bitwise-identical results)                                             */
+  SEM_TUNE_BASIS_CPOL = 10,  /* SEM_BASIS_CPOL: basis loads of sem_basis_dot2 / update -- 0: non-temporal in
+                                dot2, plain in update (measured best); 1: non-temporal in both; 2: plain in
+                                both (bitwise-identical results)                                        */
   SEM_TUNE_COND_CPOL = 11,   /* SEM_COND_CPOL: 1 = the nested solve's element step reads its factors
-                                non-temporally (bitwise-identical results)                              */
+                                non-temporally (bitwise-identical; measured 0.5 % slower at cfg5)       */
   SEM_TUNE_COUNT = 12
 };
 

@@ -25,7 +25,9 @@ namespace sem {
 // then sums the chunks in order: results are bitwise reproducible.
 constexpr int kDotThreads = 256, kDotPer = 8, kDotCols = kDotThreads * kDotPer, kDotRows = 16;
 
-// Basis loads: NT = true reads V non-temporally (gfx950 `nt`; SEM_BASIS_CPOL=1); bitwise-identical results.
+// Basis loads: NT = true reads V non-temporally (gfx950 `nt`); bitwise-identical results.  Alternated A/B
+// (k = 1000, n = 263169; profiles/r05/basis_cpol/): dot2 427 -> 399 us with nt, update 399 -> 415 us -- so the
+// default is nt for dot2 and plain loads for update; SEM_BASIS_CPOL=1: nt for both, 2: plain for both.
 template <bool NT>
 __device__ __forceinline__ double ldv_(const double* p) {
   if constexpr (NT)
@@ -147,7 +149,7 @@ int sem_basis_dot2(const double* V, int64_t ldv, int k, int64_t n, const double*
   if (groups > 65535) return sem::set_error(SEM_EINVAL, "basis_dot2: too many basis vectors");
   auto s = reinterpret_cast<hipStream_t>(stream);
   const int nch = dot2_chunks(n);
-  if (sem::tune(SEM_TUNE_BASIS_CPOL) == 1)
+  if (sem::tune(SEM_TUNE_BASIS_CPOL) != 2)
     hipLaunchKernelGGL(sem::basis_dot2_kernel<true>, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n,
                        nch, a, b, work);
   else

@@ -72,7 +72,8 @@ __device__ __forceinline__ double rhs(const CondArgs& a, int e, int64_t o) {
 // (LDS) in split order.  More rows: each thread owns rows t, t + 256, ... over all columns.
 // out(row, value) stores.
 // NT: the factor block is read once per solve -- load it non-temporally (gfx950 `nt`; SEM_COND_CPOL=1).  The
-// load policy only: results are bitwise identical.
+// load policy only: results are bitwise identical.  Measured slower (cfg5 velocity solve 8.00 -> 8.04 ms,
+// alternated, profiles/r05/basis_cpol/condcpol_*.json), so off by default.
 template <bool NT>
 __device__ __forceinline__ double ldm(const double* p) {
   if constexpr (NT)
