@@ -16,7 +16,7 @@ ABI_VERSION = 12
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 (TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE, TUNE_NS_APPLY,
  TUNE_EDGE_THOMAS, TUNE_BAND_ORDER, TUNE_GEMV_CPOL, TUNE_BASIS_CPOL,
- TUNE_COND_CPOL) = range(12)
+ TUNE_COND_CPOL, TUNE_GEMV_SHAPE) = range(13)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
 DIR_NONE, DIR_IDENTITY, DIR_REPLACE = 0, 1, 2
 ALGO_AUTO, ALGO_VALU, ALGO_MFMA, ALGO_COLUMN, ALGO_BAND = 0, 1, 2, 3, 4

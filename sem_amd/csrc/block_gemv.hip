@@ -152,8 +152,12 @@ __device__ __forceinline__ double2 load_a2(const double* p) {
   }
 }
 
-template <bool VEC, bool NT = false>
+// R rows per workgroup, U iterations of loads in flight: neither changes the order in which a row's products are
+// summed (each lane walks its columns in increasing order; the four waves' sums meet in wave order), so every
+// (R, U) gives bitwise-identical results (SEM_GEMV_SHAPE selects one for A/B runs).
+template <bool VEC, bool NT = false, int R = kRowsWG, int U = kSweepUnroll>
 __global__ __launch_bounds__(256) void row_gemv_kernel(const RowGemv2Args g) {
+  constexpr int kRowsWG = R, kSweepUnroll = U;
   __shared__ double part[4][kRowsWG];
   const bool second = static_cast<int>(blockIdx.x) >= g.nb0;
   const RowGemvArgs a = second ? g.p[1] : g.p[0];
@@ -235,6 +239,33 @@ static bool row_vec(const RowGemvArgs& a) {
          (a.lda % 2) == 0 && (a.K % 2) == 0;
 }
 
+template <int R, int U>
+static void launch_row_gemv_ru(RowGemv2Args& g, int M, int parts, hipStream_t s) {
+  const int nb = (M + R - 1) / R;
+  g.nb0 = nb;
+  if (tune(SEM_TUNE_GEMV_CPOL) != 2)
+    hipLaunchKernelGGL((row_gemv_kernel<true, true, R, U>), dim3(parts * nb), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((row_gemv_kernel<true, false, R, U>), dim3(parts * nb), dim3(256), 0, s, g);
+}
+
+// parts = 1 (sem_gemv_rows) or 2 (sem_gemv_rows2: blocks [0, nb) the first GEMV, the rest the second)
+static void launch_row_gemv(RowGemv2Args& g, int M, int parts, bool vec, hipStream_t s) {
+  if (!vec) {
+    const int nb = (M + kRowsWG - 1) / kRowsWG;
+    g.nb0 = nb;
+    hipLaunchKernelGGL((row_gemv_kernel<false>), dim3(parts * nb), dim3(256), 0, s, g);
+    return;
+  }
+  switch (tune(SEM_TUNE_GEMV_SHAPE)) {
+    case 1: launch_row_gemv_ru<8, 4>(g, M, parts, s); break;
+    case 2: launch_row_gemv_ru<4, 8>(g, M, parts, s); break;
+    case 3: launch_row_gemv_ru<2, 8>(g, M, parts, s); break;
+    case 4: launch_row_gemv_ru<8, 2>(g, M, parts, s); break;
+    default: launch_row_gemv_ru<kRowsWG, kSweepUnroll>(g, M, parts, s); break;
+  }
+}
+
 }  // namespace sem
 
 extern "C" {
@@ -244,16 +275,8 @@ int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, cons
   if (M < 0 || K < 0 || lda < K) return sem::set_error(SEM_EINVAL, "gemv_rows: bad sizes");
   if (M == 0) return SEM_OK;
   if (!A || !x || !y) return sem::set_error(SEM_EINVAL, "gemv_rows: null argument");
-  const int nb = (M + sem::kRowsWG - 1) / sem::kRowsWG;
-  sem::RowGemv2Args g{{sem::RowGemvArgs{A, x, y, lda, alpha, beta, M, K}, sem::RowGemvArgs{}}, nb};
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (sem::row_vec(g.p[0]))
-    if (sem::tune(SEM_TUNE_GEMV_CPOL) != 2)
-      hipLaunchKernelGGL((sem::row_gemv_kernel<true, true>), dim3(nb), dim3(256), 0, s, g);
-    else
-      hipLaunchKernelGGL((sem::row_gemv_kernel<true, false>), dim3(nb), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL(sem::row_gemv_kernel<false>, dim3(nb), dim3(256), 0, s, g);
+  sem::RowGemv2Args g{{sem::RowGemvArgs{A, x, y, lda, alpha, beta, M, K}, sem::RowGemvArgs{}}, 0};
+  sem::launch_row_gemv(g, M, 1, sem::row_vec(g.p[0]), reinterpret_cast<hipStream_t>(stream));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("gemv_rows launch: ") + hipGetErrorString(e));
   return SEM_OK;
@@ -264,17 +287,9 @@ int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, i
   if (M < 0 || K0 < 0 || K1 < 0 || lda0 < K0 || lda1 < K1) return sem::set_error(SEM_EINVAL, "gemv_rows2: bad sizes");
   if (M == 0) return SEM_OK;
   if (!A0 || !x0 || !y0 || !A1 || !x1 || !y1) return sem::set_error(SEM_EINVAL, "gemv_rows2: null argument");
-  const int nb = (M + sem::kRowsWG - 1) / sem::kRowsWG;
   sem::RowGemv2Args g{{sem::RowGemvArgs{A0, x0, y0, lda0, alpha, beta, M, K0},
-                       sem::RowGemvArgs{A1, x1, y1, lda1, alpha, beta, M, K1}}, nb};
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (sem::row_vec(g.p[0]) && sem::row_vec(g.p[1]))
-    if (sem::tune(SEM_TUNE_GEMV_CPOL) != 2)
-      hipLaunchKernelGGL((sem::row_gemv_kernel<true, true>), dim3(2 * nb), dim3(256), 0, s, g);
-    else
-      hipLaunchKernelGGL((sem::row_gemv_kernel<true, false>), dim3(2 * nb), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL(sem::row_gemv_kernel<false>, dim3(2 * nb), dim3(256), 0, s, g);
+                       sem::RowGemvArgs{A1, x1, y1, lda1, alpha, beta, M, K1}}, 0};
+  sem::launch_row_gemv(g, M, 2, sem::row_vec(g.p[0]) && sem::row_vec(g.p[1]), reinterpret_cast<hipStream_t>(stream));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("gemv_rows2 launch: ") + hipGetErrorString(e));
   return SEM_OK;

@@ -51,6 +51,7 @@ Tuning& tuning() {
     r.v[SEM_TUNE_GEMV_CPOL] = env_int("SEM_GEMV_CPOL");
     r.v[SEM_TUNE_BASIS_CPOL] = env_int("SEM_BASIS_CPOL");
     r.v[SEM_TUNE_COND_CPOL] = env_int("SEM_COND_CPOL");
+    r.v[SEM_TUNE_GEMV_SHAPE] = env_int("SEM_GEMV_SHAPE");
     return r;
   }();
   return t;

@@ -380,6 +380,45 @@ def test_gemv_rows_matches_torch(gpu, M, K, lda, alpha, beta):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("M,K", [(3074, 6148), (1537, 3074), (13, 130), (7, 2), (770, 1540)])
+def test_gemv_rows_shapes_and_load_policy_bitwise(gpu, M, K):
+    """Every rows-per-workgroup x loads-in-flight variant of sem_gemv_rows (SEM_TUNE_GEMV_SHAPE 0-4) and both load
+    policies (non-temporal default, SEM_TUNE_GEMV_CPOL = 2 plain) give the same bits: the variants change neither
+    a lane's column order nor the order in which the waves' sums meet; likewise sem_gemv_rows2."""
+    import ctypes as C
+    from sem_amd import _lib
+    lib = _lib.load()
+    dev = torch.device("cuda")
+    r = np.random.default_rng(3 * M + K)
+    A = torch.as_tensor(r.uniform(-1, 1, (M, K)), device=dev)
+    B = torch.as_tensor(r.uniform(-1, 1, (M, K)), device=dev)
+    x = torch.as_tensor(r.uniform(-1, 1, K), device=dev)
+    y0 = torch.as_tensor(r.uniform(-1, 1, M), device=dev)
+    P_ = C.c_void_p
+    st = P_(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    try:
+        for shape in range(5):
+            for cpol in (0, 2):
+                _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_SHAPE, shape))
+                _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_CPOL, cpol))
+                y, z = y0.clone(), y0.clone()
+                _lib.check(lib.sem_gemv_rows(M, K, -1.0, P_(A.data_ptr()), K, P_(x.data_ptr()), 1.0, P_(y.data_ptr()),
+                                             st))
+                _lib.check(lib.sem_gemv_rows2(M, -1.0, 1.0, K, P_(A.data_ptr()), K, P_(x.data_ptr()),
+                                              P_(z.data_ptr()), K, P_(B.data_ptr()), K, P_(x.data_ptr()),
+                                              P_(y0.clone().data_ptr()), st))
+                outs.append((y, z))
+    finally:
+        _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_SHAPE, 0))
+        _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_CPOL, 0))
+    for y, z in outs[1:]:
+        assert torch.equal(y, outs[0][0]) and torch.equal(z, outs[0][1])
+    assert torch.equal(outs[0][0], outs[0][1])          # the dual launch's first half is the single call's bits
+    want = y0 - A @ x
+    assert (outs[0][0] - want).abs().max().item() <= 1e-13 * max(1.0, want.abs().max().item()) * np.sqrt(K)
+
+
 @pytest.mark.parametrize("M,K0,K1,odd", [(3074, 6148, 6148, False), (3074, 3074, 3074, False), (1537, 3074, 1537, True),
                                          (5, 7, 12, False), (13, 130, 4, True), (1, 1, 1, False)])
 def test_gemv_rows2_matches_two_gemvs(gpu, M, K0, K1, odd):

@@ -90,6 +90,14 @@ for s in "$@"; do
         SEM_GEMV_CPOL=$c TAILN=1 step vsolvecpol_${c}_$rep 300 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 \
           --solves 30 --out "$O/vsolvecpol_${c}_$rep.json"
       done; done ;;
+    gemvshape)  # streaming GEMV rows per workgroup x loads in flight (SEM_GEMV_SHAPE 0-4; bitwise-identical results):
+                # the bitwise test, then the operator shapes and the cfg5 velocity solve, one process per variant
+      step gemvshapetest 300 $PYT tests/test_gpu_ns_velocity.py -k "shapes_and_load_policy"
+      for rep in 1 2; do for v in 0 1 2 3 4; do
+        SEM_GEMV_SHAPE=$v TAILN=3 step gemvshape_${v}_$rep 300 python tools/gemv_shapes.py
+        SEM_GEMV_SHAPE=$v TAILN=1 step vsolveshape_${v}_$rep 300 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 \
+          --solves 30 --out "$O/vsolveshape_${v}_$rep.json"
+      done; done ;;
     cpolab)     # non-temporal loads (1) against plain (0), one process per setting, alternated (bitwise-identical results):
                 # the Krylov basis passes (sweep_bench at the 64^2 CD size and at cfg4's Ra = 1e6 block solve) and the
                 # nested solve's element step (the cfg5 velocity solve)
