@@ -147,8 +147,9 @@ enum sem_tune {
                                 both (bitwise-identical results)                                        */
   SEM_TUNE_COND_CPOL = 11,   /* SEM_COND_CPOL: 1 = the nested solve's element step reads its factors
                                 non-temporally (bitwise-identical; measured 0.5 % slower at cfg5)       */
-  SEM_TUNE_GEMV_SHAPE = 12,  /* SEM_GEMV_SHAPE: sem_gemv_rows rows per workgroup x loads in flight -- 0: 4 x 4,
-                                1: 8 x 4, 2: 4 x 8, 3: 2 x 8, 4: 8 x 2 (bitwise-identical results)      */
+  SEM_TUNE_GEMV_SHAPE = 12,  /* SEM_GEMV_SHAPE: sem_gemv_rows rows per workgroup x loads in flight -- 0: 2 x 8
+                                (default), 1: 8 x 4, 2: 4 x 8, 3: 4 x 4 (round 4), 4: 8 x 2, 5: 1 x 8,
+                                6: 2 x 16, 7: 1 x 16 (bitwise-identical results)                       */
   SEM_TUNE_COUNT = 13
 };
 

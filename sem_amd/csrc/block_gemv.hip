@@ -257,12 +257,17 @@ static void launch_row_gemv(RowGemv2Args& g, int M, int parts, bool vec, hipStre
     hipLaunchKernelGGL((row_gemv_kernel<false>), dim3(parts * nb), dim3(256), 0, s, g);
     return;
   }
+  // default 2 x 8 (alternated A/B, profiles/r05/gemv_shape/: cfg5 velocity solve 7.90 -> 7.82 ms against round 4's
+  // 4 x 4, the sweep's m x 2m GEMV 5.05 -> 5.3 TB/s)
   switch (tune(SEM_TUNE_GEMV_SHAPE)) {
     case 1: launch_row_gemv_ru<8, 4>(g, M, parts, s); break;
     case 2: launch_row_gemv_ru<4, 8>(g, M, parts, s); break;
-    case 3: launch_row_gemv_ru<2, 8>(g, M, parts, s); break;
+    case 3: launch_row_gemv_ru<4, 4>(g, M, parts, s); break;
     case 4: launch_row_gemv_ru<8, 2>(g, M, parts, s); break;
-    default: launch_row_gemv_ru<kRowsWG, kSweepUnroll>(g, M, parts, s); break;
+    case 5: launch_row_gemv_ru<1, 8>(g, M, parts, s); break;
+    case 6: launch_row_gemv_ru<2, 16>(g, M, parts, s); break;
+    case 7: launch_row_gemv_ru<1, 16>(g, M, parts, s); break;
+    default: launch_row_gemv_ru<2, 8>(g, M, parts, s); break;
   }
 }
 
