@@ -92,7 +92,7 @@ for s in "$@"; do
       done; done ;;
     gemvshape)  # streaming GEMV rows per workgroup x loads in flight (SEM_GEMV_SHAPE 0-4; bitwise-identical results):
                 # the bitwise test, then the operator shapes and the cfg5 velocity solve, one process per variant
-      step gemvshapetest 300 $PYT tests/test_gpu_ns_velocity.py -k "shapes_and_load_policy"
+      SEM_TEST_GEMV_SHAPES=8 step gemvshapetest 300 $PYT tests/test_gpu_ns_velocity.py -k "shapes_and_load_policy"
       for rep in 1 2; do for v in ${GEMV_SHAPES:-0 3 5 6 7}; do
         SEM_GEMV_SHAPE=$v TAILN=3 step gemvshape_${v}_$rep 300 python tools/gemv_shapes.py
         SEM_GEMV_SHAPE=$v TAILN=1 step vsolveshape_${v}_$rep 300 python tools/vsolve_probe.py --ab-edge 0 --ab-back 0 \
