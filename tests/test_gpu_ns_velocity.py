@@ -2,6 +2,7 @@
 NavierStokes_Solver.py:176-192): the HIP block assembly (sem_velocity_blocks) against the pieces of
 the oracle's assembled Jacobian, and the condensed device solve against SciPy's sparse solve."""
 import os
+
 import numpy as np
 import pytest
 import scipy.sparse.linalg as spla
