@@ -400,7 +400,7 @@ def test_gemv_rows_shapes_and_load_policy_bitwise(gpu, M, K):
     st = P_(torch.cuda.current_stream().cuda_stream)
     outs = []
     try:
-        for shape in range(int(os.environ.get("SEM_TEST_GEMV_SHAPES", "5"))):   # 5-7: 1 x 8, 2 x 16, 1 x 16
+        for shape in range(int(os.environ.get("SEM_TEST_GEMV_SHAPES", "8"))):
             for cpol in (0, 2):
                 _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_SHAPE, shape))
                 _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_CPOL, cpol))
