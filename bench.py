@@ -175,6 +175,31 @@ def graph_kernel_us(fn, dev, launches=1000, trials=5):
     return float(np.median(ts))
 
 
+def build_strip_step(P, nex, ney, d, Pe, parts, rank, dev, dist, exchange="allreduce", overlap=True, seed=2024):
+    """This rank's strip (element columns of StripPartition(nex, parts)) and its bench step: the fused apply of the
+    CD system operator plus, with parts > 1, the interface assembly (StripApply: the interface positions first, the
+    RCCL all-reduce or send/recv started, the interior applied while it runs).  Returns (step, mesh, (T, y, kw),
+    (eb, ee)).  tests/test_gpu_rccl.py drives this with a real one-rank RCCL group and parts = 2."""
+    from sem_amd import _lib
+    from sem_amd.device import get_mesh
+    from sem_amd.parallel import StripApply, StripPartition
+    part = StripPartition(nex, parts)
+    eb, ee = part.bounds[rank], part.bounds[rank + 1]
+    mesh = get_mesh(P, nex, ney, d, d, eb, ee, dev.index)
+    T, u, v = make_inputs(mesh, seed=seed)
+    y = torch.empty_like(T)
+    kw = dict(c_stiff=1.0, c_gradx=Pe, cu=u, c_grady=Pe, cv=v, dir_mode=_lib.DIR_IDENTITY,
+              dir_sides=_lib.SIDE_W | _lib.SIDE_E)
+    strip = StripApply(part, mesh, dist, kind=exchange, overlap=overlap) if parts > 1 else None
+
+    def step():
+        if strip is None:
+            mesh.apply(T, y, **kw)
+        else:
+            strip(T, y, **kw)
+    return step, mesh, (T, y, kw), (eb, ee)
+
+
 def cpu_baseline(P, ne, Pe, seconds):
     """Oracle (CPU restatement of the reference path): SciPy CSR `Sys @ T` + Dirichlet rows,
     single core, cfg2.  Sys assembled once as the reference does (SEM.py:186-223)."""
@@ -263,27 +288,14 @@ def main():
 
     from sem_amd import _lib
     from sem_amd.device import get_mesh
-    from sem_amd.parallel import StripApply, StripPartition
 
     P, ne, Pe = args.P, args.ne, args.Pe
 
     def strip_case(nex, ney, d, steps, warmup, seed):
         """Build this rank's strip of an nex x ney mesh and time `steps` partitioned applies (apply + interface
         exchange).  Returns (seconds max-reduced over ranks, graph used, mesh, operands)."""
-        part = StripPartition(nex, world)
-        eb, ee = part.bounds[rank], part.bounds[rank + 1]
-        mesh = get_mesh(P, nex, ney, d, d, eb, ee, dev.index)
-        T, u, v = make_inputs(mesh, seed=seed)
-        y = torch.empty_like(T)
-        sides = _lib.SIDE_W | _lib.SIDE_E
-        kw = dict(c_stiff=1.0, c_gradx=Pe, cu=u, c_grady=Pe, cv=v, dir_mode=_lib.DIR_IDENTITY, dir_sides=sides)
-        strip = StripApply(part, mesh, dist, kind=args.exchange, overlap=bool(args.overlap)) if world > 1 else None
-
-        def step():
-            if strip is None:
-                mesh.apply(T, y, **kw)
-            else:
-                strip(T, y, **kw)
+        step, mesh, (T, y, kw), (eb, ee) = build_strip_step(P, nex, ney, d, Pe, world, rank, dev, dist,
+                                                            args.exchange, bool(args.overlap), seed)
 
         # N > 1 over RCCL: the whole step (apply, pack, RCCL all-reduce or send/recv, unpack) is captured
         # too -- RCCL collectives are stream-capturable -- so the per-step host cost (four launches and a
@@ -393,6 +405,12 @@ def main():
                                "bound": "hbm", "achieved": bb / kb / 1e9, "peak": HBM_PEAK_GBS, "unit_bw": "GB/s",
                                "frac": bb / kb / 1e9 / HBM_PEAK_GBS, "traffic": tb, "traffic_kernel": tbk,
                                "kernel_us": kb * 1e6}
+        # BASELINE.json's metric read literally (the Laplacian-only y = K T, 16 B/DOF) in the HBM regime
+        kbl = graph_kernel_us(lambda: big.apply(Tb, yb, c_stiff=1.0), dev, launches=50, trials=3) * 1e-6
+        bl = 16.0 * big.n_local
+        out["roofline_hbm"]["laplacian_only"] = {
+            "kernel": big.kernel_name(), "value": big.n_local / kbl, "unit": "DOF-updates/s", "kernel_us": kbl * 1e6,
+            "bytes_per_launch": bl, "achieved": bl / kbl / 1e9, "unit_bw": "GB/s", "frac": bl / kbl / 1e9 / HBM_PEAK_GBS}
         del Tb, ub, vb, yb
 
     if args.extra_steps > 0:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 12
+#define SEM_ABI_VERSION 13
 
 enum sem_status {
   SEM_OK = 0,
@@ -123,33 +123,32 @@ typedef struct sem_apply_desc {
   int pos_begin, pos_end;
 } sem_apply_desc;
 
-/* Kernel-selection knobs.  Every value selects a variant with bitwise-identical results (tile
- * shape, cache policy, argument passing); none changes an answer.  Defaults come from the
- * environment variable named beside each knob, read ONCE at the first use; 0 = library default. */
+/* Kernel-selection knobs (test / A-B use only).  Defaults come from the environment variable named
+ * beside each knob, read ONCE at the first use; 0 = library default.  The values are PROCESS-GLOBAL
+ * and unsynchronised: sem_set_tuning is not thread-safe, and a knob changed while launches are in
+ * flight on other threads or streams affects whichever launches read it afterwards.  Set knobs from
+ * one thread before launching; the handles themselves stay immutable (include note in sem_create).
+ * Round 6 retired the knobs whose A/B lost (their enum values stay reserved; sem_set_tuning returns
+ * SEM_EINVAL for them): band cache policy, marching kernel, tile order, GEMV / basis / condensed-solve
+ * load policies, GEMV shapes, the band kernel's other tiles and scalar-load coefficients, the column
+ * kernel's other tiles, the two-ended edge sweep. */
 enum sem_tune {
-  SEM_TUNE_BAND_TILE = 0, /* SEM_BAND_TILE: band kernel tile / variant (tools/kbench.py)          */
-  SEM_TUNE_BAND_CPOL = 1, /* SEM_BAND_CPOL: cache policy of the band kernel's y stores / u,v loads */
-  SEM_TUNE_BAND_KP = 2,   /* SEM_BAND_KP: -1 = struct-only kernel arguments, else preloaded      */
-  SEM_TUNE_MARCH_WG = 3,  /* SEM_MARCH_WG: workgroups of the marching variant                     */
-  SEM_TUNE_MFMA_TILE = 4, /* SEM_MFMA_TILE: 0 = band-form MFMA kernel; 1, 2, 3 = element-block MFMA */
-  SEM_TUNE_COL_TILE = 5,  /* SEM_COL_TILE: column kernel tile                                     */
+  SEM_TUNE_BAND_TILE = 0, /* SEM_BAND_TILE: 3 = DPP-broadcast coefficients, 4 = fp64 immediates (the
+                           * band kernel picks by mesh size; bitwise-identical results)              */
+  SEM_TUNE_RETIRED_1 = 1,
+  SEM_TUNE_BAND_KP = 2,   /* SEM_BAND_KP: -1 = struct-only kernel arguments, else preloaded (bitwise) */
+  SEM_TUNE_RETIRED_3 = 3,
+  SEM_TUNE_MFMA_TILE = 4, /* SEM_MFMA_TILE: 0 = band-form MFMA kernel; 3 = element-block MFMA (round 4) */
+  SEM_TUNE_RETIRED_5 = 5,
   SEM_TUNE_NS_APPLY = 6,  /* SEM_NS_APPLY: 1 = sem_ns_apply's LDS-tile form instead of the band form
-                           * (the one knob whose variants agree to rounding, not bitwise)           */
+                           * (agree to rounding, not bitwise)                                         */
   SEM_TUNE_EDGE_THOMAS = 7, /* SEM_EDGE_THOMAS: 1 = the ABI-9 runtime-width edge sweep of sem_nested_solve
-                             * instead of the templated one, 2 = the one-ended templated sweep even when
-                             * the two-ended factors are given (ABI 12; A/B only; agree to rounding)     */
-  SEM_TUNE_BAND_ORDER = 8,  /* SEM_BAND_ORDER: 1 = the band kernel's full tiles before its ghost tiles in
-                             * every XCD's share (measured slower; A/B only; bitwise identical) */
-  SEM_TUNE_GEMV_CPOL = 9,   /* SEM_GEMV_CPOL: 2 = sem_gemv_rows / rows2 load the operator with plain loads
-                               instead of the default non-temporal ones (bitwise-identical results)       */
-  SEM_TUNE_BASIS_CPOL = 10,  /* SEM_BASIS_CPOL: basis loads of sem_basis_dot2 / update -- 0: non-temporal in
-                                dot2, plain in update (measured best); 1: non-temporal in both; 2: plain in
-                                both (bitwise-identical results)                                        */
-  SEM_TUNE_COND_CPOL = 11,   /* SEM_COND_CPOL: 1 = the nested solve's element step reads its factors
-                                non-temporally (bitwise-identical; measured 0.5 % slower at cfg5)       */
-  SEM_TUNE_GEMV_SHAPE = 12,  /* SEM_GEMV_SHAPE: sem_gemv_rows rows per workgroup x loads in flight -- 0: 2 x 8
-                                (default), 1: 8 x 4, 2: 4 x 8, 3: 4 x 4 (round 4), 4: 8 x 2, 5: 1 x 8,
-                                6: 2 x 16, 7: 1 x 16 (bitwise-identical results)                       */
+                             * instead of the templated one (agree to rounding)                     */
+  SEM_TUNE_RETIRED_8 = 8,
+  SEM_TUNE_RETIRED_9 = 9,
+  SEM_TUNE_RETIRED_10 = 10,
+  SEM_TUNE_RETIRED_11 = 11,
+  SEM_TUNE_RETIRED_12 = 12,
   SEM_TUNE_COUNT = 13
 };
 
@@ -162,7 +161,8 @@ int sem_max_order(void);
  * Python loader refuses a library whose hash differs from the in-tree sources.  A "+diag" suffix
  * marks a diagnostic build. */
 const char* sem_build_id(void);
-/* Set / read a kernel-selection knob (enum sem_tune); SEM_EINVAL for an unknown knob. */
+/* Set / read a kernel-selection knob (enum sem_tune); SEM_EINVAL for an unknown or retired knob.
+ * Not thread-safe (process-global state, see enum sem_tune). */
 int sem_set_tuning(int knob, int value);
 int sem_get_tuning(int knob, int* value);
 
@@ -328,15 +328,8 @@ typedef struct sem_nested_desc {
    * columns edges n, n+1), and a work array Pw of nex * 2 * m doubles.  Used by sem_nested_iface_rhs. */
   const double* ABY;
   double* Pw;
-  /* ABI 12 (nullable; block-Thomas form only): the two-ended edge sweep.  The chain from edge 0 (Ed, El, Eu for
-   * k < edge_mid, as above) and the chain from edge N_ey (Edb[k] = inverse pivot block of the bottom chain for
-   * k > edge_mid, Es[k] = A_up[k] raw (edge k <- k+1), Eub[k-1] = Edb[k] A_lo[k-1] (edge k <- k-1)) run side by
-   * side and meet at edge_mid (1 <= edge_mid <= N_ey - 1), Edb[edge_mid] = the inverse of the meeting block:
-   * N_ey + 2 dependent block steps per column instead of 2 N_ey + 1.  Row-major blocks, as Ed / El / Eu. */
-  const double* Es;
-  const double* Edb;
-  const double* Eub;
-  int edge_mid;
+  /* (ABI 12's two-ended edge sweep -- Es, Edb, Eub, edge_mid -- was removed in ABI 13: without pivoting across
+   * its meeting block it lost accuracy on some meshes and made cfg5's coupled solve diverge) */
 } sem_nested_desc;
 /* Column e's right-hand side at R + e ld_r (interior offsets o = (l-1) m + c N_y + gy), minus
  * aIB[e][l-1][s][.] xB[e+s][.] when aIB and xB are given (the back substitution r = b - A_IB x_B);

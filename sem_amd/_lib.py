@@ -12,11 +12,12 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.environ.get("SEM_LIBDIR") or os.path.join(_HERE, "lib"), "libsemops.so")
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
-(TUNE_BAND_TILE, TUNE_BAND_CPOL, TUNE_BAND_KP, TUNE_MARCH_WG, TUNE_MFMA_TILE, TUNE_COL_TILE, TUNE_NS_APPLY,
- TUNE_EDGE_THOMAS, TUNE_BAND_ORDER, TUNE_GEMV_CPOL, TUNE_BASIS_CPOL,
- TUNE_COND_CPOL, TUNE_GEMV_SHAPE) = range(13)
+# kernel-selection knobs (include/sem_ops.h enum sem_tune; process-global, not thread-safe); the values between
+# them are retired knobs (round 6), refused by sem_set_tuning
+TUNE_BAND_TILE, TUNE_BAND_KP, TUNE_MFMA_TILE, TUNE_NS_APPLY, TUNE_EDGE_THOMAS = 0, 2, 4, 6, 7
+TUNE_RETIRED = (1, 3, 5, 8, 9, 10, 11, 12)
 SIDE_W, SIDE_E, SIDE_S, SIDE_N = 1, 2, 4, 8
 DIR_NONE, DIR_IDENTITY, DIR_REPLACE = 0, 1, 2
 ALGO_AUTO, ALGO_VALU, ALGO_MFMA, ALGO_COLUMN, ALGO_BAND = 0, 1, 2, 3, 4
@@ -52,8 +53,7 @@ class SemNestedDesc(C.Structure):
                 ("Xi", C.c_void_p), ("Aei", C.c_void_p), ("Yie", C.c_void_p), ("Se", C.c_void_p),
                 ("pi", C.c_void_p), ("pe", C.c_void_p), ("T", C.c_void_p), ("C", C.c_void_p), ("Ye", C.c_void_p),
                 ("Ed", C.c_void_p), ("El", C.c_void_p), ("Eu", C.c_void_p), ("XiB", C.c_void_p), ("AXB", C.c_void_p),
-                ("ABY", C.c_void_p), ("Pw", C.c_void_p), ("Es", C.c_void_p), ("Edb", C.c_void_p), ("Eub", C.c_void_p),
-                ("edge_mid", C.c_int)]
+                ("ABY", C.c_void_p), ("Pw", C.c_void_p)]
 
 
 class SemNsDesc(C.Structure):

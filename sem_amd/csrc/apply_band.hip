@@ -189,21 +189,14 @@ struct CList {
 
 template <int P, int NS>
 __device__ const typename CList<P, NS>::Tab kBandCoef = CList<P, NS>::make();
-// the same lists in the constant address space: read with wave-uniform compile-time offsets, they
-// become scalar-memory loads (s_load through the scalar cache) instead of two s_mov_b32 per fp64
-// immediate (coefficient mode CM = 2)
-template <int P, int NS>
-__constant__ typename CList<P, NS>::Tab kBandCoefC = CList<P, NS>::make();
 
 // acc + c * x with the coefficient of entry IDX of split S's list: CM = 0 an fp64 immediate (two
 // s_mov_b32 into an SGPR pair), CM = 1 a DPP broadcast from the split's VGPR-resident list (only valid
-// with every lane of the wave active: a DPP read of a disabled lane does not return its value),
-// CM = 2 a scalar load from the constant-memory copy of the list.
+// with every lane of the wave active: a DPP read of a disabled lane does not return its value).  (Round 2's
+// CM = 2, scalar loads from a constant-memory copy, measured no faster and was retired in round 6.)
 template <int CM, int P, int NS, int S, int IDX, int NCV>
 __device__ __forceinline__ double cfma(const double (&cv)[NCV], double c, double x, double acc) {
-  if constexpr (CM == 2) {
-    return fma(kBandCoefC<P, NS>.v[S * CList<P, NS>::NPAD + IDX], x, acc);
-  } else if constexpr (CM == 1) {
+  if constexpr (CM == 1) {
     asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
         : "+v"(acc)
         : "v"(cv[IDX / 16]), "v"(x), "n"(IDX % 16));
@@ -224,16 +217,22 @@ __device__ __forceinline__ void eo_rows(const double (&t)[2 * P + 1], double fk,
   using CL = CList<P, NS>;
   constexpr int H = E::H;
   double e[H], o[H];
-  if constexpr (L::needs_eo(S)) {
+  // row 0 (which reads the whole window) before the even / odd sums (which read t[P..2P] only): the left half of
+  // the window dies before e, o are formed (round 6: 8 fewer live VGPRs at P = 8)
+  auto form_eo = [&]() {
+    if constexpr (L::needs_eo(S)) {
 #pragma unroll
-    for (int m = 0; m < H; ++m) {
-      e[m] = t[P + m] + t[2 * P - m];
-      o[m] = t[P + m] - t[2 * P - m];
+      for (int m = 0; m < H; ++m) {
+        e[m] = t[P + m] + t[2 * P - m];
+        o[m] = t[P + m] - t[2 * P - m];
+      }
     }
-  }
+  };
+  if constexpr (!L::in_split(0, S)) form_eo();
   for_rows(std::make_integer_sequence<int, L::NITEMS>{}, [&](auto KI) {
     constexpr int kk = decltype(KI)::value;
     constexpr int it = L::code(kk);
+    if constexpr (kk == 1 && L::in_split(0, S)) form_eo();
     if constexpr (L::in_split(kk, S)) {
       constexpr int sl = L::slot(S, kk);
       constexpr int cb = CL::base(S, kk);
@@ -303,6 +302,12 @@ struct BCfg {
   static constexpr int PY = LW + 1;                     // result tiles: BX lines x LW columns
   static constexpr int NSTAGE = (RX * RY + THREADS - 1) / THREADS;
   static constexpr int NE = (BX * LW + THREADS - 1) / THREADS;  // epilogue nodes per thread
+  // staging (round 6): wave w stages window lines w + NW k, k < NSL (lanes = columns 0..63), and the columns
+  // 64..RY-1 of its lines (RYX per line) in NXL further loads
+  static constexpr int NSL = (RX + NW - 1) / NW;
+  static constexpr int RYX = RY - 64;
+  static constexpr int NXL = (NSL * RYX + 63) / 64;
+  static_assert(RY > 64 && RY <= 128, "staging assumes 64 < RY <= 128 window columns");
   static_assert(NS >= 1 && NS <= 4, "1 to 4 splits");
   static_assert(THREADS <= 1024, "workgroup too large");
 };
@@ -416,6 +421,19 @@ __device__ __forceinline__ double gll_w(int J) {
   return r;
 }
 
+// GLL weights of order P as a device table (the band kernel's LDS weight array ws[] is filled from it)
+template <int P>
+struct GllWTab {
+  double v[P + 1];
+  static constexpr GllWTab make() {
+    GllWTab t{};
+    for (int k = 0; k <= P; ++k) t.v[k] = GllConst<P>::w[k];
+    return t;
+  }
+};
+template <int P>
+__device__ const GllWTab<P> kGllW = GllWTab<P>::make();
+
 // FULL = false: no extra / accumulate terms, no Dirichlet mask or values (side bits only).
 // DPP = true: row coefficients from the split's DPP-broadcast list (CList) instead of immediates.
 // GRAD = false: no gradient / convection terms (mass + stiffness only: the Laplacian K x, the
@@ -434,45 +452,25 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   using PL = EPlan<P, NS>;
   using CL = CList<P, NS>;
   constexpr bool DPP = CM == 1;
-  constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW;
+  constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW, NW = C::NW;
   __shared__ double Ts[C::RX * PT];
   __shared__ double XK[BX * PY];
-  __shared__ double XG[BX * PY];
+  __shared__ double XG[GRAD ? BX * PY : 1];
   __shared__ double YK[BX * PY];
-  __shared__ double YG[BX * PY];
+  __shared__ double YG[GRAD ? BX * PY : 1];
   __shared__ double ws[n];
 
-  // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
-  // tiles (y fastest) and neighbouring tiles share their halo lines through that XCD's L2.
-  // SEM_BAND_ORDER=1 (a negative tiles_y): within each XCD's share the full tiles first and the tiles of the
-  // last tile row and column (the ghost positions: one line or one column, light) last, so that the
-  // dispatcher deals two full workgroups to every CU at cfg2.  Measured 3.5 % SLOWER at cfg2 (4.35 against
-  // 4.19 us, profiles/r04/cfg2_anatomy/order_ab.txt) and at 256^2, so the default is the contiguous order
-  // below.  Only the block -> tile map changes: results are bitwise those of any other order.
-  const int nb = pnblk, bid = blockIdx.x, tyn = ptiles_y < 0 ? -ptiles_y : ptiles_y, txn = nb / tyn;
-  const int NI = ptiles_y < 0 ? (txn - 1) * (tyn - 1) : 0;  // full tiles: off the last tile row and column
-  const int xcd = bid & 7, rk = bid >> 3, q8 = nb >> 3, rem = nb & 7, qi = NI >> 3, ri = NI & 7;
-  const int Fx = qi + (xcd < ri ? 1 : 0);  // full tiles of this XCD
-  int tx, ty;
-  if (ptiles_y > 0) {  // default: one contiguous run of tiles per XCD, ghost tiles where they fall
-    const int Lr = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + rk;
-    tx = Lr / tyn;
-    ty = Lr - tx * tyn;
-  } else if (rk < Fx) {
-    const int fi = xcd * qi + min(xcd, ri) + rk;
-    tx = fi / (tyn - 1);
-    ty = fi - tx * (tyn - 1);
-  } else {
-    const int gi = (xcd * q8 + min(xcd, rem)) - (xcd * qi + min(xcd, ri)) + (rk - Fx);
-    tx = gi < tyn ? txn - 1 : gi - tyn;
-    ty = gi < tyn ? gi : tyn - 1;
-  }
-  const int L = tx * tyn + ty;
+  // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of tiles (y fastest) and
+  // neighbouring tiles share their halo lines through that XCD's L2.
+  const int nb = pnblk, bid = blockIdx.x, tyn = ptiles_y;
+  const int xcd = bid & 7, rk = bid >> 3, q8 = nb >> 3, rem = nb & 7;
+  const int L = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + rk;
+  const int tx = L / tyn, ty = L - tx * tyn;
 
   const int lb0 = plb0, NY = pNY;
-  // element positions [m0, m1) x [n0, n1); position ex_end (ney) is the ghost holding the closing line (column)
-  // KP kernels cover every position; the struct kernel may be restricted to [pos0, pos1) (the
-  // multi-GPU overlap applies the interface positions first, then the interior)
+  // element positions [m0, m1) x [n0, n1); position ex_end (ney) is the ghost holding the closing line (column).
+  // KP kernels cover every position; the struct kernel may be restricted to [pos0, pos1) (the multi-GPU overlap
+  // applies the interface positions first, then the interior)
   const int m0 = pex_begin + (KP ? 0 : a.pos0) + tx * TXE;
   const int m1 = min(m0 + TXE, KP ? pex_end + 1 : pex_begin + a.pos1);
   const int n0 = ty * TYE, n1 = min(n0 + TYE, pney + 1);
@@ -481,19 +479,6 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   const int cols_ok = (min(n1, pney) - n0) * P + (n1 > pney ? 1 : 0);       // valid columns
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // Diagnostics (SEM_DIAG bit 8): s_memtime phase stamps held in SGPRs, written at the very end
-  // so that no diagnostic store sits in the vmcnt queue of the measured phases.
-  unsigned long long stv[7] = {0, 0, 0, 0, 0, 0, 0}, rt0 = 0, rt1 = 0;  // stv[6]: epilogue values formed (slot 10)
-  if (kDiag && !KP && a.stamps) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
-#define BSTAMP(k)                                                                      \
-  do {                                                                                 \
-    if (kDiag && (!KP || (k) >= 2) && a.stamps) {  /* KP: no stamps before the loads issue */   \
-      __builtin_amdgcn_sched_barrier(0);                                               \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stv[k])::"memory"); \
-      __builtin_amdgcn_sched_barrier(0);                                               \
-    }                                                                                  \
-  } while (0)
-  BSTAMP(0);
 
   const int nbytes = pnbytes;
   const bool has_u = pcu != nullptr, has_v = pcv != nullptr;
@@ -501,19 +486,17 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   const auto ry = brsrc(a.y, nbytes);
   const int nodeb = (gx0 - lb0) * NY + gy0;  // local DOF index of the tile's first node
 
-  // ---- issue every global load first, in the order they are consumed (vmcnt retires in order):
-  // the staged x window, then u, v of this thread's epilogue nodes.  Buffer bounds make lines
-  // outside the local range read 0; columns past the domain's y-ends wrap into neighbouring
-  // lines.  Neither is ever consumed.
-  const int sbase = (kDiag && !KP && (a.diag & 64)) ? -(1 << 30) : ((gx0 - P - lb0) * NY + gy0 - P) * 8;  // diag 64: no staging loads
-  double st[C::NSTAGE];
-#pragma unroll
-  for (int s = 0; s < C::NSTAGE; ++s) {
-    const int idx = min(tid + s * C::THREADS, C::RX * C::RY - 1);
-    const int rr = idx / C::RY, cc = idx - rr * C::RY;
-    st[s] = bload(rx, sbase + (rr * NY + cc) * 8);
-  }
-  // DPP variant: this wave's coefficient list (split of its role), entry 16 j + (lane & 15) in cv[j]
+  // ---- staging, one window line per wave step (round 6: per-lane index math once, not per staged value).
+  // Wave w stages lines rr = w + NW k of the window [gx0 - P, gx0 + BX] x [gy0 - P, gy0 + BY]: lanes = columns
+  // 0..63 (one load each), and the columns 64..RY-1 of all its lines together in NXL more loads.  A column outside
+  // [0, NY) carries the offset 2^31 + line offset, a line outside the local range a negative offset: both are
+  // outside the buffer (the launcher keeps nbytes + (P + 1) NY 8 <= 2^31), so every absent node loads 0 -- no
+  // select per value.  Loads are issued in the order they are consumed (vmcnt retires in order).
+  // the GLL weights for ws[]: loaded from a device table FIRST, so the load returns under the staging loads behind it
+  // (issued after them it put one more memory round trip on wave 0's way to the barrier: +2-6 % on HBM-sized meshes)
+  const double wsv = tid < n ? kGllW<P>.v[tid] : 0.0;
+  // DPP variant: this wave's coefficient list (split of its role), entry 16 j + (lane & 15) in cv[j] -- also before
+  // the staging loads (the contractions wait for it)
   double cv[DPP ? CL::NCV : 1];
   if constexpr (DPP) {
     const int wsplit = w < C::NXW ? (w / C::XW) % NS : (w - C::NXW) / C::YW;
@@ -523,6 +506,26 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   } else {
     cv[0] = 0.0;
   }
+  const int lstep = NW * NY * 8;
+  const int line0 = (gx0 - P - lb0 + w) * NY * 8;  // byte offset of this wave's first staged line
+  const int gyA = gy0 - P + lane;
+  const unsigned vA = (gyA >= 0 && gyA < NY) ? static_cast<unsigned>(gyA) * 8u : 0x80000000u;
+  double sA[C::NSL];
+#pragma unroll
+  for (int k = 0; k < C::NSL; ++k)
+    if (k < C::NSL - 1 || w + NW * k < C::RX)  // only the last step can pass the window's end
+      sA[k] = bload(rx, static_cast<int>(vA + static_cast<unsigned>(line0 + k * lstep)));
+  double sX[C::NXL];
+  int xts[C::NXL];
+#pragma unroll
+  for (int j = 0; j < C::NXL; ++j) {
+    const int lp = lane + 64 * j, k = lp / C::RYX, cc = 64 + lp - k * C::RYX, rr = w + NW * k;
+    const int gy = gy0 - P + cc;
+    const bool ok = k < C::NSL && rr < C::RX;
+    const unsigned vx = (ok && gy >= 0 && gy < NY) ? static_cast<unsigned>(gy) * 8u : 0x80000000u;
+    xts[j] = ok ? rr * PT + cc : -1;
+    sX[j] = bload(rx, static_cast<int>(vx + static_cast<unsigned>(line0 + k * lstep)));
+  }
   // epilogue nodes of this thread: q = tid + e*THREADS -> tile line r = q / LW, column c = q % LW
   double pu[C::NE], pv[C::NE];
   int eoff[C::NE];
@@ -531,28 +534,10 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   for (int e = 0; e < C::NE; ++e) {
     const int q = tid + e * C::THREADS;
     const int r = q / LW, c = q - r * LW;
-    const bool ok = q < BX * LW && r < rows_ok && c < cols_ok && !(kDiag && (a.diag & 32));  // diag 32: no u/v/y traffic
+    const bool ok = q < BX * LW && r < rows_ok && c < cols_ok;
     eoff[e] = ok ? nodeb + r * NY + c : -(1 << 26);  // out of bounds: touches no memory
   }
-  // The epilogue's pointwise operands are issued after the staged window has gone to LDS (round 4): issued
-  // with it, behind the cache-policy branch, they made the compiler wait for every load (vmcnt(0)) before
-  // the staging stores, so u and v landed before the barrier instead of during the contractions.
-  auto issue_pointwise = [&]() {
-#pragma unroll
-    for (int e = 0; e < C::NE; ++e) {
-      if (a.cpol & 256) {  // u, v are read once per launch: non-temporal
-        pu[e] = bload_c<2>(ru, eoff[e] * 8);
-        pv[e] = bload_c<2>(rv, eoff[e] * 8);
-      } else {
-        pu[e] = bload(ru, eoff[e] * 8);
-        pv[e] = bload(rv, eoff[e] * 8);
-      }
-    }
-    if constexpr (FULL) {
-#pragma unroll
-      for (int e = 0; e < C::NE; ++e) ops[e] = load_node_ops(a, eoff[e]);
-    }
-  };
+  const bool nt_uv = (a.cpol & 256) != 0;   // u, v are read once per launch: non-temporal (HBM-sized meshes)
   if constexpr (KP) {  // the struct's fields: fetched now, while the staging loads are in flight
     BPIN(a.y);
     BPIN(a.fKx);
@@ -566,30 +551,43 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
     BPIN(a.cpol);
     BPIN(a.lb1);
     BPIN(a.nex);
-    if constexpr (kDiag) BPIN(a.diag);
   }
 
-  // ---- LDS: weights, staged window (columns outside the domain staged as 0: absent elements)
-  if (tid < n) ws[tid] = gll_w<P>(tid);
+  // ---- LDS: staged window, weights
 #pragma unroll
-  for (int s = 0; s < C::NSTAGE; ++s) {
-    const int idx = tid + s * C::THREADS;
-    if ((s + 1) * C::THREADS <= C::RX * C::RY || idx < C::RX * C::RY) {
-      const int rr = idx / C::RY, cc = idx - rr * C::RY;
-      const int gy = gy0 - P + cc;
-      Ts[rr * PT + cc] = (gy >= 0 && gy < NY) ? st[s] : 0.0;
+  for (int k = 0; k < C::NSL; ++k)
+    if (k < C::NSL - 1 || w + NW * k < C::RX) Ts[(w + NW * k) * PT + lane] = sA[k];
+#pragma unroll
+  for (int j = 0; j < C::NXL; ++j)
+    if (xts[j] >= 0) Ts[xts[j]] = sX[j];
+  if (tid < n) ws[tid] = wsv;
+  // the epilogue's pointwise operands: issued after the staged window has gone to LDS, so they land during the
+  // contractions (round 4)
+  if (nt_uv) {
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e) {
+      pu[e] = bload_c<2>(ru, eoff[e] * 8);
+      pv[e] = bload_c<2>(rv, eoff[e] * 8);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e) {
+      pu[e] = bload(ru, eoff[e] * 8);
+      pv[e] = bload(rv, eoff[e] * 8);
     }
   }
-  issue_pointwise();
-  BSTAMP(1);
+  if constexpr (FULL) {
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e) ops[e] = load_node_ops(a, eoff[e]);
+  }
   __syncthreads();
-  BSTAMP(2);
 
   constexpr double w0 = GllConst<P>::w[0], wP = GllConst<P>::w[P];
   if (w < C::NXW) {
-    // ---- X role: wave = (element position xa, split xs), lane = column xc: the x-direction rows
-    // of the split from a (2P+1)-node window along x -> LDS.  Lines outside the local range are
-    // staged as 0, so absent elements contribute nothing.
+    // ---- X role: wave = (element position xa, split xs), lane = column xc: the x-direction rows of the split
+    // from a (2P+1)-node window along x -> LDS, scaled by the column's fKx My and fX My (round 6: the epilogue's
+    // column factors moved here, once per lane).  Lines outside the local range are staged as 0, so absent
+    // elements contribute nothing.
     const int xg = w / C::XW;
     const int xa = xg / NS, xs = xg - xa * NS;
     const int xc = (w - xg * C::XW) * 64 + lane;
@@ -608,24 +606,27 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
         for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
         double k[C::RP], g[C::RP];
         eo_rows<P, NS, s, CM>(t, fk, fg, k, g, cv);
+        const int jc = xc % P, nc = n0 + xc / P;
+        const double myc = jc != 0 ? ws[jc] : (nc - 1 >= 0 ? wP : 0.0) + (nc < pney ? w0 : 0.0);
+        const double sxk = a.fKx * myc, sxg = a.fX * myc;
 #pragma unroll
         for (int sl = 0; sl < PL::nrows(s); ++sl) {
           const int i = PL::row(s, sl);
           if (xghost && i != 0) continue;  // a ghost position holds its row 0 only
-          XK[(xa * P + i) * PY + xc] = k[sl];
-          if constexpr (GRAD) XG[(xa * P + i) * PY + xc] = g[sl];
+          XK[(xa * P + i) * PY + xc] = sxk * k[sl];
+          if constexpr (GRAD) XG[(xa * P + i) * PY + xc] = sxg * g[sl];
         }
       });
     }
   } else {
-    // ---- Y role: wave = split h, lane = (line r, element position b): the y-direction columns of
-    // the split from a (2P+1)-node window along the line -> LDS, scaled by Mx of the line.
+    // ---- Y role: wave = split h, lane = (line r, element position b): the y-direction columns of the split from
+    // a (2P+1)-node window along the line -> LDS, scaled by Mx of the line.
     const int wy = w - C::NXW;
     const int h = wy / C::YW;
     const int t2 = (wy - h * C::YW) * 64 + lane;
     const bool yok = t2 < C::YL && t2 % BX < rows_ok && t2 / BX < n1 - n0;
-    // the DPP variant computes on every lane (a DPP read of a disabled lane is not its value) from
-    // clamped, in-bounds positions; only the LDS stores are predicated
+    // the DPP variant computes on every lane (a DPP read of a disabled lane is not its value) from clamped,
+    // in-bounds positions; only the LDS stores are predicated
     const int r = DPP ? min(t2 % BX, BX - 1) : t2 % BX, b = DPP ? min(t2 / BX, C::YL / BX - 1) : t2 / BX;
     if (DPP || yok) {
       const bool hasLy = n0 + b - 1 >= 0, hasRy = n0 + b < pney;
@@ -655,59 +656,47 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
       });
     }
   }
-  BSTAMP(3);
   __syncthreads();
-  BSTAMP(4);
 
-  // ---- epilogue, every wave: node (r, c) = both directions + pointwise terms + Dirichlet rows;
-  // all values are formed before the first (coalesced) store
+  // ---- epilogue, every wave: node (r, c) = X + Y rows (+ mass) + the pointwise convection terms; Dirichlet rows, the extra /
+  // accumulate terms and the strip-ownership rules only in a tile that can hold one (tile-uniform test)
+  const int NXg = a.NXg;
+  bool special = FULL;
+  if (a.dir_mode != SEM_DIR_NONE) {
+    const int gxl = gx0 + rows_ok - 1, gyl = gy0 + cols_ok - 1;
+    const unsigned sd = a.sides;
+    special = special || ((sd & SEM_SIDE_W) && gx0 == 0) || ((sd & SEM_SIDE_E) && gxl >= NXg - 1) ||
+              ((sd & SEM_SIDE_S) && gy0 == 0) || ((sd & SEM_SIDE_N) && gyl >= NY - 1);
+  }
   double zz[C::NE];
 #pragma unroll
   for (int e = 0; e < C::NE; ++e) {
     const int q = tid + e * C::THREADS;
     const int r = q / LW, c = q - r * LW;
-    zz[e] = 0.0;
-    if (q < BX * LW && r < rows_ok && c < cols_ok) {
-      const int i = r % P, me = m0 + r / P;
+    const int o = r * PY + c;
+    double z = XK[o] + YK[o];
+    if (a.fM != 0.0) {   // the mass term (not on the CD / NS hot paths: a uniform branch, its weights from LDS)
+      const int i = r % P, me = m0 + r / P, j = c % P, ne = n0 + c / P;
       const double mx = i != 0 ? ws[i] : (me - 1 >= pex_begin ? wP : 0.0) + (me < pex_end ? w0 : 0.0);
-      const int j = c % P, ne = n0 + c / P;
       const double my = j != 0 ? ws[j] : (ne - 1 >= 0 ? wP : 0.0) + (ne < pney ? w0 : 0.0);
-      const int o = r * PY + c;
-      const double xv = Ts[(P + r) * PT + P + c];
-      const double u_ = has_u ? pu[e] : 1.0, v_ = has_v ? pv[e] : 1.0;
-      double z = fma(a.fKx * my, XK[o], YK[o]);
-      z = fma(a.fM * mx * my, xv, z);
-      if constexpr (GRAD) {
-        z = fma(a.fX * u_, my * XG[o], z);
-        z = fma(v_, YG[o], z);
-      }
-      zz[e] = finish_node<FULL>(a, ops[e], gx0 + r, gy0 + c, xv, z);
+      z = fma(a.fM * mx * my, Ts[(P + r) * PT + P + c], z);
     }
+    if constexpr (GRAD) {
+      z = fma(has_u ? pu[e] : 1.0, XG[o], z);
+      z = fma(has_v ? pv[e] : 1.0, YG[o], z);
+    }
+    if (special && eoff[e] >= 0) z = finish_node<FULL>(a, ops[e], gx0 + r, gy0 + c, Ts[(P + r) * PT + P + c], z);
+    zz[e] = z;
   }
-  BSTAMP(6);
+  if ((a.cpol & 255) == 3) {   // system-scope stores (a mesh whose working set stays in the MALL)
 #pragma unroll
-  for (int e = 0; e < C::NE; ++e) {
-    const int q = tid + e * C::THREADS;
-    const int r = q / LW, c = q - r * LW;
-    if (q < BX * LW && r < rows_ok && c < cols_ok && !(kDiag && (a.diag & 16))) bstore_any(a.cpol, ry, eoff[e] * 8, zz[e]);
+    for (int e = 0; e < C::NE; ++e)
+      if (eoff[e] >= 0) bstore_c<17>(ry, eoff[e] * 8, zz[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e)
+      if (eoff[e] >= 0) bstore(ry, eoff[e] * 8, zz[e]);
   }
-  BSTAMP(5);
-  if (kDiag && a.stamps) {
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1)::"memory");
-    unsigned xcc_, hw_;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)" : "=s"(xcc_), "=s"(hw_));
-    if (lane == 0) {  // 16 slots per wave: 0-5 s_memtime phases, 6 tile, 7 hw id, 8-9 s_memrealtime start/end,
-                      // 10 epilogue values formed (before the stores)
-      unsigned long long* o = a.stamps + (blockIdx.x * C::NW + w) * 16;
-      for (int k = 0; k < 6; ++k) o[k] = stv[k];
-      o[10] = stv[6];
-      o[6] = L;
-      o[7] = (static_cast<unsigned long long>(hw_) << 8) | (xcc_ & 0xf);
-      o[8] = rt0;
-      o[9] = rt1;
-    }
-  }
-#undef BSTAMP
 }
 
 template <int P, int TXE, int TYE, int NS, bool FULL, int CM, bool GRAD = true>
@@ -751,279 +740,6 @@ __global__ __launch_bounds__((BCfg<P, TXE, TYE, NS>::THREADS)) void apply_band_k
     int pnblk, int ptiles_y, int pnbytes, const BandArgs a) {
   band_body<P, TXE, TYE, NS, FULL, CM, GRAD, true>(px, pcu, pcv, pNY, plb0, pex_begin, pex_end, pney, pnblk, ptiles_y,
                                                     pnbytes, a);
-}
-
-// ---- Marching form of the band kernel (HBM-sized meshes).
-// Same per-node arithmetic as apply_band<P, 1, TYE, NS> in the same order (results are bitwise
-// identical), but one workgroup owns a column band of TYE element rows and marches along x over a
-// chunk of `mchunk` element positions.  The staged (2P+1)-line window is a ring in LDS: a step
-// loads only the P lines the next element adds (the left element's lines stay), so x is read
-// once per band instead of (2P+1)/P times, and the next element's lines, u and v are loaded into
-// registers while the current element is contracted and stored -- the memory pipe stays busy
-// through the compute phases instead of every workgroup alternating load / compute / store.
-// Step m (element position m; ghost position ex_end holds only the closing line):
-//   A  ring holds lines [mP-P, mP+P]            -> X / Y contractions (ring reads) -> XK..YG
-//   B  new lines [(m+1)P+1, (m+1)P+P] -> ring slots of lines [mP-P, mP-1] (read only before B);
-//      epilogue of lines [mP, mP+P) (ring reads of those lines only) -> y
-template <int P, int TYE, int NS, bool FULL, bool DPP, bool GRAD>
-__global__ __launch_bounds__((BCfg<P, 1, TYE, NS>::THREADS)) void apply_march(const BandArgs a) {
-  using C = BCfg<P, 1, TYE, NS>;
-  using PL = EPlan<P, NS>;
-  using CL = CList<P, NS>;
-  constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW;
-  constexpr int R = C::RX;                                  // ring of 2P+1 lines
-  constexpr int NSTEP = (P * C::RY + C::THREADS - 1) / C::THREADS;  // new-line loads per thread per step
-  __shared__ double Ts[R * PT];
-  __shared__ double XK[BX * PY];
-  __shared__ double XG[BX * PY];
-  __shared__ double YK[BX * PY];
-  __shared__ double YG[BX * PY];
-  __shared__ double ws[n];
-
-  BPIN(a.x);
-  BPIN(a.y);
-  BPIN(a.cu);
-  BPIN(a.cv);
-  BPIN(a.fKx);
-  BPIN(a.fKy);
-  BPIN(a.fM);
-  BPIN(a.fX);
-  BPIN(a.fY);
-  BPIN(a.NY);
-  BPIN(a.lb0);
-  BPIN(a.lb1);
-  BPIN(a.ex_begin);
-  BPIN(a.ex_end);
-  BPIN(a.ney);
-  BPIN(a.nex);
-  BPIN(a.NXg);
-  BPIN(a.tiles_y);
-  BPIN(a.nbytes);
-  BPIN(a.dir_mode);
-  BPIN(a.sides);
-  BPIN(a.flags);
-  BPIN(a.nblk);
-  BPIN(a.cpol);
-  BPIN(a.mchunk);
-
-  // XCD-aware remap as in apply_band: an XCD gets a contiguous run of (chunk, band) pairs, band
-  // fastest, so bands marching side by side share their column halos in that XCD's L2
-  const int nb = a.nblk, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nb >> 3, rem = nb & 7;
-  const int Lq = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (bid >> 3);
-  const int cx = Lq / a.tiles_y, ty = Lq - cx * a.tiles_y;
-  const int mA = a.ex_begin + cx * a.mchunk, mB = min(mA + a.mchunk, a.ex_end + 1);
-  const int lb0 = a.lb0, NY = a.NY;
-  const int n0 = ty * TYE, n1 = min(n0 + TYE, a.ney + 1);
-  const int gy0 = n0 * P;
-  const int cols_ok = (min(n1, a.ney) - n0) * P + (n1 > a.ney ? 1 : 0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nbytes = a.nbytes;
-  const bool has_u = a.flags & 1, has_v = a.flags & 2;
-  const auto rx = brsrc(a.x, nbytes), ru = brsrc(a.cu, has_u ? nbytes : 0), rv = brsrc(a.cv, has_v ? nbytes : 0);
-  const auto ry = brsrc(a.y, nbytes);
-
-  // column part of a staged index, and whether it is inside the domain (outside: staged as 0)
-  auto stage_col_ok = [&](int cc) { const int gy = gy0 - P + cc; return gy >= 0 && gy < NY; };
-
-  // ---- prologue: the full window of the first position, u / v (and operands) of its nodes
-  {
-    const int sbase = ((mA * P - P - lb0) * NY + gy0 - P) * 8;
-    double st[C::NSTAGE];
-#pragma unroll
-    for (int s = 0; s < C::NSTAGE; ++s) {
-      const int idx = min(tid + s * C::THREADS, C::RX * C::RY - 1);
-      const int rr = idx / C::RY, cc = idx - rr * C::RY;
-      st[s] = bload(rx, sbase + (rr * NY + cc) * 8);
-    }
-    if (tid < n) ws[tid] = gll_w<P>(tid);
-#pragma unroll
-    for (int s = 0; s < C::NSTAGE; ++s) {
-      const int idx = tid + s * C::THREADS;
-      if ((s + 1) * C::THREADS <= C::RX * C::RY || idx < C::RX * C::RY) {
-        const int rr = idx / C::RY, cc = idx - rr * C::RY;
-        Ts[rr * PT + cc] = stage_col_ok(cc) ? st[s] : 0.0;
-      }
-    }
-  }
-  double cv[DPP ? CL::NCV : 1];
-  if constexpr (DPP) {
-    const int wsplit = w < C::NXW ? (w / C::XW) % NS : (w - C::NXW) / C::YW;
-    const double* tb = kBandCoef<P, NS>.v + wsplit * CL::NPAD + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < CL::NCV; ++j) cv[j] = tb[16 * j];
-  } else {
-    cv[0] = 0.0;
-  }
-  // epilogue nodes of this thread (q = tid + e*THREADS -> line r, column c of the position)
-  int er[C::NE], ec_[C::NE];
-#pragma unroll
-  for (int e = 0; e < C::NE; ++e) {
-    const int q = tid + e * C::THREADS;
-    er[e] = q / LW;
-    ec_[e] = q - er[e] * LW;
-  }
-  auto node_off = [&](int m, int e) {  // local DOF of epilogue node e at position m (OOB if none)
-    const int rows_ok = m < a.ex_end ? P : 1;
-    const int q = tid + e * C::THREADS;
-    const bool ok = q < BX * LW && er[e] < rows_ok && ec_[e] < cols_ok;
-    return ok ? (m * P + er[e] - lb0) * NY + gy0 + ec_[e] : -(1 << 26);
-  };
-  double pu[C::NE], pv[C::NE];
-  NodeOps ops[C::NE] = {};
-  auto load_uv = [&](int m, double (&u_)[C::NE], double (&v_)[C::NE], NodeOps (&o_)[C::NE]) {
-#pragma unroll
-    for (int e = 0; e < C::NE; ++e) {
-      const int off = node_off(m, e);
-      if (a.cpol & 256) {
-        u_[e] = bload_c<2>(ru, off * 8);
-        v_[e] = bload_c<2>(rv, off * 8);
-      } else {
-        u_[e] = bload(ru, off * 8);
-        v_[e] = bload(rv, off * 8);
-      }
-      if constexpr (FULL) o_[e] = load_node_ops(a, off);
-    }
-  };
-  load_uv(mA, pu, pv, ops);
-
-  constexpr double w0 = GllConst<P>::w[0], wP = GllConst<P>::w[P];
-  int sh = 0;  // ring slot of the window's first line (mP - P)
-#pragma unroll 1
-  for (int m = mA; m < mB; ++m) {
-    const bool more = m + 1 < mB;  // uniform
-    // ---- next position's new lines and node operands, in flight through this step
-    double nx[NSTEP];
-    double pun[C::NE], pvn[C::NE];
-    NodeOps opsn[C::NE] = {};
-    if (more) {
-      const int nbase = (((m + 1) * P + 1 - lb0) * NY + gy0 - P) * 8;
-#pragma unroll
-      for (int s = 0; s < NSTEP; ++s) {
-        const int idx = min(tid + s * C::THREADS, P * C::RY - 1);
-        const int rr = idx / C::RY, cc = idx - rr * C::RY;
-        nx[s] = bload(rx, nbase + (rr * NY + cc) * 8);
-      }
-      load_uv(m + 1, pun, pvn, opsn);
-    }
-    auto slot = [&](int rr) { const int s_ = sh + rr; return s_ >= R ? s_ - R : s_; };
-    __syncthreads();  // A
-
-    const int rows_ok = m < a.ex_end ? P : 1;
-    if (w < C::NXW) {
-      const int xg = w / C::XW;
-      const int xs = xg % NS;
-      const int xc = (w - xg * C::XW) * 64 + lane;
-      const bool xghost = m == a.ex_end, hasLx = m - 1 >= a.ex_begin;
-      const double fk = (hasLx ? 1.0 : 0.0) + (xghost ? 0.0 : 1.0);
-      const double fg = (xghost ? 0.0 : 1.0) - (hasLx ? 1.0 : 0.0);
-      for_rows(std::make_integer_sequence<int, NS>{}, [&](auto S) {
-        constexpr int s = decltype(S)::value;
-        if (xs != s) return;
-        double t[2 * P + 1];
-        constexpr int q0 = PL::needs_left(s) ? 0 : P;
-#pragma unroll
-        for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[slot(qq) * PT + P + xc];
-#pragma unroll
-        for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
-        double k[C::RP], g[C::RP];
-        eo_rows<P, NS, s, DPP ? 1 : 0>(t, fk, fg, k, g, cv);
-#pragma unroll
-        for (int sl = 0; sl < PL::nrows(s); ++sl) {
-          const int i = PL::row(s, sl);
-          if (xghost && i != 0) continue;
-          XK[i * PY + xc] = k[sl];
-          if constexpr (GRAD) XG[i * PY + xc] = g[sl];
-        }
-      });
-    } else {
-      const int wy = w - C::NXW;
-      const int h = wy / C::YW;
-      const int t2 = (wy - h * C::YW) * 64 + lane;
-      const bool yok = t2 < C::YL && t2 % BX < rows_ok && t2 / BX < n1 - n0;
-      const int r = DPP ? min(t2 % BX, BX - 1) : t2 % BX, b = DPP ? min(t2 / BX, C::YL / BX - 1) : t2 / BX;
-      if (DPP || yok) {
-        const bool hasLy = n0 + b - 1 >= 0, hasRy = n0 + b < a.ney;
-        const double fk = (hasLy ? 1.0 : 0.0) + (hasRy ? 1.0 : 0.0), fg = (hasRy ? 1.0 : 0.0) - (hasLy ? 1.0 : 0.0);
-        const int i = r;
-        const double mx = i != 0 ? ws[i] : (m - 1 >= a.ex_begin ? wP : 0.0) + (m < a.ex_end ? w0 : 0.0);
-        const double sk = a.fKy * mx, sg = a.fY * mx;
-        const int srow = slot(P + r) * PT + b * P;
-        for_rows(std::make_integer_sequence<int, NS>{}, [&](auto H) {
-          constexpr int hh = decltype(H)::value;
-          if (h != hh) return;
-          double t[2 * P + 1];
-          constexpr int q0 = PL::needs_left(hh) ? 0 : P;
-#pragma unroll
-          for (int qq = q0; qq <= 2 * P; ++qq) t[qq] = Ts[srow + qq];
-#pragma unroll
-          for (int qq = 0; qq < q0; ++qq) t[qq] = 0.0;
-          double k[C::RP], g[C::RP];
-          eo_rows<P, NS, hh, DPP ? 1 : 0>(t, fk, fg, k, g, cv);
-          if (yok) {
-#pragma unroll
-            for (int sl = 0; sl < PL::nrows(hh); ++sl) {
-              const int j = PL::row(hh, sl);
-              YK[r * PY + b * P + j] = sk * k[sl];
-              if constexpr (GRAD) YG[r * PY + b * P + j] = sg * g[sl];
-            }
-          }
-        });
-      }
-    }
-    __syncthreads();  // B
-
-    // ---- next position's new lines into the ring (slots of lines mP-P..mP-1, no longer read)
-    if (more) {
-#pragma unroll
-      for (int s = 0; s < NSTEP; ++s) {
-        const int idx = tid + s * C::THREADS;
-        if ((s + 1) * C::THREADS <= P * C::RY || idx < P * C::RY) {
-          const int rr = idx / C::RY, cc = idx - rr * C::RY;
-          Ts[slot(rr) * PT + cc] = stage_col_ok(cc) ? nx[s] : 0.0;  // line mP+P+1+rr = slot (sh+rr) of step m
-        }
-      }
-    }
-
-    // ---- epilogue of position m
-    double zz[C::NE];
-    int eoff[C::NE];
-#pragma unroll
-    for (int e = 0; e < C::NE; ++e) {
-      const int r = er[e], c = ec_[e];
-      eoff[e] = node_off(m, e);
-      zz[e] = 0.0;
-      if (eoff[e] >= 0) {
-        const int i = r;
-        const double mx = i != 0 ? ws[i] : (m - 1 >= a.ex_begin ? wP : 0.0) + (m < a.ex_end ? w0 : 0.0);
-        const int j = c % P, ne = n0 + c / P;
-        const double my = j != 0 ? ws[j] : (ne - 1 >= 0 ? wP : 0.0) + (ne < a.ney ? w0 : 0.0);
-        const int o = r * PY + c;
-        const double xv = Ts[slot(P + r) * PT + P + c];
-        const double u_ = has_u ? pu[e] : 1.0, v_ = has_v ? pv[e] : 1.0;
-        double z = fma(a.fKx * my, XK[o], YK[o]);
-        z = fma(a.fM * mx * my, xv, z);
-        if constexpr (GRAD) {
-          z = fma(a.fX * u_, my * XG[o], z);
-          z = fma(v_, YG[o], z);
-        }
-        zz[e] = finish_node<FULL>(a, ops[e], m * P + r, gy0 + c, xv, z);
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < C::NE; ++e)
-      if (eoff[e] >= 0) bstore_any(a.cpol, ry, eoff[e] * 8, zz[e]);
-    if (more) {
-#pragma unroll
-      for (int e = 0; e < C::NE; ++e) {
-        pu[e] = pun[e];
-        pv[e] = pvn[e];
-        if constexpr (FULL) ops[e] = opsn[e];
-      }
-    }
-    sh = sh + P >= R ? sh + P - R : sh + P;
-  }
 }
 
 static int hip_check_b(hipError_t e, const char* what) {
@@ -1074,7 +790,7 @@ static BandArgs band_args(const ApplyArgs& g) {
   b.has_e1 = g.has_e1;
   b.has_e2 = g.has_e2;
   b.stamps = g.stamps;
-  b.cpol = tune(SEM_TUNE_BAND_CPOL) ? tune(SEM_TUNE_BAND_CPOL) : band_cpol(g.n_local32);
+  b.cpol = band_cpol(g.n_local32);
   return b;
 }
 
@@ -1085,18 +801,14 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   // element positions [pos0, pos1) of 0..ncols (ncols = the ghost position of the closing line)
   const bool ranged = g.pos1 > 0;
   const int pos0 = ranged ? g.pos0 : 0, pos1 = ranged ? g.pos1 : ncols + 1;
-  // diagnostic bit 128 (diagnostic builds only; WRONG results on the closing line and column): the ghost tiles
-  // are not launched, so the grid is the full tiles alone (512 equal workgroups at cfg2, two per CU) -- the
-  // upper bound of what folding the closing line / column into the last full tiles could gain
-  const bool skip_ghost = kDiag && (g.diag & 128) && !ranged;
-  const int tiles_x = (pos1 - pos0 + TXE - 1) / TXE - (skip_ghost ? 1 : 0);
-  const int tiles_y = (h->ney + 1 + TYE - 1) / TYE - (skip_ghost ? 1 : 0);
+  const int tiles_x = (pos1 - pos0 + TXE - 1) / TXE;
+  const int tiles_y = (h->ney + 1 + TYE - 1) / TYE;
   const long long nblk = static_cast<long long>(tiles_x) * tiles_y;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
   BandArgs b = band_args(g);
   b.pos0 = pos0;
   b.pos1 = pos1;
-  b.tiles_y = tune(SEM_TUNE_BAND_ORDER) == 1 ? -tiles_y : tiles_y;
+  b.tiles_y = tiles_y;
   b.nblk = static_cast<int>(nblk);
   const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
   const bool grad = g.cX != 0.0 || g.cY != 0.0;
@@ -1123,73 +835,6 @@ static int launch_band(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
   else
     hipLaunchKernelGGL((apply_band<P, TXE, TYE, NS, false, CM, false>), grid, block, 0, s, b);
   return hip_check_b(hipGetLastError(), "apply (band) launch");
-}
-
-// Marching launch: one workgroup per (column band of TYE element rows, chunk of element positions).
-// The chunk length is chosen so that about SEM_MARCH_WG (default 1024: four per CU) workgroups cover
-// the mesh in one resident round.
-template <int P, int TYE, int NS, bool DPP>
-static int launch_march(const ApplyArgs& g, const sem_handle* h, hipStream_t s) {
-  using C = BCfg<P, 1, TYE, NS>;
-  const int ncols = h->ex_end - h->ex_begin;
-  const long long npos = ncols + 1;  // + the ghost position of the closing line
-  const long long tiles_y = (h->ney + 1 + TYE - 1) / TYE;
-  const long long target = std::max(64, tune(SEM_TUNE_MARCH_WG) ? tune(SEM_TUNE_MARCH_WG) : 1024);
-  const long long chunks_want = std::max(1LL, std::min(npos, target / tiles_y));
-  const long long mchunk = (npos + chunks_want - 1) / chunks_want;
-  const long long nchunks = (npos + mchunk - 1) / mchunk;
-  const long long nblk = nchunks * tiles_y;
-  if (nblk <= 0 || nblk > 0x7fffffffLL) return set_error(SEM_EINVAL, "mesh too large for one launch");
-  BandArgs b{};
-  b.x = g.x;
-  b.y = g.y;
-  b.cu = g.cu;
-  b.cv = g.cv;
-  b.fKx = g.cK * g.sx;
-  b.fKy = g.cK * g.sy;
-  b.fM = g.cM * g.hxy;
-  b.fX = g.cX * g.hy;
-  b.fY = g.cY * g.hx;
-  b.NY = static_cast<int>(g.NY);
-  b.lb0 = static_cast<int>(g.line_begin);
-  b.lb1 = static_cast<int>(g.line_end);
-  b.ex_begin = g.ex_begin;
-  b.ex_end = g.ex_end;
-  b.ney = g.ney;
-  b.nex = g.nex;
-  b.NXg = static_cast<int>(g.NXg);
-  b.tiles_y = static_cast<int>(tiles_y);
-  b.nbytes = g.n_local32 * 8;
-  b.dir_mode = g.dir_mode;
-  b.diag = g.diag;
-  b.sides = g.sides;
-  b.flags = (g.cu ? 1u : 0u) | (g.cv ? 2u : 0u);
-  b.ea = g.ea;
-  b.eb = g.eb;
-  b.ec = g.ec;
-  b.ed = g.ed;
-  b.dval = g.dval;
-  b.mask = g.mask;
-  b.cE = g.cE;
-  b.cA = g.cA;
-  b.has_e1 = g.has_e1;
-  b.has_e2 = g.has_e2;
-  b.stamps = nullptr;
-  b.nblk = static_cast<int>(nblk);
-  b.mchunk = static_cast<int>(mchunk);
-  b.cpol = tune(SEM_TUNE_BAND_CPOL) ? tune(SEM_TUNE_BAND_CPOL) : band_cpol(g.n_local32);
-  const bool full = g.has_e1 || g.has_e2 || g.cA != 0.0 || g.mask || g.dval;
-  const bool grad = g.cX != 0.0 || g.cY != 0.0;
-  const dim3 grid(static_cast<unsigned>(nblk)), block(C::THREADS);
-  if (full && grad)
-    hipLaunchKernelGGL((apply_march<P, TYE, NS, true, DPP, true>), grid, block, 0, s, b);
-  else if (full)
-    hipLaunchKernelGGL((apply_march<P, TYE, NS, true, DPP, false>), grid, block, 0, s, b);
-  else if (grad)
-    hipLaunchKernelGGL((apply_march<P, TYE, NS, false, DPP, true>), grid, block, 0, s, b);
-  else
-    hipLaunchKernelGGL((apply_march<P, TYE, NS, false, DPP, false>), grid, block, 0, s, b);
-  return hip_check_b(hipGetLastError(), "apply (march) launch");
 }
 
 // =========================================================================== band-form MFMA kernel
@@ -1430,24 +1075,12 @@ struct BandShape {
 template <int P>
 static int launch_band_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
   using S = BandShape<P>;
-  const int force = tune(SEM_TUNE_BAND_TILE);  // tuning knob (sem_set_tuning / SEM_BAND_TILE, read once)
-  if constexpr (P == 8) {
-    if (force == 1) return launch_band<P, 1, S::TYE, 4>(args, h, s);
-    if (force == 2) return launch_band<P, 2, S::TYE, 4>(args, h, s);
-    if (force == 5) return launch_band<P, 2, S::TYE, 2, 1>(args, h, s);
-    if (force == 6) return launch_band<P, 1, S::TYE, 1, 1>(args, h, s);
-  }
-  if constexpr (P == 8 || P == 12) {  // the marching variant covers whole strips only
-    if (force == 7 && args.pos1 == 0) return launch_march<P, S::TYE, S::NS, false>(args, h, s);
-    if (force == 8 && args.pos1 == 0) return launch_march<P, S::TYE, S::NS, true>(args, h, s);
-  }
-  if (force == 3) return launch_band<P, S::TXE, S::TYE, S::NS, 1>(args, h, s);
-  if (force == 4) return launch_band<P, S::TXE, S::TYE, S::NS, 0>(args, h, s);
-  if (force == 9) return launch_band<P, S::TXE, S::TYE, S::NS, 2>(args, h, s);  // scalar-load coefficients
-  // DPP-broadcast coefficients: 2-4 % faster from ~1M DOFs up (the VALU-bound regime), 2-3 % slower on
-  // the launch-latency-bound cfg2 mesh, whose extra coefficient loads sit on the critical path
-  // (profiles/r01/band/dpp_ab.txt)
-  if (args.n_local32 >= (1 << 20)) return launch_band<P, S::TXE, S::TYE, S::NS, 1>(args, h, s);
+  // coefficient mode: DPP-broadcast lists from ~1M DOFs up (the issue-bound regime), fp64 immediates below (the
+  // launch-latency-bound meshes, whose extra coefficient loads sit on the critical path: profiles/r01/band/dpp_ab.txt);
+  // SEM_BAND_TILE = 3 / 4 forces DPP / immediates (the bitwise-variant tests)
+  const int force = tune(SEM_TUNE_BAND_TILE);
+  const bool dpp = force == 3 || (force != 4 && args.n_local32 >= (1 << 20));
+  if (dpp) return launch_band<P, S::TXE, S::TYE, S::NS, 1>(args, h, s);
   return launch_band<P, S::TXE, S::TYE, S::NS, 0>(args, h, s);
 }
 
@@ -1455,14 +1088,10 @@ std::string band_kernel_name(int P, long long n_local) {
   const int TYE = std::max(1, 64 / P), TXE = std::min(4, std::max(1, 8 / P));
   const int NS = P >= 2 ? 2 : 1;
   const int force = tune(SEM_TUNE_BAND_TILE);
-  const bool dpp = force == 3 || force == 8 || (force == 0 && n_local >= (1 << 20));
-  const bool smem = force == 9;
-  if (force == 7 || force == 8)
-    return "sem::apply_march<" + std::to_string(P) + ", " + std::to_string(TYE) + ", " + std::to_string(NS) +
-           (dpp ? ", dpp" : "") + ">";
+  const bool dpp = force == 3 || (force != 4 && n_local >= (1 << 20));
   const bool kp = tune(SEM_TUNE_BAND_KP) >= 0;
   return std::string(kp ? "sem::apply_band_kp<" : "sem::apply_band<") + std::to_string(P) + ", " + std::to_string(TXE) +
-         ", " + std::to_string(TYE) + ", " + std::to_string(NS) + (dpp ? ", dpp" : "") + (smem ? ", smem" : "") + ">";
+         ", " + std::to_string(TYE) + ", " + std::to_string(NS) + (dpp ? ", dpp" : "") + ">";
 }
 
 int launch_apply_bmfma(const ApplyArgs& a, const sem_handle* h, hipStream_t s) {

@@ -243,10 +243,8 @@ template <int R, int U>
 static void launch_row_gemv_ru(RowGemv2Args& g, int M, int parts, hipStream_t s) {
   const int nb = (M + R - 1) / R;
   g.nb0 = nb;
-  if (tune(SEM_TUNE_GEMV_CPOL) != 2)
-    hipLaunchKernelGGL((row_gemv_kernel<true, true, R, U>), dim3(parts * nb), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL((row_gemv_kernel<true, false, R, U>), dim3(parts * nb), dim3(256), 0, s, g);
+  // non-temporal operator loads (round 5 A/B, profiles/r05/gemv_cpol/: the plain-load variant was retired in round 6)
+  hipLaunchKernelGGL((row_gemv_kernel<true, true, R, U>), dim3(parts * nb), dim3(256), 0, s, g);
 }
 
 // parts = 1 (sem_gemv_rows) or 2 (sem_gemv_rows2: blocks [0, nb) the first GEMV, the rest the second)
@@ -257,18 +255,9 @@ static void launch_row_gemv(RowGemv2Args& g, int M, int parts, bool vec, hipStre
     hipLaunchKernelGGL((row_gemv_kernel<false>), dim3(parts * nb), dim3(256), 0, s, g);
     return;
   }
-  // default 2 x 8 (alternated A/B, profiles/r05/gemv_shape/: cfg5 velocity solve 7.90 -> 7.82 ms against round 4's
-  // 4 x 4, the sweep's m x 2m GEMV 5.05 -> 5.3 TB/s)
-  switch (tune(SEM_TUNE_GEMV_SHAPE)) {
-    case 1: launch_row_gemv_ru<8, 4>(g, M, parts, s); break;
-    case 2: launch_row_gemv_ru<4, 8>(g, M, parts, s); break;
-    case 3: launch_row_gemv_ru<4, 4>(g, M, parts, s); break;
-    case 4: launch_row_gemv_ru<8, 2>(g, M, parts, s); break;
-    case 5: launch_row_gemv_ru<1, 8>(g, M, parts, s); break;
-    case 6: launch_row_gemv_ru<2, 16>(g, M, parts, s); break;
-    case 7: launch_row_gemv_ru<1, 16>(g, M, parts, s); break;
-    default: launch_row_gemv_ru<2, 8>(g, M, parts, s); break;
-  }
+  // 2 rows per workgroup x 8 loads in flight (alternated A/B over eight shapes, profiles/r05/gemv_shape/: cfg5 velocity
+  // solve 7.90 -> 7.82 ms against round 4's 4 x 4; the other shapes were retired in round 6)
+  launch_row_gemv_ru<2, 8>(g, M, parts, s);
 }
 
 }  // namespace sem

@@ -39,19 +39,11 @@ Tuning& tuning() {
   static Tuning t = [] {  // the environment is read once, at the first use
     Tuning r{};
     r.v[SEM_TUNE_BAND_TILE] = env_int("SEM_BAND_TILE");
-    r.v[SEM_TUNE_BAND_CPOL] = env_int("SEM_BAND_CPOL");
     const char* kp = std::getenv("SEM_BAND_KP");  // SEM_BAND_KP=0: struct-only kernel arguments
     r.v[SEM_TUNE_BAND_KP] = (kp && std::atoi(kp) == 0) ? -1 : 0;
-    r.v[SEM_TUNE_MARCH_WG] = env_int("SEM_MARCH_WG");
     r.v[SEM_TUNE_MFMA_TILE] = env_int("SEM_MFMA_TILE");
-    r.v[SEM_TUNE_COL_TILE] = env_int("SEM_COL_TILE");
     r.v[SEM_TUNE_NS_APPLY] = env_int("SEM_NS_APPLY");
     r.v[SEM_TUNE_EDGE_THOMAS] = env_int("SEM_EDGE_THOMAS");
-    r.v[SEM_TUNE_BAND_ORDER] = env_int("SEM_BAND_ORDER");
-    r.v[SEM_TUNE_GEMV_CPOL] = env_int("SEM_GEMV_CPOL");
-    r.v[SEM_TUNE_BASIS_CPOL] = env_int("SEM_BASIS_CPOL");
-    r.v[SEM_TUNE_COND_CPOL] = env_int("SEM_COND_CPOL");
-    r.v[SEM_TUNE_GEMV_SHAPE] = env_int("SEM_GEMV_SHAPE");
     return r;
   }();
   return t;

@@ -149,12 +149,9 @@ int sem_basis_dot2(const double* V, int64_t ldv, int k, int64_t n, const double*
   if (groups > 65535) return sem::set_error(SEM_EINVAL, "basis_dot2: too many basis vectors");
   auto s = reinterpret_cast<hipStream_t>(stream);
   const int nch = dot2_chunks(n);
-  if (sem::tune(SEM_TUNE_BASIS_CPOL) != 2)
-    hipLaunchKernelGGL(sem::basis_dot2_kernel<true>, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n,
-                       nch, a, b, work);
-  else
-    hipLaunchKernelGGL(sem::basis_dot2_kernel<false>, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n,
-                       nch, a, b, work);
+  // non-temporal basis loads in the dot pass (round 5 A/B, profiles/r05/basis_cpol/: -6.5 %)
+  hipLaunchKernelGGL(sem::basis_dot2_kernel<true>, dim3(nch, groups), dim3(sem::kDotThreads), 0, s, V, ldv, k, n, nch,
+                     a, b, work);
   hipLaunchKernelGGL(sem::basis_dot2_finish, dim3((2 * k + 255) / 256), dim3(256), 0, s, work, k, nch, out);
   return sem::hip_check_k(hipGetLastError(), "basis_dot2 launch");
 }
@@ -166,12 +163,9 @@ int sem_basis_update(const double* V, int64_t ldv, int k, int64_t n, const doubl
   const int64_t blocks = (n + sem::kUpdThreads - 1) / sem::kUpdThreads;
   if (blocks > 0x7fffffffLL) return sem::set_error(SEM_EINVAL, "basis_update: vector too long");
   auto s = reinterpret_cast<hipStream_t>(stream);
-  if (sem::tune(SEM_TUNE_BASIS_CPOL) == 1)
-    hipLaunchKernelGGL(sem::basis_update_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(sem::kUpdThreads), 0,
-                       s, V, ldv, k, n, c, w);
-  else
-    hipLaunchKernelGGL(sem::basis_update_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(sem::kUpdThreads), 0,
-                       s, V, ldv, k, n, c, w);
+  // plain loads in the update pass (non-temporal measured slower there, round 5)
+  hipLaunchKernelGGL(sem::basis_update_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(sem::kUpdThreads), 0, s,
+                     V, ldv, k, n, c, w);
   return sem::hip_check_k(hipGetLastError(), "basis_update launch");
 }
 

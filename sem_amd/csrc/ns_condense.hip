@@ -42,8 +42,6 @@ struct CondArgs {
   double* Pw;                  // ABI 11: per-column interface partial sums (nex, 2, m)
   const double* aBI;           // ABI 11 (sem_nested_iface_rhs): interface <- interior lines, (nex, 2, P-1, m)
   const double *Ed, *El, *Eu;  // block-Thomas factors of the edge Schur complement (Se == nullptr)
-  const double *Es, *Edb, *Eub;  // ABI 12: the bottom chain of the two-ended edge sweep (nullable)
-  int edge_mid;
   const int64_t *pi, *pe;
   double *T, *C, *Ye;
   const double* R;     // column e interior at R + e ld_r (offset o)
@@ -146,10 +144,8 @@ __global__ __launch_bounds__(kCondThreads) void cond_fwd_kernel(const CondArgs a
 }
 
 static void launch_cond_fwd(const CondArgs& a, unsigned elems, size_t lds, hipStream_t s) {
-  if (tune(SEM_TUNE_COND_CPOL) == 1)
-    hipLaunchKernelGGL(cond_fwd_kernel<true>, dim3(elems), dim3(kCondThreads), lds, s, a);
-  else
-    hipLaunchKernelGGL(cond_fwd_kernel<false>, dim3(elems), dim3(kCondThreads), lds, s, a);
+  // plain factor loads (non-temporal measured slower in the nested element step, round 5)
+  hipLaunchKernelGGL(cond_fwd_kernel<false>, dim3(elems), dim3(kCondThreads), lds, s, a);
 }
 
 // K1 of the back substitution (ABI 11): r_i = b_i - A_iB x_B, so Xi r_i = Xi b_i - XiB x_B|n and
@@ -503,166 +499,6 @@ static void launch_edge_thomas(const CondArgs& a, hipStream_t s) {
     launch_edge_thomas<B + 1>(a, s);
 }
 
-// K2, two-ended block-Thomas form (ABI 12): two waves per column.  Wave 0 runs the chain from edge 0
-// (z_k = Ed_k (r_k - El_{k-1} z_{k-1}), k < mid), wave 1 the chain from edge N_ey (w_k = Edb_k (r_k - Es_k w_{k+1}),
-// k > mid), side by side; at the meeting edge wave 0 forms x_mid = Edb_mid (r_mid - El_{mid-1} z_{mid-1} -
-// Es_mid w_{mid+1}), and both back-substitute outward (x_k = z_k - Eu_k x_{k+1} above, x_k = w_k - Eub_{k-1} x_{k-1}
-// below).  Each wave keeps the one-ended kernel's lane layout (half-rows, pair sums through LDS), operand ring and
-// wave-local LDS ordering; the two barriers at the meeting edge are the only cross-wave synchronisation.
-// N_ey + 2 dependent block steps per column instead of 2 N_ey + 1.
-template <int B>
-__global__ __launch_bounds__(128) void cond_edge_twisted_kernel(const CondArgs a) {
-  constexpr int H = EdgeThomas<B>::H, D = EdgeThomas<B>::D;
-  constexpr int64_t bb = static_cast<int64_t>(B) * B;
-  __shared__ double pt[2][2][2 * H], pz[2][2][2 * H], xm[2][2 * H];  // [wave][half][row] partial sums
-  const int e = blockIdx.x, nb = a.ney + 1, mid = a.edge_mid;
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5, j0 = h * H;
-  const bool act = i < 2 * H, row = i < B, own = row && h == 0;
-  const double* C = a.C + static_cast<int64_t>(e) * a.ney * 2 * B;
-  const double* Ed = a.Ed + static_cast<int64_t>(e) * nb * bb;
-  const double* El = a.El + static_cast<int64_t>(e) * a.ney * bb;
-  const double* Eu = a.Eu + static_cast<int64_t>(e) * a.ney * bb;
-  const double* Es = a.Es + static_cast<int64_t>(e) * a.ney * bb;
-  const double* Edb = a.Edb + static_cast<int64_t>(e) * nb * bb;
-  const double* Eub = a.Eub + static_cast<int64_t>(e) * a.ney * bb;
-  double* Ye = a.Ye + static_cast<int64_t>(e) * a.n_e;
-  double* Y = a.Y + e * a.ld_y;
-  const int nc = B / (a.P - 1), NY = a.m / nc;
-  const int64_t off_i = static_cast<int64_t>(i / nc) * a.m + static_cast<int64_t>(i % nc) * NY;
-  auto edge_off = [&](int k) { return off_i + static_cast<int64_t>(k) * a.P; };
-  const int ic = i < B ? i : B - 1;
-  const int64_t off_c = static_cast<int64_t>(ic / nc) * a.m + static_cast<int64_t>(ic % nc) * NY;
-  const bool coupled = a.aIB != nullptr;
-  auto redge = [&](int k, EdgeRhs& q) {
-    const int64_t o = off_c + static_cast<int64_t>(k) * a.P, l1 = o / a.m, r = o - l1 * a.m;
-    const double* rp = a.R + e * a.ld_r + o;
-    const double* ab = coupled ? a.aIB + ((static_cast<int64_t>(e) * (a.P - 1) + l1) * 2) * a.m + r : rp;
-    const double* xb = coupled ? a.xB + static_cast<int64_t>(e) * a.m + r : rp;
-    const int64_t am = coupled ? a.m : 0;
-    const int kc0 = k < a.ney ? k : a.ney - 1, kc1 = k > 0 ? k - 1 : 0;
-    q.r = *rp;
-    q.a0 = ab[0];
-    q.x0 = xb[0];
-    q.a1 = ab[am];
-    q.x1 = xb[am];
-    q.c0 = C[static_cast<int64_t>(kc0) * 2 * B + ic];
-    q.c1 = C[static_cast<int64_t>(kc1) * 2 * B + B + ic];
-  };
-  double (*PT)[2 * H] = pt[wv], (*PZ)[2 * H] = pz[wv];
-  // this wave's chain: n steps, step j at edge k(j); the coupling block of edge k toward the chain's previous edge,
-  // the pivot inverse of edge k, the back-substitution block of edge k
-  const bool top = wv == 0;
-  const int nf = top ? mid : nb - 1 - mid;
-  auto kf = [&](int j) { return top ? j : nb - 1 - j; };
-  auto cpl = [&](int k) { return top ? El + (k > 0 ? k - 1 : 0) * bb : Es + (k < a.ney ? k : a.ney - 1) * bb; };
-  auto piv = [&](int k) { return top ? Ed + k * bb : Edb + k * bb; };
-  double rl[D][H], rd[D][H];
-  EdgeRhs rr[D];
-  auto load_fwd = [&](int j, int s) {
-    const int k = kf(j < nf ? j : nf - 1);
-    load_half_row<B>(cpl(k), i, h, rl[s]);
-    load_half_row<B>(piv(k), i, h, rd[s]);
-    redge(k, rr[s]);
-  };
-  auto fwd_step = [&](int j, int s) {
-    const int k = kf(j);
-    double t = rr[s].value(own, coupled, k, a.ney);
-    if (j > 0) t -= half_dot<H>(rl[s], &PZ[0][j0], &PZ[1][j0]);
-    wave_lds_sync();
-    if (act) PT[h][i] = row ? t : 0.0;
-    wave_lds_sync();
-    const double z = half_dot<H>(rd[s], &PT[0][j0], &PT[1][j0]);
-    wave_lds_sync();
-    if (act) PZ[h][i] = row ? z : 0.0;
-    wave_lds_sync();
-    if (own) Ye[static_cast<int64_t>(k) * B + i] = PZ[0][i] + PZ[1][i];
-  };
-  if (act) {
-#pragma unroll
-    for (int s = 0; s < D; ++s) load_fwd(s, s);
-    int j0f = 0;
-    for (; j0f + D <= nf; j0f += D) {
-#pragma unroll
-      for (int s = 0; s < D; ++s) {
-        fwd_step(j0f + s, s);
-        load_fwd(j0f + s + D, s);
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < D - 1; ++s)
-      if (j0f + s < nf) fwd_step(j0f + s, s);
-  }
-  __syncthreads();   // both chains have ended: pz[0] = z_{mid-1}, pz[1] = w_{mid+1} (partial sums)
-  if (top && act) {  // the meeting edge
-    double ra[H], rb[H], rm[H];
-    EdgeRhs q;
-    load_half_row<B>(El + (mid - 1) * bb, i, h, ra);
-    load_half_row<B>(Es + mid * bb, i, h, rb);
-    load_half_row<B>(Edb + mid * bb, i, h, rm);
-    redge(mid, q);
-    const double t = q.value(own, coupled, mid, a.ney) - half_dot<H>(ra, &pz[0][0][j0], &pz[0][1][j0]) -
-                     half_dot<H>(rb, &pz[1][0][j0], &pz[1][1][j0]);
-    wave_lds_sync();
-    pt[0][h][i] = row ? t : 0.0;
-    wave_lds_sync();
-    const double x = half_dot<H>(rm, &pt[0][0][j0], &pt[0][1][j0]);
-    xm[h][i] = row ? x : 0.0;
-    wave_lds_sync();
-    if (own) {
-      const double v = xm[0][i] + xm[1][i];
-      Ye[static_cast<int64_t>(mid) * B + i] = v;
-      Y[edge_off(mid)] = v;
-    }
-  }
-  __syncthreads();   // x_mid in xm for both chains
-  if (!act) return;
-  // ---- back substitution outward from the meeting edge: step j at edge kb(j), operator of edge k
-  const int nbk = top ? mid : nb - 1 - mid;
-  auto kb = [&](int j) { return top ? mid - 1 - j : mid + 1 + j; };
-  auto bop = [&](int k) { return top ? Eu + k * bb : Eub + (k - 1) * bb; };
-  double ru[D][H], rz[D];
-  auto load_back = [&](int j, int s) {
-    const int k = kb(j < nbk ? j : nbk - 1);
-    load_half_row<B>(bop(k), i, h, ru[s]);
-    rz[s] = Ye[static_cast<int64_t>(k) * B + ic];
-  };
-  auto back_step = [&](int j, int s) {
-    const int k = kb(j);
-    const double* src0 = j == 0 ? &xm[0][j0] : &PZ[0][j0];
-    const double* src1 = j == 0 ? &xm[1][j0] : &PZ[1][j0];
-    const double y = (own ? rz[s] : 0.0) - half_dot<H>(ru[s], src0, src1);
-    wave_lds_sync();
-    PZ[h][i] = row ? y : 0.0;
-    wave_lds_sync();
-    if (own) {
-      const double v = PZ[0][i] + PZ[1][i];
-      Ye[static_cast<int64_t>(k) * B + i] = v;
-      Y[edge_off(k)] = v;
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < D; ++s) load_back(s, s);
-  int c0 = 0;
-  for (; c0 + D <= nbk; c0 += D) {
-#pragma unroll
-    for (int s = 0; s < D; ++s) {
-      back_step(c0 + s, s);
-      load_back(c0 + s + D, s);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < D - 1; ++s)
-    if (c0 + s < nbk) back_step(c0 + s, s);
-}
-
-template <int B>
-static void launch_edge_twisted(const CondArgs& a, hipStream_t s) {
-  if (a.ne1 == B)
-    hipLaunchKernelGGL(cond_edge_twisted_kernel<B>, dim3(a.nex), dim3(128), 0, s, a);
-  else if constexpr (B < kThomasB)
-    launch_edge_twisted<B + 1>(a, s);
-}
-
 // K3: y_i = T - Yie [y_e[n]; y_e[n+1]] for element (e, n), written to the element's interior nodes.
 __global__ __launch_bounds__(kCondThreads) void cond_back_kernel(const CondArgs a) {
   extern __shared__ double lds[];
@@ -791,14 +627,6 @@ static int nested_args(const sem_nested_desc* d, const double* R, int64_t ld_r, 
   a.Ed = d->Ed;
   a.El = d->El;
   a.Eu = d->Eu;
-  if (thomas && d->Es) {
-    if (!d->Edb || !d->Eub || d->edge_mid < 1 || d->edge_mid > d->ney - 1)
-      return set_error(SEM_EINVAL, "nested_solve: two-ended edge sweep needs Edb, Eub and 1 <= edge_mid <= ney - 1");
-    a.Es = d->Es;
-    a.Edb = d->Edb;
-    a.Eub = d->Eub;
-    a.edge_mid = d->edge_mid;
-  }
   a.pi = d->pi;
   a.pe = d->pe;
   a.T = d->T;
@@ -828,8 +656,6 @@ static int nested_args(const sem_nested_desc* d, const double* R, int64_t ld_r, 
 static int nested_edge(const CondArgs& a, hipStream_t s) {
   if (a.Se == nullptr && tune(SEM_TUNE_EDGE_THOMAS) == 1)
     hipLaunchKernelGGL(cond_edge_thomas_rt_kernel, dim3(a.nex), dim3(64), 0, s, a);
-  else if (a.Se == nullptr && a.Es != nullptr && tune(SEM_TUNE_EDGE_THOMAS) != 2)
-    launch_edge_twisted<1>(a, s);
   else if (a.Se == nullptr)
     launch_edge_thomas<1>(a, s);
   else

@@ -38,6 +38,7 @@
 namespace sem {
 
 int launch_apply_band(const ApplyArgs& a, const sem_handle* h, hipStream_t s);  // apply_band.hip
+static bool band_fits(const sem_handle* h) { return h->n_local + (h->P + 1) * h->NY < (int64_t(1) << 28); }
 std::string band_kernel_name(int P, long long n_local);
 int launch_apply_bmfma(const ApplyArgs& a, const sem_handle* h, hipStream_t s);  // apply_band.hip
 std::string bmfma_kernel_name(int P);
@@ -684,10 +685,8 @@ static int launch_apply_mfma_auto(const ApplyArgs& args, const sem_handle* h, hi
   constexpr int TL = (32 / P) > 0 ? 32 / P : 1;
   constexpr int TS = (16 / P) > 0 ? 16 / P : 1;
   const long long big_tiles = static_cast<long long>((h->ex_end - h->ex_begin + TL - 1) / TL) * ((h->ney + TL - 1) / TL);
-  const int force = tune(SEM_TUNE_MFMA_TILE);  // tuning knob (sem_set_tuning / SEM_MFMA_TILE, read once)
-  if (force == 2 || (force == 0 && big_tiles >= 4 * 256)) return launch_apply_mfma<P, TL, TL, 4, true, false>(args, h, s);
-  if (force == 1) return launch_apply_mfma<P, TS, TS, 2, false, false>(args, h, s);
-  return launch_apply_mfma<P, TS, TS, 4, false, true>(args, h, s);   // force 3: the round-4 default
+  if (big_tiles >= 4 * 256) return launch_apply_mfma<P, TL, TL, 4, true, false>(args, h, s);
+  return launch_apply_mfma<P, TS, TS, 4, false, true>(args, h, s);   // the round-4 default
 }
 
 // =========================================================================== column kernel
@@ -885,17 +884,7 @@ static int launch_apply_col(const ApplyArgs& args_in, const sem_handle* h, hipSt
 
 template <int P>
 static int launch_apply_col_auto(const ApplyArgs& args, const sem_handle* h, hipStream_t s) {
-  const int force = tune(SEM_TUNE_COL_TILE);  // tuning knob (sem_set_tuning / SEM_COL_TILE, read once)
-  constexpr int RS = (P % 4 == 0) ? 4 : (P % 2 == 0 ? 2 : 1);
-  constexpr int BYs = 64 / RS > 16 ? 64 / RS : 16;
-  if (force == 1) return launch_apply_col<P, 2, BYs, RS>(args, h, s);
-  if (force == 2) return launch_apply_col<P, 4, 64, 1>(args, h, s);
-  if constexpr (RS > 1) {
-    if (force == 4) return launch_apply_col<P, 2, 64, RS>(args, h, s);
-    if (force == 5) return launch_apply_col<P, 1, 64, RS>(args, h, s);
-    if (force == 6) return launch_apply_col<P, 1, 64, 2>(args, h, s);
-    if (force == 7) return launch_apply_col<P, 2, 64, 2>(args, h, s);
-  }
+  // 2 element columns x 64 lines, no row split (the other tiles of rounds 1-2 lost their A/B; retired in round 6)
   return launch_apply_col<P, 2, 64, 1>(args, h, s);
 }
 
@@ -1013,8 +1002,14 @@ extern "C" {
 
 int sem_abi_version(void) { return SEM_ABI_VERSION; }
 
+static bool retired_knob(int knob) {
+  return knob == SEM_TUNE_RETIRED_1 || knob == SEM_TUNE_RETIRED_3 || knob == SEM_TUNE_RETIRED_5 ||
+         (knob >= SEM_TUNE_RETIRED_8 && knob <= SEM_TUNE_RETIRED_12);
+}
+
 int sem_set_tuning(int knob, int value) {
   if (knob < 0 || knob >= SEM_TUNE_COUNT) return set_error(SEM_EINVAL, "unknown tuning knob");
+  if (retired_knob(knob)) return set_error(SEM_EINVAL, "retired tuning knob (round 6)");
   tuning().v[knob] = value;
   return SEM_OK;
 }
@@ -1193,10 +1188,12 @@ int sem_apply(sem_handle* h, const sem_apply_desc* d, const double* x, double* y
   // fits its 32-bit buffer offsets (it beats the other kernels from 64^2 to 1024^2 elements);
   // the single-phase column kernel above that.
   const bool fits32 = h->n_local < (int64_t(1) << 28);
-  const bool band_auto = fits32;
-  if (ranged && !fits32) return set_error(SEM_EUNSUPPORTED, "element-position ranges need n_local < 2^28");
+  // the band kernel's staging offsets (an absent column at 2^31 + a line offset) stay outside the buffer when
+  // n_local + (P + 1) N_y <= 2^28 (apply_band.hip, band_body)
+  const bool band_auto = band_fits(h);
+  if (ranged && !band_auto) return set_error(SEM_EUNSUPPORTED, "element-position ranges need n_local + (P+1) N_y < 2^28");
   if (d->algo == SEM_ALGO_BAND || (d->algo == SEM_ALGO_AUTO && band_auto)) {
-    if (!fits32) return set_error(SEM_EUNSUPPORTED, "band path needs n_local < 2^28");
+    if (!band_auto) return set_error(SEM_EUNSUPPORTED, "band path needs n_local + (P+1) N_y < 2^28");
     return launch_apply_band(a, h, s);
   }
   const bool use_col = d->algo == SEM_ALGO_COLUMN || d->algo == SEM_ALGO_AUTO;
@@ -1243,7 +1240,7 @@ int sem_kernel_name(const sem_handle* h, int algo, char* buf, int len) {
   if (!h || !buf || len < 1) return set_error(SEM_EINVAL, "bad arguments");
   std::string name;
   const int P = h->P;
-  if (algo == SEM_ALGO_BAND || (algo == SEM_ALGO_AUTO && h->n_local < (int64_t(1) << 28))) {
+  if (algo == SEM_ALGO_BAND || (algo == SEM_ALGO_AUTO && band_fits(h))) {
     name = band_kernel_name(P, h->n_local);
   } else if (algo == SEM_ALGO_COLUMN || algo == SEM_ALGO_AUTO) {
     name = "sem::apply_tp_col<" + std::to_string(P) + ", 2, 64, 1>";

@@ -23,6 +23,7 @@ condensation itself is unit-tested on CPU against SciPy's sparse solve
 (tests/test_velocity_solve.py); the block assembly needs the GPU.
 """
 import contextlib
+import math
 import os
 import time
 
@@ -404,13 +405,6 @@ class VelocityJacobianSolver:
         # ABI-9 form: O(N_ey ne1^2) doubles per column read per solve instead of the n_e^2 of the dense
         # inverse -- 1.5 MB instead of 64 MB per cfg5 column); "dense" keeps the dense inverse
         self.edge_solve = "auto"
-        # ABI 12 two-ended edge sweep: "auto" on the GPU (the kernel's form), True also on the CPU (the torch form,
-        # for tests), False never.  Opt-in (SEM_EDGE_TWISTED=1): with it on, cfg5's coupled JNK solve at Ra = 1e4
-        # diverged where the one-ended sweep reproduces round 4's converged run
-        env = os.environ.get("SEM_EDGE_TWISTED", "0")
-        self.edge_two_ended = {"1": "auto", "force": True}.get(env, False)
-        if env == "force":   # tests: block-Thomas edge solves, two-ended, on any device
-            self.edge_dense_max, self.edge_solve = 0, "thomas"
         self._edge_thomas = False
         # HIP nested solves: "coupled" (ABI 11: the interface right-hand side from the forward element step's
         # T = Xi b_i and the edge values, sem_nested_iface_rhs; the back substitution T -= Xi A_iB x_B from the
@@ -534,24 +528,6 @@ class VelocityJacobianSolver:
             Et = [torch.empty(sh, **z) for sh in ((nex, ney + 1, ne1, ne1), (nex, ney, ne1, ne1), (nex, ney, ne1, ne1))]
             self._EtT = tuple(Et)                                   # row-major blocks (ABI 10)
             self._Ed, self._El, self._Eu = Et
-        # ABI 12: the two-ended edge sweep (chains from edge 0 and from edge N_ey meeting at edge t): its bottom
-        # chain's factors beside the one-ended ones (which the dense fallback and the top chain use), and the meeting
-        # block of three candidate edges t; check_refinement's probe picks the sweep (_select_edge_sweep).  Until
-        # then, and without a probe, the solve runs the one-ended sweep.
-        nb = ney + 1
-        mid = nb // 2
-        two = self.edge_two_ended
-        self._edge_mid, self._edge_twisted, self._tw_done = 0, False, False
-        self._tw_ready = (self._edge_thomas and nb >= 3
-                          and (two is True or (two == "auto" and self.device.type == "cuda")))
-        self._Etw = None
-        if self._tw_ready:   # Es = A_up (raw), Edb[k > t] = bottom pivot inverses, Edb[t] = M_t^-1, Eub[k-1] = UhB_k
-            self._Etw = tuple(torch.empty(sh, **z) for sh in ((nex, ney, ne1, ne1), (nex, ney + 1, ne1, ne1),
-                                                               (nex, ney, ne1, ne1)))
-            self._tw_cand = list(dict.fromkeys(t for t in (mid, mid + 1, mid - 1) if 1 <= t <= nb - 2))
-            # M_t^-1 of every candidate, and the bottom pivot inverse Db_t that slot t of Edb holds otherwise
-            self._tw_Mi = torch.empty((nex, len(self._tw_cand), ne1, ne1), **z)
-            self._tw_Db = torch.empty((nex, len(self._tw_cand), ne1, ne1), **z)
         if self.device.type == "cuda":
             T = [torch.empty(s[:-2] + (s[-1], s[-2]), **z) for s in shapes]
             if self._edge_thomas:
@@ -663,9 +639,6 @@ class VelocityJacobianSolver:
             self._edge_to_dense(c0)
         if self._edge_thomas:
             self._Ed[c0:c1], self._El[c0:c1], self._Eu[c0:c1] = fac[0], Sl, fac[1]
-            if self._tw_ready:
-                with self._phase("edge_twisted"):
-                    self._twisted_edge_factor(Sd, Su, Sl, fac, c0, c1)
         else:
             self._Se_inv[c0:c1] = Se_inv
         with self._phase("coupling_pieces"):
@@ -713,102 +686,6 @@ class VelocityJacobianSolver:
             Cv[:, n, :, n, :] += C_GG.permute(1, 0, 2, 3)
             inv = self._group_perm()
             return Cg[:, inv][:, :, inv]
-
-    def _twisted_edge_factor(self, Sd, Su, Sl, fac, c0, c1):
-        """Bottom chain and candidate meeting blocks of the two-ended edge sweep (ABI 12), for columns [c0, c1):
-          bottom  Db_{nb-1} = Sd_{nb-1}^-1,  UhB_k = Db_k Sl_{k-1},  Db_k = (Sd_k - Su_k UhB_{k+1})^-1   (k > t)
-          middle  M_t^-1 = (Sd_t - Sl_{t-1} UhT_{t-1} - Su_t UhB_{t+1})^-1
-        (the top chain's Dinv_k, UhT_k = Dinv_k Su_k for k < t are the one-ended factors), for each candidate
-        meeting edge t (the middle edge and its two neighbours)."""
-        Dinv, Uh = fac
-        nb = Sd.shape[1]
-        lo = min(self._tw_cand)
-        inv = lambda A: torch.linalg.inv_ex(A)[0]  # noqa: E731
-        Es, Edb, Eub = self._Etw
-        Es[c0:c1] = Su
-        Db = inv(Sd[:, nb - 1])
-        Edb[c0:c1, nb - 1] = Db
-        for k in range(nb - 1, lo, -1):
-            if k < nb - 1:
-                Db = inv(Sd[:, k] - Su[:, k] @ Eub[c0:c1, k])          # Eub[:, k] holds UhB_{k+1}
-                Edb[c0:c1, k] = Db
-            Eub[c0:c1, k - 1] = Db @ Sl[:, k - 1]                      # UhB_k
-        for i, t in enumerate(self._tw_cand):
-            self._tw_Mi[c0:c1, i] = inv(Sd[:, t] - Sl[:, t - 1] @ Uh[:, t - 1] - Su[:, t] @ Eub[c0:c1, t])
-            self._tw_Db[c0:c1, i] = Edb[c0:c1, t]                      # (unset for t = lo: no chain meets below it)
-
-    def _set_edge_sweep(self, t):
-        """Edge sweep of the following solves: two-ended meeting at candidate edge t, or one-ended (t None)."""
-        Edb = self._Etw[1]
-        for i, c in enumerate(self._tw_cand):
-            Edb[:, c] = self._tw_Db[:, i]
-        if t is not None:
-            Edb[:, t] = self._tw_Mi[:, self._tw_cand.index(t)]
-        self._edge_twisted, self._edge_mid = t is not None, (0 if t is None else t)
-        self._nd = None                                                 # the descriptor carries the sweep
-
-    def _select_edge_sweep(self, probe, slack=1.5, floor=1e-15, nprobe=4):
-        """Block elimination without inter-block pivoting multiplies rounding by its multipliers, and the two chains
-        of a two-ended sweep meet different Schur complements: at P = 16, 2 x 6 elements, Re = 300 the chain from the
-        bottom meets a nearly singular one at edge 4 (||Db_4|| = 600; <= 10 from the top), and meeting at the middle
-        edge 3 gave 180x the one-ended sweep's backward error; at P = 7, 2 x 8, Re = 200 meeting at edge 4 is ~7x
-        worse on most right-hand sides.  Neither the multipliers nor one random probe predict that reliably (two
-        elimination orders differ by 0.3-7x on any single right-hand side), so the candidates are judged on
-        `nprobe` probe right-hand sides: the first of (middle, middle + 1, middle - 1) whose worst probe backward
-        error is within `slack` of the one-ended sweep's worst, or below `floor` (SuperLU's class), is kept; else
-        the one-ended sweep.  Returns the kept sweep's worst probe error.  Every rank of a partition takes the same
-        decisions (the probe's norms are reduced over the ranks)."""
-        if getattr(self, "_tw_done", False):   # judged at an earlier probe: keep that sweep
-            return probe(0)
-        self._tw_done = True
-        ready = getattr(self, "_tw_ready", False) and self._Etw is not None
-        ready = self._amax(torch.tensor([0.0 if ready else 1.0], dtype=torch.float64, device=self.device)) == 0.0
-        if not ready:
-            self._edge_twisted, self._edge_mid = False, 0
-            eta = probe(0)
-            self._tw_eta = {"one-ended": eta}
-            return eta
-        self._set_edge_sweep(None)
-        eta1 = max(probe(k) for k in range(nprobe))
-        bar = max(slack * eta1, floor)
-        self._tw_eta = {"one-ended": eta1}
-        best = None
-        for t in self._tw_cand:
-            self._set_edge_sweep(t)
-            eta = 0.0
-            for k in range(nprobe):   # stop at the first probe past the bar
-                eta = max(eta, probe(k))
-                if eta > bar:
-                    break
-            self._tw_eta[t] = eta
-            if eta <= bar:
-                best = (t, eta)
-                break
-        self._set_edge_sweep(None if best is None else best[0])
-        self._tw_Mi = self._tw_Db = None
-        return eta1 if best is None else best[1]
-
-    def _edge_twisted_solve(self, Re, cols=slice(None)):
-        """S_e^-1 Re by the two-ended sweep (the torch form of cond_edge_twisted_kernel): chains from edge 0 and
-        from edge N_ey, the meeting block at edge mid, back substitution outwards."""
-        Ed, El, Eu = self._Ed[cols], self._El[cols], self._Eu[cols]
-        Es, Edb, Eub = (t[cols] for t in self._Etw)
-        nex, nb, b = Ed.shape[0], Ed.shape[1], Ed.shape[2]
-        t = self._edge_mid
-        R = Re.view(nex, nb, b, -1)
-        Z = torch.empty_like(R)
-        Z[:, 0] = Ed[:, 0] @ R[:, 0]
-        for k in range(1, t):
-            Z[:, k] = Ed[:, k] @ (R[:, k] - El[:, k - 1] @ Z[:, k - 1])
-        Z[:, nb - 1] = Edb[:, nb - 1] @ R[:, nb - 1]
-        for k in range(nb - 2, t, -1):
-            Z[:, k] = Edb[:, k] @ (R[:, k] - Es[:, k] @ Z[:, k + 1])
-        Z[:, t] = Edb[:, t] @ (R[:, t] - El[:, t - 1] @ Z[:, t - 1] - Es[:, t] @ Z[:, t + 1])
-        for k in range(t - 1, -1, -1):
-            Z[:, k] -= Eu[:, k] @ Z[:, k + 1]
-        for k in range(t + 1, nb):
-            Z[:, k] -= Eub[:, k - 1] @ Z[:, k - 1]
-        return Z.view(Re.shape)
 
     def _blocktri_inverse(self, Sd, Su, Sl, factors=False):
         """Dense inverse of block-tridiagonal matrices (batched over columns): diagonal blocks Sd (cc, nb, b, b),
@@ -874,8 +751,7 @@ class VelocityJacobianSolver:
         if self._hipT is not None:
             self._hipT = self._hipT[:3] + (SeT,)
         self._edge_thomas = False
-        self._edge_twisted = self._tw_ready = False
-        self._Ed = self._El = self._Eu = self._EtT = self._Etw = None
+        self._Ed = self._El = self._Eu = self._EtT = None
 
     @staticmethod
     def _blocktri_dense(Sd, Su, Sl):
@@ -1130,7 +1006,7 @@ class VelocityJacobianSolver:
         Rv[:, :-1] -= Cn[:, :, :ne1]
         Rv[:, 1:] -= Cn[:, :, ne1:]
         if self._edge_thomas:
-            Ye = (self._edge_twisted_solve if self._edge_twisted else self._edge_thomas_solve)(Re, cols)
+            Ye = self._edge_thomas_solve(Re, cols)
         else:
             Ye = self._Se_inv[cols] @ Re                                # (nex, n_e, k)
         Yv = Ye.view(nex, ney + 1, ne1, k)
@@ -1161,7 +1037,7 @@ class VelocityJacobianSolver:
             nex, ney, P, m = self.nex, self.ney, self.P, self.m
             ni, ne1 = self._pi.shape[1], self._ne1
             z = dict(dtype=torch.float64, device=self.device)
-            if getattr(self, "_work", None) is None:   # kept when only the descriptor is rebuilt (_set_edge_sweep)
+            if getattr(self, "_work", None) is None:
                 self._work = (torch.empty(nex * ney * ni, **z), torch.empty(nex * ney * 2 * ne1, **z),
                               torch.empty(nex * (ney + 1) * ne1, **z), torch.empty((nex, self.nI), **z),
                               torch.empty((nex + 1, m), **z), torch.empty(nex * 2 * m, **z))
@@ -1177,11 +1053,9 @@ class VelocityJacobianSolver:
                     raise RuntimeError("nested solve: edge offsets differ from the block-Thomas sweep's layout")
             q = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
             hb = self._hipB if getattr(self, "_hipB", None) is not None else (None, None, None)
-            tw = self._Etw if (self._edge_thomas and getattr(self, "_edge_twisted", False)) else (None, None, None)
             self._nd = _lib.SemNestedDesc(P, nex, ney, self.ncomp, self.NY, p(XiT), p(AeiT), p(YieT), q(SeT),
                                           p(self._pi), p(self._pe), p(T), p(Cw), p(Ye), *(q(t) for t in Et),
-                                          *(q(t) for t in hb), p(Pw), *(q(t) for t in tw),
-                                          self._edge_mid if tw[0] is not None else 0)
+                                          *(q(t) for t in hb), p(Pw))
         return self._nd
 
     def _own_rhs(self, g, B):
@@ -1254,9 +1128,9 @@ class VelocityJacobianSolver:
         """Measure the factor's normwise backward error eta = ||J x - b|| / (||J|| ||x|| + ||b||) (max norms) on a
         seeded probe, ||J|| estimated from below by ||J s|| for a random sign vector s (so eta is over-estimated),
         and turn on one refinement step per solve when eta > tau (SEM_REFINE_ETA, default 1e-13; 0 refines
-        always, inf never).  With the opt-in two-ended edge sweep factored, the same probe first picks the edge
-        sweep (_select_edge_sweep) and eta is the kept sweep's.  Every part of a partitioned solve takes the same
-        decisions (reduced norms).  Returns eta."""
+        always, inf never).  Every part of a partitioned solve takes the same decisions (reduced norms).  A
+        non-finite eta (a singular or overflowing factor block) raises RuntimeError instead of passing as "no
+        refinement needed" (max(0, nan) is 0).  Returns eta."""
         if self._apply is None:
             raise RuntimeError("set_operator() first")
         if tau is None:
@@ -1281,7 +1155,10 @@ class VelocityJacobianSolver:
             x = self._solve_lines(bk)
             return self._amax(bk - self._apply(x)) / (nJ * self._amax(x) + self._amax(bk))
 
-        eta = self._select_edge_sweep(probe)
+        eta = probe(0)
+        if not math.isfinite(eta):
+            raise RuntimeError(f"velocity factor: non-finite backward error on the probe ({eta}): a singular or "
+                               "overflowing pivot block")
         self.refine_eta = eta
         self.refine = eta > tau
         return eta

@@ -62,7 +62,7 @@ def test_sweeps_refuse_other_dtypes(gpu):
 
 
 def test_tuning_knobs_do_not_change_results(gpu, tuning):
-    """Every knob value selects a variant with bitwise-identical results."""
+    """Every band-kernel knob value selects a variant with bitwise-identical results; retired knobs are refused."""
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     mesh = get_mesh(8, 20, 17, 1 / 20, 1 / 17)
@@ -71,8 +71,7 @@ def test_tuning_knobs_do_not_change_results(gpu, tuning):
     kw = dict(c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, dir_mode=_lib.DIR_IDENTITY,
               dir_sides=_lib.SIDE_W | _lib.SIDE_E)
     base = mesh.apply(X, **kw)
-    for knob, vals in ((_lib.TUNE_BAND_CPOL, (1, 2, 3, 4, 256)), (_lib.TUNE_BAND_KP, (-1, 0)),
-                       (_lib.TUNE_BAND_TILE, (1, 2, 3, 4, 5, 6, 7, 8, 9))):
+    for knob, vals in ((_lib.TUNE_BAND_KP, (-1, 0)), (_lib.TUNE_BAND_TILE, (3, 4))):
         for v in vals:
             tuning(knob, v)
             assert torch.equal(mesh.apply(X, **kw), base), (knob, v)

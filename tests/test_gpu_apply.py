@@ -72,9 +72,8 @@ CASES = [(1, 3, 2), (2, 5, 3), (3, 4, 7), (4, 1, 1), (5, 2, 9), (6, 3, 3), (7, 4
 
 # VALU two-phase, MFMA (band form, round 5), column kernel, assembled band (+ DPP coefficient variant), and the
 # element-block MFMA kernel of rounds 1-4 ("2eb": SEM_MFMA_TILE = 3)
-ALGOS = [1, 2, 3, 4, "4dpp", "4m", "4mdpp", "4smem", "2eb"]
-BAND_VARIANTS = {"4dpp": "3", "4t1": "1", "4t2": "2", "4t5": "5", "4t6": "6", "4imm": "4",
-                 "4m": "7", "4mdpp": "8", "4smem": "9"}  # 4m*: marching kernel (P = 8, 12; other P fall back to the band tile)  # SEM_TUNE_BAND_TILE values
+ALGOS = [1, 2, 3, 4, "4dpp", "4imm", "2eb"]
+BAND_VARIANTS = {"4dpp": "3", "4imm": "4"}  # SEM_TUNE_BAND_TILE values: DPP-broadcast / immediate coefficients
 
 
 def _algo(algo, tuning):
@@ -172,8 +171,8 @@ def test_large_tiles_vs_oracle(gpu, P, nex, ney, algo, tuning):
 
 @pytest.mark.parametrize("P,nex,ney", [(P, 7, 5) for P in range(1, 17)] + [(8, 64, 64), (8, 3, 70)])
 def test_band_variants_bitwise_equal(gpu, P, nex, ney, tuning):
-    """Band kernel variants (DPP-broadcast coefficients, other tile shapes) perform the same
-    operations in the same order as the default: results are bitwise identical."""
+    """The band kernel's coefficient modes (DPP-broadcast lists, fp64 immediates) perform the same operations in
+    the same order: results are bitwise identical."""
     from sem_amd import _lib
     from sem_amd.device import get_mesh
     mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.5 / ney)
@@ -183,8 +182,7 @@ def test_band_variants_bitwise_equal(gpu, P, nex, ney, tuning):
               dir_sides=_lib.SIDE_W | _lib.SIDE_E, algo=4)
     tuning(_lib.TUNE_BAND_TILE, 0)
     base = mesh.apply(X, **kw)
-    for name in (["4dpp", "4imm", "4t1", "4t2", "4t5", "4t6", "4m", "4mdpp", "4smem"] if P in (8, 12)
-                 else ["4dpp", "4imm", "4smem"]):
+    for name in ("4dpp", "4imm"):
         tuning(_lib.TUNE_BAND_TILE, BAND_VARIANTS[name])
         assert torch.equal(mesh.apply(X, **kw), base), name
 
@@ -218,34 +216,6 @@ def test_band_kernarg_forms_bitwise_equal(gpu, P, nex, ney, eb, ee, full, tuning
     a0 = mesh.apply(X, **kw0)
     tuning(_lib.TUNE_BAND_KP, 0)
     assert torch.equal(mesh.apply(X, **kw0), a0)
-
-
-@pytest.mark.parametrize("P,nex,ney,eb,ee,wg", [(8, 40, 13, 0, 40, 64), (8, 40, 13, 10, 30, 64), (8, 40, 13, 0, 17, 8),
-                                               (12, 9, 21, 3, 9, 32), (8, 33, 64, 0, 33, 1024), (8, 5, 3, 2, 3, 64)])
-@pytest.mark.parametrize("full", [False, True])
-def test_march_bitwise_equal_band(gpu, P, nex, ney, eb, ee, wg, full, tuning):
-    """The marching kernel (LDS ring of staged lines, chunks of element positions per workgroup)
-    reproduces the band kernel bitwise: strips, chunk boundaries, ghost positions, and the
-    FULL path (extra pairs, accumulate, explicit Dirichlet mask and values)."""
-    from sem_amd import _lib
-    from sem_amd.device import get_mesh
-    mesh = get_mesh(P, nex, ney, 1.0 / nex, 1.5 / ney, eb, ee)
-    r = np.random.default_rng(nex * 100 + eb)
-    N = mesh.n_local
-    X, U, V, A, B, Y0, G = (mesh.to_device(r.uniform(-1, 1, N)) for _ in range(7))
-    kw = dict(c_mass=0.25, c_stiff=1.0, c_gradx=40.0, cu=U, c_grady=40.0, cv=V, algo=4)
-    if full:
-        mask = mesh.to_device((r.uniform(0, 1, N) < 0.1).astype(np.uint8), dtype=torch.uint8)
-        kw.update(c_extra=3.0, ea=A, eb=B, c_acc=2.0, dir_mode=_lib.DIR_IDENTITY, dir_mask=mask, dir_val=G)
-    else:
-        kw.update(dir_mode=_lib.DIR_IDENTITY, dir_sides=_lib.SIDE_W | _lib.SIDE_E | _lib.SIDE_N)
-    tuning(_lib.TUNE_MARCH_WG, wg)
-    outs = {}
-    for name in ("4imm", "4m", "4mdpp"):
-        tuning(_lib.TUNE_BAND_TILE, BAND_VARIANTS[name])
-        outs[name] = mesh.apply(X, Y0.clone(), **kw)
-    assert torch.equal(outs["4m"], outs["4imm"])
-    assert torch.equal(outs["4mdpp"], outs["4imm"])
 
 
 @pytest.mark.parametrize("key", ["P4_4x4", "P4_3x2", "P8_8x8", "P12_5x3"])

@@ -247,7 +247,7 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
     kw = dict(juu=ns._Jac_u_u._coeffs()[4], juv=ns._Jac_u_v._coeffs()[4], jvu=ns._Jac_v_u._coeffs()[4],
               jvv=ns._Jac_v_v._coeffs()[4], dir_mask=ns._dir.mask, dir_sides=ns._dir.sides, **ns._sys_kw(ns._Sys))
     ch = VelocityJacobianSolver(P, nex, ney, ns._mesh.device)
-    ch.edge_dense_max, ch.edge_solve, ch.edge_two_ended = 0, "auto", "auto"   # the two-ended sweep is opt-in
+    ch.edge_dense_max, ch.edge_solve = 0, "auto"
     ch.factor_mesh(ns._mesh, budget_bytes=1, **kw)
     assert ch._edge_thomas
     ch.set_operator(ns._velocity_apply_lines)
@@ -268,41 +268,13 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
             _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
         return out
 
-    # ABI 12: the factor's probe (check_refinement) picks the edge sweep: two-ended, meeting at the first of the middle
-    # edge and its neighbours whose worst backward error over 4 probes is within 1.5x of the one-ended sweep's worst
-    # (or below 1e-15), else one-ended
-    # (VelocityJacobianSolver._select_edge_sweep: P = 16, 2 x 6 elements meets at edge 4, not 3); knob 2 forces the
-    # one-ended templated sweep
-    assert not ch._edge_twisted
     eta0 = ch.check_refinement()
-    print(f"edge sweep probe {ch._tw_eta}: meeting edge {ch._edge_mid}")
-    if ney + 1 >= 3:
-        bar = max(1.5 * ch._tw_eta["one-ended"], 1e-15)
-        assert ch._edge_twisted == any(k != "one-ended" and v <= bar for k, v in ch._tw_eta.items())
-    # two elimination orders: on one right-hand side their backward errors differ by 0.3x - 7x either way (CPU, 20
-    # draws per mesh), so the bar is over 16 draws: the worst two-ended error within 2x of the worst one-ended one
-    e_tw, e_one = [], []
-    for sd in range(16):
-        rr = np.random.default_rng(100 + sd)
-        cu, cv = ns._dev(rr.uniform(-1, 1, ns.N)), ns._dev(rr.uniform(-1, 1, ns.N))
-        cb = np.hstack((cu.cpu().numpy(), cv.cpu().numpy()))
-        try:
-            for k, acc in ((0, e_tw), (2, e_one)):
-                _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, k))
-                acc.append(_eta(J, torch.cat(ch.solve(cu, cv)), cb))
-        finally:
-            _lib.check(lib.sem_set_tuning(_lib.TUNE_EDGE_THOMAS, 0))
-    print(f"over 16 right-hand sides: two-ended edge sweep worst {max(e_tw):.1e} median {np.median(e_tw):.1e}, "
-          f"one-ended worst {max(e_one):.1e} median {np.median(e_one):.1e}")
-    assert max(e_tw) <= 2 * max(e_one) + 1e-15
-    # the one-ended templated sweep (knob 2) against the ABI-9 sweep (knob 1): one factor, one elimination order
-    x_new, x_old = both(False, first=2)
+    # the templated sweep (default) against the ABI-9 sweep (knob 1): one factor, one elimination order
+    x_new, x_old = both(False)
     e_new, e_old, e_lu = _eta(J, x_new, bb), _eta(J, x_old, bb), _eta(J, spla.spsolve(J.tocsc(), bb), bb)
-    f_new, f_old = both(True, first=2)
+    f_new, f_old = both(True)
     g_new, g_old = _eta(J, f_new, bb), _eta(J, f_old, bb)
-    mid = ch._edge_mid
-    eta = ch.check_refinement()                                    # a second probe keeps the chosen sweep
-    assert ch._edge_mid == mid
+    eta = ch.check_refinement()
     x_s = torch.cat(ch.solve(bu, bv))
     e_s = _eta(J, x_s, bb)
     print(f"velocity pair, block width {ch._ne1}: backward error templated {e_new:.1e} / ABI-9 {e_old:.1e} / SuperLU "
@@ -383,10 +355,10 @@ def test_gemv_rows_matches_torch(gpu, M, K, lda, alpha, beta):
 
 
 @pytest.mark.parametrize("M,K", [(3074, 6148), (1537, 3074), (13, 130), (7, 2), (770, 1540)])
-def test_gemv_rows_shapes_and_load_policy_bitwise(gpu, M, K):
-    """The rows-per-workgroup x loads-in-flight variants of sem_gemv_rows (SEM_TUNE_GEMV_SHAPE) and both load
-    policies (non-temporal default, SEM_TUNE_GEMV_CPOL = 2 plain) give the same bits: the variants change neither
-    a lane's column order nor the order in which the waves' sums meet; likewise sem_gemv_rows2."""
+def test_gemv_rows_matches_torch(gpu, M, K):
+    """sem_gemv_rows (2 rows per workgroup x 8 loads in flight, non-temporal operator loads: the shape and policy
+    the round-5 A/B kept; the other variants were retired in round 6) against torch's GEMV, and sem_gemv_rows2's
+    first half bit for bit against the single call."""
     import ctypes as C
     from sem_amd import _lib
     lib = _lib.load()
@@ -398,27 +370,13 @@ def test_gemv_rows_shapes_and_load_policy_bitwise(gpu, M, K):
     y0 = torch.as_tensor(r.uniform(-1, 1, M), device=dev)
     P_ = C.c_void_p
     st = P_(torch.cuda.current_stream().cuda_stream)
-    outs = []
-    try:
-        for shape in range(int(os.environ.get("SEM_TEST_GEMV_SHAPES", "8"))):
-            for cpol in (0, 2):
-                _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_SHAPE, shape))
-                _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_CPOL, cpol))
-                y, z = y0.clone(), y0.clone()
-                _lib.check(lib.sem_gemv_rows(M, K, -1.0, P_(A.data_ptr()), K, P_(x.data_ptr()), 1.0, P_(y.data_ptr()),
-                                             st))
-                _lib.check(lib.sem_gemv_rows2(M, -1.0, 1.0, K, P_(A.data_ptr()), K, P_(x.data_ptr()),
-                                              P_(z.data_ptr()), K, P_(B.data_ptr()), K, P_(x.data_ptr()),
-                                              P_(y0.clone().data_ptr()), st))
-                outs.append((y, z))
-    finally:
-        _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_SHAPE, 0))
-        _lib.check(lib.sem_set_tuning(_lib.TUNE_GEMV_CPOL, 0))
-    for y, z in outs[1:]:
-        assert torch.equal(y, outs[0][0]) and torch.equal(z, outs[0][1])
-    assert torch.equal(outs[0][0], outs[0][1])          # the dual launch's first half is the single call's bits
+    y, z = y0.clone(), y0.clone()
+    _lib.check(lib.sem_gemv_rows(M, K, -1.0, P_(A.data_ptr()), K, P_(x.data_ptr()), 1.0, P_(y.data_ptr()), st))
+    _lib.check(lib.sem_gemv_rows2(M, -1.0, 1.0, K, P_(A.data_ptr()), K, P_(x.data_ptr()), P_(z.data_ptr()), K,
+                                  P_(B.data_ptr()), K, P_(x.data_ptr()), P_(y0.clone().data_ptr()), st))
+    assert torch.equal(y, z)          # the dual launch's first half is the single call's bits
     want = y0 - A @ x
-    assert (outs[0][0] - want).abs().max().item() <= 1e-13 * max(1.0, want.abs().max().item()) * np.sqrt(K)
+    assert (y - want).abs().max().item() <= 1e-13 * max(1.0, want.abs().max().item()) * np.sqrt(K)
 
 
 @pytest.mark.parametrize("M,K0,K1,odd", [(3074, 6148, 6148, False), (3074, 3074, 3074, False), (1537, 3074, 1537, True),

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(_lib.exported_symbols()) == declared
-    assert lib.sem_abi_version() == _lib.ABI_VERSION == 12
+    assert lib.sem_abi_version() == _lib.ABI_VERSION == 13
     assert lib.sem_max_order() == 16
 
 
@@ -128,6 +128,8 @@ def test_tuning_knobs_set_and_get():
     assert v.value == 3
     _lib.check(lib.sem_set_tuning(_lib.TUNE_BAND_TILE, old))
     assert lib.sem_set_tuning(99, 1) == _lib.SEM_EINVAL
+    for knob in _lib.TUNE_RETIRED:           # round 6: the knobs whose A/B lost are refused
+        assert lib.sem_set_tuning(knob, 1) == _lib.SEM_EINVAL
     assert lib.sem_get_tuning(-1, C.byref(v)) == _lib.SEM_EINVAL
 
 

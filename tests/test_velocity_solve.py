@@ -190,61 +190,3 @@ def test_twisted_thomas_matches_dense_solve(n, m):
             Uh[L] = Dinv[L] @ Su[L]
     one = fused_thomas_solve(*fused_thomas_operators(Dinv, Sl, Uh), rhs)
     assert (got - one).abs().max().item() <= 1e-12 * want.abs().max().item()
-
-
-@pytest.mark.parametrize("P,nex,ney,Re,mid", [(16, 2, 6, 300.0, 4), (5, 4, 7, 400.0, None), (4, 3, 2, 100.0, 1),
-                                              (12, 2, 5, 100.0, 3), (12, 2, 12, 1000.0, None)])
-def test_two_ended_edge_sweep(P, nex, ney, Re, mid):
-    """ABI 12's two-ended edge sweep in its torch form (the kernel's arithmetic) solves the Jacobian as the one-ended
-    sweep does.  The sweep is chosen by the solver's backward-error probe (check_refinement): the first of the
-    middle edge and its two neighbours whose worst error over 4 probe right-hand sides is within 1.5x of the
-    one-ended sweep's worst (or below 1e-15).  At P = 16,
-    2 x 6 elements, Re = 300 the chain from the bottom meets a nearly singular Schur complement at edge 4
-    (||Db_4|| ~ 600): meeting at the middle edge 3 multiplies the error ~100x, so the probe moves the meeting to
-    edge 4.  (12, 2, 5): edge 2 has the smallest multipliers yet 10x the error on solve right-hand sides -- the
-    reason the choice is the probe's, not a multiplier score's.)"""
-    ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex + ney)
-    pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
-    r = np.random.default_rng(9)
-    bu, bv = (torch.as_tensor(r.uniform(-1, 1, ns.N)) for _ in range(2))
-    b = np.hstack((bu.numpy(), bv.numpy()))
-    J = ns.Jvelo
-    NX = nex * P + 1
-
-    def apply_lines(X):   # J X on (NX, 2 NY) line arrays (every line: u then v)
-        X3 = X.view(NX, 2, -1)
-        y = J @ np.hstack((X3[:, 0].reshape(-1).numpy(), X3[:, 1].reshape(-1).numpy()))
-        Y = torch.as_tensor(y).view(2, NX, -1)
-        return torch.stack((Y[0], Y[1]), dim=1).reshape(X.shape)
-
-    def run(two):
-        ch = VelocityJacobianSolver(P, nex, ney, "cpu")
-        cond = ch.condense_dense(pcs["AII"])
-
-        def fill(blocks, cols):
-            c0, c1 = cols
-            for k in ("D", "aIB", "aBI", "E", "F"):
-                blocks[k].copy_(pcs[k])
-            for k, v in cond.items():
-                blocks[k].copy_(v[c0:c1])
-
-        ch.edge_dense_max, ch.edge_solve, ch.edge_two_ended = 0, "thomas", two
-        ch.factor_condensed(fill, chunk_cols=1)
-        assert not ch._edge_twisted                       # one-ended until the probe has judged the candidates
-        ch.set_operator(apply_lines)
-        ch.check_refinement(tau=float("inf"))
-        x = np.hstack([t.numpy() for t in ch.solve(bu, bv)])
-        return ch, x, np.abs(J @ x - b).max() / (abs(J).sum(1).max() * np.abs(x).max() + np.abs(b).max())
-
-    one, x1, e1 = run(False)
-    two, x2, e2 = run(True)
-    print(f"probe eta {two._tw_eta}, meeting edge {two._edge_mid}; solve eta {e2:.1e} (one-ended {e1:.1e})")
-    assert not one._edge_twisted and two._tw_eta["one-ended"] >= one.refine_eta   # worst of 4 probes vs probe 0
-    assert two._edge_twisted == (mid is not None or two._edge_mid != 0)
-    if mid is not None:
-        assert two._edge_twisted and two._edge_mid == mid
-    if (P, ney) == (16, 6):
-        assert two._tw_eta[3] > 30 * two._tw_eta["one-ended"]   # the middle edge: the bottom chain's large pivot
-    want = spla.spsolve(J.tocsc(), b)
-    assert np.abs(x2 - want).max() <= 1e-10 * np.abs(want).max()
-    assert e2 <= 4 * e1 + 1e-15

@@ -29,9 +29,8 @@ def main():
     from sem_amd.device import get_mesh
     vals = args.values.split(",")
     lib = _lib.load()
-    knob = {"SEM_BAND_TILE": _lib.TUNE_BAND_TILE, "SEM_BAND_CPOL": _lib.TUNE_BAND_CPOL, "SEM_BAND_KP": _lib.TUNE_BAND_KP,
-            "SEM_MARCH_WG": _lib.TUNE_MARCH_WG, "SEM_MFMA_TILE": _lib.TUNE_MFMA_TILE,
-            "SEM_COL_TILE": _lib.TUNE_COL_TILE}[args.var]
+    knob = {"SEM_BAND_TILE": _lib.TUNE_BAND_TILE, "SEM_BAND_KP": _lib.TUNE_BAND_KP,
+            "SEM_MFMA_TILE": _lib.TUNE_MFMA_TILE}[args.var]
     for spec in args.meshes.split(","):
         P, ne = (int(a) for a in spec.split(":"))
         mesh = get_mesh(P, ne, ne, 1.0 / ne, 1.0 / ne)

@@ -193,8 +193,6 @@ def rehearsal(args):
     torch.cuda.synchronize(dev)
     rec["factor_s"] = time.perf_counter() - t0
     rec["refine"], rec["refine_eta"] = bool(vs.refine), vs.refine_eta
-    rec["edge_sweep"] = {"two_ended": bool(vs._edge_twisted), "meeting_edge": vs._edge_mid,
-                         "probe_eta": {str(k): v for k, v in getattr(vs, "_tw_eta", {}).items()}}
     say(f"factor {rec['factor_s']:.2f} s, backward error {vs.refine_eta:.1e}, refine {vs.refine}")
     for k in list(stats):
         stats[k][:] = [0, 0, 0.0]
@@ -316,7 +314,6 @@ def solo(args):
         # large backward error and switched refinement on, doubling every solve): time the plain solve, as a real
         # partition whose gate passes runs it
         rec["refine_eta_loopback"] = vs.refine_eta
-        rec["edge_sweep"] = {"two_ended": bool(vs._edge_twisted), "meeting_edge": vs._edge_mid}
         vs.refine = False
         rec["twisted_interior"] = vs._T is not None and vs._T[0][0] == "twisted"
         fake.calls.clear()
