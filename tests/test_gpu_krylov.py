@@ -119,3 +119,27 @@ def test_segmented_dot2_matches_masked_products(gpu):
         S = _DeviceSweeps(V, segs).dot2(k, a, b)
         want = torch.stack((V[:k] @ (a * own), V[:k] @ (b * own)), dim=1)
         assert (S - want).abs().max().item() <= 1e-12
+
+
+@pytest.mark.parametrize("eta", [1e-4, 2.0])
+def test_segmented_pipelined_gmres_matches_plain(gpu, monkeypatch, eta):
+    """the partitioned Krylov path -- GMRES on owned segments through DistributedInner, its reduce on the
+    device (no host staging, so the pipelined step runs) -- against plain GMRES on the same system, with and without
+    the forced reorthogonalisation (REORTH_ETA = 2).  One rank and segments covering the whole vector: the
+    partitioned arithmetic must give plain GMRES's iterations and x to rounding."""
+    import sem_amd.krylov as K
+    from sem_amd.parallel import DistributedInner
+    A, b = _cd_like(600, 13)
+    d = 1.0 / torch.diagonal(A)
+    n = b.numel()
+    monkeypatch.setattr(K, "REORTH_ETA", eta)
+    inner = DistributedInner(None, (n, "cuda"), None, segments=[(0, 250), (250, 600)])
+    assert inner.bdev is None            # no host staging: the pipelined step is taken
+    ref = K.gmres(lambda v: A @ v, b, atol=1e-10, restart=300, maxiter=2000, precond=lambda v: d * v)
+    got = K.gmres(lambda v: A @ v, b, atol=1e-10, restart=300, maxiter=2000, precond=lambda v: d * v, inner=inner)
+    assert ref.info == 0 and got.info == 0
+    assert abs(got.iters - ref.iters) <= 1
+    assert got.discarded >= 1            # the pipeline ran (its speculation past convergence was dropped)
+    assert (got.x - ref.x).abs().max().item() < 1e-9
+    if eta > 1:
+        assert got.reorth >= got.iters - 1

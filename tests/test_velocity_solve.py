@@ -190,3 +190,34 @@ def test_twisted_thomas_matches_dense_solve(n, m):
             Uh[L] = Dinv[L] @ Su[L]
     one = fused_thomas_solve(*fused_thomas_operators(Dinv, Sl, Uh), rhs)
     assert (got - one).abs().max().item() <= 1e-12 * want.abs().max().item()
+
+
+def test_refinement_gate_rejects_a_non_finite_factor():
+    """a singular or overflowing factor makes the probe's backward error NaN, and max(0, nan) is 0 in
+    Python -- the gate must raise instead of reading it as "no refinement needed".  (A singular interior block is
+    caught earlier, by the factor's own inverse check; the probe's last line of defence is exercised with an
+    operator that returns NaN.)"""
+    P, nex, ney, Re = 4, 3, 2, 100.0
+    ns, _, _ = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
+    pcs = {k: torch.as_tensor(v) for k, v in extract(ns.Jvelo.toarray(), P, nex, ney).items()}
+    J = ns.Jvelo
+    NX = nex * P + 1
+
+    def apply_lines(X):
+        X3 = X.view(NX, 2, -1)
+        y = J @ np.hstack((X3[:, 0].reshape(-1).numpy(), X3[:, 1].reshape(-1).numpy()))
+        Y = torch.as_tensor(y).view(2, NX, -1)
+        return torch.stack((Y[0], Y[1]), dim=1).reshape(X.shape)
+
+    vs = VelocityJacobianSolver(P, nex, ney, "cpu", interior="inverse", sweep="thomas")
+    vs.factor(pcs["AII"], pcs["D"], pcs["aIB"], pcs["aBI"], pcs["E"], pcs["F"])
+    vs.set_operator(apply_lines)
+    assert vs.check_refinement() < 1e-13               # the healthy factor passes
+    A = pcs["AII"].clone()
+    A[1] = 0.0
+    with pytest.raises(RuntimeError):                   # a singular interior block: refused at factor time
+        VelocityJacobianSolver(P, nex, ney, "cpu", interior="inverse", sweep="thomas").factor(
+            A, pcs["D"], pcs["aIB"], pcs["aBI"], pcs["E"], pcs["F"])
+    vs.set_operator(lambda X: apply_lines(X) * float("nan"))
+    with pytest.raises(RuntimeError, match="non-finite"):
+        vs.check_refinement()

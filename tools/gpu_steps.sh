@@ -219,12 +219,16 @@ for s in "$@"; do
     cfg4a)      # BASELINE cfg4 end to end, part 1: Ra 1e3 -> 1e4 -> 1e5 -> 3e5 from rest, checkpointed
       step cfg4a 1150 python -u tools/bous_solve.py --ne 48 --P 8 --continuation 1e3,1e4,1e5 --Ra 3e5 --iprint 2 \
         --ckpt "$O/ckpt" --out "$O/cfg4_to3e5.json" ;;
-    cfg4b)      # part 2: Ra = 1e6 from the Ra = 3e5 state (ckpt/bous_48_300000.npy, copied into the tree)
-      step cfg4b 1150 python -u tools/bous_solve.py --ne 48 --P 8 --Ra 1e6 --x0 ckpt/bous_48_300000.npy --iprint 2 \
+    cfg4b)      # part 2: Ra = 1e6 from the Ra = 3e5 state cfg4a wrote to $O/ckpt (ckpt/ is ignored by git
+                # and gpurun, so the start state must come from this session's own cfg4a step); its sha256 goes
+                # into the step log for the record
+      sha256sum "$O/ckpt/bous_48_300000.npy" | tee -a "$O/cfg4_provenance.txt"
+      step cfg4b 1150 python -u tools/bous_solve.py --ne 48 --P 8 --Ra 1e6 --x0 "$O/ckpt/bous_48_300000.npy" --iprint 2 \
         --ckpt "$O/ckpt" --out "$O/cfg4_ra1e6.json" ;;
-    cfg4c)      # part 3 (if part 2 hit its limit): Ra = 1e6 resumed from the last Newton checkpoint
-      step cfg4c 1150 python -u tools/bous_solve.py --ne 48 --P 8 --Ra 1e6 --x0 ckpt/bous_48_1e+06_newton.npy --resume 1 \
-        --iprint 2 --ckpt "$O/ckpt" --out "$O/cfg4_ra1e6_resumed.json" ;;
+    cfg4c)      # part 3 (if part 2 hit its limit): Ra = 1e6 resumed from part 2's last Newton checkpoint in $O/ckpt
+      sha256sum "$O/ckpt/bous_48_1e+06_newton.npy" | tee -a "$O/cfg4_provenance.txt"
+      step cfg4c 1150 python -u tools/bous_solve.py --ne 48 --P 8 --Ra 1e6 --x0 "$O/ckpt/bous_48_1e+06_newton.npy" \
+        --resume 1 --iprint 2 --ckpt "$O/ckpt" --out "$O/cfg4_ra1e6_resumed.json" ;;
     bmfma)      # band-form MFMA kernel (round 5): parity, then A/B against the band VALU kernel and the element-block
                 # MFMA kernel of rounds 1-4 (SEM_MFMA_TILE=3), and the counter passes of the new kernel at cfg2
       step bmfmatests 900 $PYT tests/test_gpu_apply.py tests/test_gpu_partition.py
