@@ -917,8 +917,23 @@ __device__ const typename BMTab<P>::Tab kBMTab = BMTab<P>::make();
 template <int P, bool FULL, bool GRAD>
 __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs a) {
   using C = BMCfg<P>;
-  __shared__ double Ts[C::SL * C::PT];
-  __shared__ double ws[P + 1];   // GLL weights: one LDS read per node instead of a compare-select chain per weight
+  constexpr int NW = C::NB, PT = C::PT;
+  constexpr int NTAB = (GRAD ? 2 : 1) * 16 * C::KW;                 // operand table [K | G][i][k] (global, dense)
+  // its LDS copy: row pitch AP = 2 (mod 32) doubles, so a half-wave's reads (rows lr = 0..15, entries lk = 0, 1)
+  // fall on 32 distinct 2-bank slots -- the dense pitch KW = 28 put rows lr and lr + 8 on one bank (2-way conflicts:
+  // 45.5 M conflict cycles per 1024^2 launch, profiles/r06/mfma)
+  constexpr int AP = (C::KW + 29) / 32 * 32 + 2 >= C::KW ? (C::KW + 29) / 32 * 32 + 2 : (C::KW + 29) / 32 * 32 + 34;
+  constexpr int NAP = (GRAD ? 2 : 1) * 16 * AP;
+  constexpr int NAB = (NTAB + C::THREADS - 1) / C::THREADS;
+  // staging (round 6, as the band kernel): wave w stages window lines w + NW k (lanes = columns 0..63) and the
+  // columns 64..SC-1 of its lines in NXL more loads; absent columns / lines load 0 through out-of-range offsets
+  constexpr int NSL = (C::SL + NW - 1) / NW, SCX = C::SC - 64, NXL = SCX > 0 ? (NSL * SCX + 63) / 64 : 0;
+  static_assert(C::SC <= 128, "staged columns");
+  __shared__ double Ts[C::SL * PT];
+  __shared__ double ws[P + 1];   // GLL weights: one LDS read per weight instead of a compare-select chain
+  // the Ab operands live in LDS, read per k-step (round 6): as per-lane registers they held 2 KS doubles per lane through
+  // the whole kernel and, with the accumulators, capped the kernel at 4 waves per SIMD
+  __shared__ double Ab[NAP];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lk = lane >> 4;
@@ -934,14 +949,32 @@ __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs 
   const bool has_u = (a.flags & 1) != 0, has_v = (a.flags & 2) != 0;
   const auto ru = brsrc(a.cu, has_u ? nbytes : 0), rv = brsrc(a.cv, has_v ? nbytes : 0);
 
-  // ---- staged window: lines gx0 - P .., columns gy0 - P .. (lines outside the local range read 0)
-  const int sbase = ((gx0 - P - lb0) * NY + gy0 - P) * 8;
-  double st[C::NSTAGE];
+  // ---- tables first (their loads return under the staging loads), then the staged window
+  const double wsv = tid <= P ? kGllW<P>.v[tid] : 0.0;
+  double abv[NAB];
 #pragma unroll
-  for (int q = 0; q < C::NSTAGE; ++q) {
-    const int idx = min(tid + q * C::THREADS, C::SL * C::SC - 1);
-    const int rr = idx / C::SC, cc = idx - rr * C::SC;
-    st[q] = bload(rx, sbase + (rr * NY + cc) * 8);
+  for (int q = 0; q < NAB; ++q) {
+    const int idx = tid + q * C::THREADS;
+    abv[q] = idx < NTAB ? kBMTab<P>.v[idx] : 0.0;
+  }
+  const int lstep = NW * NY * 8;
+  const int line0 = (gx0 - P - lb0 + w) * NY * 8;
+  const int gyA = gy0 - P + lane;
+  const unsigned vA = (gyA >= 0 && gyA < NY) ? static_cast<unsigned>(gyA) * 8u : 0x80000000u;
+  double sA[NSL];
+#pragma unroll
+  for (int k = 0; k < NSL; ++k)
+    if (k < NSL - 1 || w + NW * k < C::SL) sA[k] = bload(rx, static_cast<int>(vA + static_cast<unsigned>(line0 + k * lstep)));
+  double sX[NXL > 0 ? NXL : 1];
+  int xts[NXL > 0 ? NXL : 1];
+#pragma unroll
+  for (int j = 0; j < NXL; ++j) {
+    const int lp = lane + 64 * j, k = lp / SCX, cc = 64 + lp - k * SCX, rr = w + NW * k;
+    const int gy = gy0 - P + cc;
+    const bool ok = k < NSL && rr < C::SL;
+    const unsigned vx = (ok && gy >= 0 && gy < NY) ? static_cast<unsigned>(gy) * 8u : 0x80000000u;
+    xts[j] = ok ? C::ts(rr, cc) : -1;
+    sX[j] = bload(rx, static_cast<int>(vx + static_cast<unsigned>(line0 + k * lstep)));
   }
   // this lane's epilogue nodes: tile row i = lk + 4 r, column gy0 + w CB + lr
   const int gyn = gy0 + w * C::CB + lr;
@@ -952,52 +985,64 @@ __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs 
     const int i = lk + 4 * r;
     eoff[r] = (col_ok && i < rows_ok) ? ((gx0 + i - lb0) * NY + gyn) : -(1 << 26);
   }
-  // the Ab operands of this lane: rows lr, window entries 4 s + lk
-  double aK[C::KS], aG[C::KS];
 #pragma unroll
-  for (int q = 0; q < C::KS; ++q) {
-    aK[q] = kBMTab<P>.v[lr * C::KW + 4 * q + lk];
-    aG[q] = GRAD ? kBMTab<P>.v[16 * C::KW + lr * C::KW + 4 * q + lk] : 0.0;
-  }
+  for (int k = 0; k < NSL; ++k)
+    if (k < NSL - 1 || w + NW * k < C::SL) Ts[C::ts(w + NW * k, lane)] = sA[k];
 #pragma unroll
-  for (int q = 0; q < C::NSTAGE; ++q) {
+  for (int j = 0; j < NXL; ++j)
+    if (xts[j] >= 0) Ts[xts[j]] = sX[j];
+  if (tid <= P) ws[tid] = wsv;
+#pragma unroll
+  for (int q = 0; q < NAB; ++q) {
     const int idx = tid + q * C::THREADS;
-    if ((q + 1) * C::THREADS <= C::SL * C::SC || idx < C::SL * C::SC) {
-      const int rr = idx / C::SC, cc = idx - rr * C::SC;
-      const int gy = gy0 - P + cc;
-      Ts[C::ts(rr, cc)] = (gy >= 0 && gy < NY) ? st[q] : 0.0;
-    }
+    if (idx < NTAB) Ab[(idx / C::KW) * AP + idx % C::KW] = abv[q];
   }
-  if (tid <= P) ws[tid] = gll_w<P>(tid);
   // pointwise operands, issued after the staging stores (they land during the products)
   double pu[4], pv[4];
   NodeOps ops[4] = {};
+  if (a.cpol & 256) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (a.cpol & 256) {
+    for (int r = 0; r < 4; ++r) {
       pu[r] = bload_c<2>(ru, eoff[r] * 8);
       pv[r] = bload_c<2>(rv, eoff[r] * 8);
-    } else {
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
       pu[r] = bload(ru, eoff[r] * 8);
       pv[r] = bload(rv, eoff[r] * 8);
     }
-    if constexpr (FULL) ops[r] = load_node_ops(a, eoff[r]);
+  }
+  if constexpr (FULL) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ops[r] = load_node_ops(a, eoff[r]);
   }
   __syncthreads();
 
   // ---- the two products of this wave's 16 x 16 output block (independent accumulator chains)
   dbl4v xk = {0.0, 0.0, 0.0, 0.0}, xg = xk, yk = xk, yg = xk;
   const int cb0 = w * C::CB;
+  // operands of step q + 1 are read while step q's MFMAs run; the scheduling barrier keeps the compiler from
+  // hoisting every step's reads to the top (which held all 4 KS operands live and cost a wave per SIMD)
+  double aK = Ab[lr * AP + lk], aG = GRAD ? Ab[16 * AP + lr * AP + lk] : 0.0;
+  double bx = Ts[C::ts(lk, P + cb0 + lr)], ay = Ts[C::ts(P + lr, cb0 + lk)];
 #pragma unroll
   for (int q = 0; q < C::KS; ++q) {
-    const double bx = Ts[C::ts(4 * q + lk, P + cb0 + lr)];     // T[gx0 - P + 4q + lk][gy0 + cb0 + lr]
-    const double ay = Ts[C::ts(P + lr, cb0 + 4 * q + lk)];     // T[gx0 + lr][gy0 + cb0 - P + 4q + lk]
-    xk = __builtin_amdgcn_mfma_f64_16x16x4f64(aK[q], bx, xk, 0, 0, 0);
-    yk = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, aK[q], yk, 0, 0, 0);
-    if constexpr (GRAD) {
-      xg = __builtin_amdgcn_mfma_f64_16x16x4f64(aG[q], bx, xg, 0, 0, 0);
-      yg = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, aG[q], yg, 0, 0, 0);
+    double aK1 = 0.0, aG1 = 0.0, bx1 = 0.0, ay1 = 0.0;
+    if (q + 1 < C::KS) {
+      aK1 = Ab[lr * AP + 4 * (q + 1) + lk];
+      if constexpr (GRAD) aG1 = Ab[16 * AP + lr * AP + 4 * (q + 1) + lk];
+      bx1 = Ts[C::ts(4 * (q + 1) + lk, P + cb0 + lr)];     // T[gx0 - P + 4q + lk][gy0 + cb0 + lr]
+      ay1 = Ts[C::ts(P + lr, cb0 + 4 * (q + 1) + lk)];     // T[gx0 + lr][gy0 + cb0 - P + 4q + lk]
     }
+    xk = __builtin_amdgcn_mfma_f64_16x16x4f64(aK, bx, xk, 0, 0, 0);
+    yk = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, aK, yk, 0, 0, 0);
+    if constexpr (GRAD) {
+      xg = __builtin_amdgcn_mfma_f64_16x16x4f64(aG, bx, xg, 0, 0, 0);
+      yg = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, aG, yg, 0, 0, 0);
+    }
+    aK = aK1, aG = aG1, bx = bx1, ay = ay1;
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // ---- epilogue in registers: node (tile row lk + 4 r, column gyn)
@@ -1007,34 +1052,63 @@ __global__ __launch_bounds__(BMCfg<P>::THREADS) void apply_bmfma(const BandArgs 
   const int lj = gyn % P, ne = gyn / P;
   const bool hasLy = lj == 0 && ne - 1 >= 0, hasRy = lj != 0 || ne < a.ney;
   const double my = lj != 0 ? ws[lj] : (hasLy ? wP : 0.0) + (hasRy ? w0 : 0.0);
+  const double sxk = a.fKx * my, sxg = a.fX * my;
+  // tile-uniform: can a node of this tile lack a neighbour element (strip / domain edge) or be a Dirichlet row?
+  const int gxl = gx0 + rows_ok - 1, gyl = gy0 + C::NB * C::CB - 1;
+  const bool xedge = gx0 <= a.ex_begin * P || gxl >= a.ex_end * P, yedge = gy0 == 0 || gyl >= NY - 1;
+  bool special = FULL;
+  if (a.dir_mode != SEM_DIR_NONE) {
+    const unsigned sd = a.sides;
+    special = special || ((sd & SEM_SIDE_W) && gx0 == 0) || ((sd & SEM_SIDE_E) && gxl >= a.NXg - 1) ||
+              ((sd & SEM_SIDE_S) && gy0 == 0) || ((sd & SEM_SIDE_N) && gyl >= NY - 1);
+  }
+  // a shared row / column without its left / right element drops that element's folded diagonal term: the y
+  // corrections are per lane (its column), the x corrections per row; both zero away from strip / domain edges
+  const double dyk = lj == 0 ? (hasLy ? 0.0 : -KPP) + (hasRy ? 0.0 : -K00) : 0.0;
+  const double dyg = lj == 0 ? (hasLy ? 0.0 : -GPP) + (hasRy ? 0.0 : -G00) : 0.0;
+  const bool full_path = xedge || yedge || a.fM != 0.0 || special;   // tile-uniform
   double zz[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = lk + 4 * r, gx = gx0 + i;
-    const double xv = Ts[C::ts(P + i, P + cb0 + lr)];
-    const int li = i % P, me = gx / P;
+    const int li = gx % P, me = gx / P;
     const bool hasLx = li == 0 && me - 1 >= a.ex_begin, hasRx = li != 0 || me < a.ex_end;
     const double mx = li != 0 ? ws[li] : (hasLx ? wP : 0.0) + (hasRx ? w0 : 0.0);
     double XK = xk[r], XG = xg[r], YK = yk[r], YG = yg[r];
-    if (li == 0) {   // a shared row without its left / right element: drop that element's diagonal term
-      if (!hasLx) { XK = fma(-KPP, xv, XK); XG = fma(-GPP, xv, XG); }
-      if (!hasRx) { XK = fma(-K00, xv, XK); XG = fma(-G00, xv, XG); }
+    double z;
+    if (full_path) {
+      const double xv = Ts[C::ts(P + i, P + cb0 + lr)];
+      const double dxk = li == 0 ? (hasLx ? 0.0 : -KPP) + (hasRx ? 0.0 : -K00) : 0.0;
+      const double dxg = li == 0 ? (hasLx ? 0.0 : -GPP) + (hasRx ? 0.0 : -G00) : 0.0;
+      XK = fma(dxk, xv, XK);
+      XG = fma(dxg, xv, XG);
+      YK = fma(dyk, xv, YK);
+      YG = fma(dyg, xv, YG);
+      z = fma(sxk, XK, a.fKy * mx * YK);
+      z = fma(a.fM * mx * my, xv, z);
+      if constexpr (GRAD) {
+        z = fma(has_u ? pu[r] : 1.0, sxg * XG, z);
+        z = fma(a.fY * (has_v ? pv[r] : 1.0), mx * YG, z);
+      }
+      if (special) z = finish_node<FULL>(a, ops[r], gx, gyn, xv, z);
+    } else {
+      z = fma(sxk, XK, a.fKy * mx * YK);
+      if constexpr (GRAD) {
+        z = fma(has_u ? pu[r] : 1.0, sxg * XG, z);
+        z = fma(a.fY * (has_v ? pv[r] : 1.0), mx * YG, z);
+      }
     }
-    if (lj == 0) {
-      if (!hasLy) { YK = fma(-KPP, xv, YK); YG = fma(-GPP, xv, YG); }
-      if (!hasRy) { YK = fma(-K00, xv, YK); YG = fma(-G00, xv, YG); }
-    }
-    double z = fma(a.fKx * my, XK, a.fKy * mx * YK);
-    z = fma(a.fM * mx * my, xv, z);
-    if constexpr (GRAD) {
-      z = fma(a.fX * (has_u ? pu[r] : 1.0), my * XG, z);
-      z = fma(a.fY * (has_v ? pv[r] : 1.0), mx * YG, z);
-    }
-    zz[r] = finish_node<FULL>(a, ops[r], gx, gyn, xv, z);
+    zz[r] = z;
   }
+  if ((a.cpol & 255) == 3) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (eoff[r] >= 0) bstore_any(a.cpol, ry, eoff[r] * 8, zz[r]);
+    for (int r = 0; r < 4; ++r)
+      if (eoff[r] >= 0) bstore_c<17>(ry, eoff[r] * 8, zz[r]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (eoff[r] >= 0) bstore(ry, eoff[r] * 8, zz[r]);
+  }
 }
 
 template <int P>

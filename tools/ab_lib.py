@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--reps", type=int, default=0, help="applies per graph (0: 1000 on small meshes, 20 on large)")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--lap", type=int, default=0)
+    ap.add_argument("--algo", type=int, default=0, help="sem_apply_desc.algo (0 AUTO = band, 2 = MFMA)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -60,10 +61,10 @@ def main():
             y = torch.empty_like(T)
             if a.lap:
                 desc = _lib.SemApplyDesc(0.0, 1.0, 0.0, 0.0, None, None, 0.0, None, None, None, None, 0.0, 0, None, None,
-                                         0, 0, 0, 0)
+                                         0, a.algo, 0, 0)
             else:
                 desc = _lib.SemApplyDesc(0.0, 1.0, 40.0, 40.0, u.data_ptr(), v.data_ptr(), 0.0, None, None, None, None,
-                                         0.0, _lib.DIR_IDENTITY, None, None, _lib.SIDE_W | _lib.SIDE_E, 0, 0, 0)
+                                         0.0, _lib.DIR_IDENTITY, None, None, _lib.SIDE_W | _lib.SIDE_E, a.algo, 0, 0)
 
             def fn(lib=lib, h=h, desc=desc, y=y):
                 s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -96,7 +97,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize(dev)
                 ts[i].append(e0.elapsed_time(e1) * 1e3 / reps)
-        rec = {"P": P, "ne": ne, "N": N, "lap": bool(a.lap), "reps": reps, "max_rel_diff": diff,
+        rec = {"P": P, "ne": ne, "N": N, "lap": bool(a.lap), "algo": a.algo, "reps": reps, "max_rel_diff": diff,
                "us": {os.path.relpath(p, ROOT): float(np.median(t)) for (p, _), t in zip(libs, ts)},
                "us_all": {os.path.relpath(p, ROOT): [round(x, 3) for x in t] for (p, _), t in zip(libs, ts)}}
         print(json.dumps(rec), flush=True)
