@@ -376,7 +376,7 @@ def gmres(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=None, maxiter=None, pr
 
 
 def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None, precond=None, callback=None,
-               inner=None):
+               inner=None, jump=None, jump_ratio=10.0):
     """Left-preconditioned restarted GMRES, SciPy's `gmres` (scipy 1.15 iterative.py) restated on
     device tensors: the Arnoldi process runs on M^-1 A, the inner loop stops on the
     preconditioned residual estimate against an adaptive tolerance (gh-8400 control), and each
@@ -390,7 +390,15 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
     `maxiter` counts restarts, as SciPy's does.  info = 0 on convergence, else maxiter.
     inner(A, w) = A @ w over a partitioned vector (sem_amd.parallel: shared lines counted once, the
     partial products all-reduced); norms follow it.
-    """
+
+    jump (round 6): safeguard for an INEXACT preconditioner.  With a fixed M, the preconditioned
+    residual ||M^-1 (b - A x)|| that starts a cycle equals the estimate the previous cycle ended with; the coupler's
+    M^-1 is a pair of iterative block solves stopped at an absolute tolerance, i.e. a slightly different operator at
+    every application, and when that inconsistency builds up the restart finds a true residual far above the
+    estimate (cfg5, Ra = 1e4: 20x and then 280x before the Newton iteration diverged, profiles/r05/cfg5/).  When the
+    new cycle's residual exceeds jump_ratio times the last estimate, jump(ratio) is called; if it returns True (the
+    caller tightened its preconditioner) the cycle's first vector is recomputed with the tightened M.  The outer
+    arithmetic is SciPy's either way; result.jumps counts the detections."""
     N = b.numel()
     dt, dev = b.dtype, b.device
     restart, maxiter = _sizes(N, restart, maxiter, inner, 20)
@@ -416,9 +424,15 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
     rnorm = vnorm(r)
     if rnorm < tol:
         return GMRESResult(x, 0, 0, rnorm, matvecs)
+    jumps, prev_presid = 0, None
     for _ in range(maxiter):
         z = psolve(r)
         zn = vnorm(z)
+        if jump is not None and prev_presid and zn > jump_ratio * prev_presid:
+            jumps += 1
+            if jump(zn / prev_presid):
+                z = psolve(r)
+                zn = vnorm(z)
         V[0] = z / zn
         H = np.zeros((restart + 1, restart))
         cs, sn = np.zeros(restart), np.zeros(restart)
@@ -468,12 +482,15 @@ def gmres_left(matvec, b, x0=None, atol=0.0, rtol=0.0, restart=20, maxiter=None,
         rnorm = vnorm(r)
         if rnorm <= tol or breakdown:
             break
+        prev_presid = presid
         if presid <= ptol:
             ptol_max = max(eps, 0.25 * ptol_max)
         else:
             ptol_max = min(1.0, 1.5 * ptol_max)
         ptol = presid * min(ptol_max, tol / rnorm)
-    return GMRESResult(x, 0 if rnorm <= tol else maxiter, total, rnorm, matvecs)
+    res = GMRESResult(x, 0 if rnorm <= tol else maxiter, total, rnorm, matvecs)
+    res.jumps = jumps
+    return res
 
 
 class Recycle:

@@ -280,28 +280,55 @@ class BoussinesqCoupler:
         self.iterations = k
         return x
 
+    # restart-jump safeguard: the block-Jacobi preconditioner is two iterative block solves stopped
+    # at mtol_internal sqrt(N); a jump of the preconditioned residual at a GMRES restart (> JUMP_RATIO x the estimate)
+    # tightens both block solves' tolerance by JUMP_TIGHTEN for the rest of that linear solve, at most JUMP_MAX times
+    JUMP_RATIO, JUMP_TIGHTEN, JUMP_MAX = 10.0, 0.1, 3
+
+    def _tighten_blocks(self, ratio):
+        """gmres_left's jump hook: one tightening step of the inner block solves (returns True when applied)."""
+        if self._jumps >= self.JUMP_MAX:
+            self._log(f'  GMRES restart jump x{ratio:.1f}: block solves already tightened {self._jumps} times')
+            return False
+        self._jumps += 1
+        for s in (self.cd, self.ns):
+            if s is not None and hasattr(s, "_mtol"):
+                s._mtol *= self.JUMP_TIGHTEN
+        self._log(f'  GMRES restart jump x{ratio:.1f}: block solves re-run at {self.JUMP_TIGHTEN ** self._jumps:g} x '
+                  f'mtol_internal')
+        return True
+
     def _linear_jnk(self, b):
         """GMRES on the coupled Jacobian, block-Jacobi preconditioned (ScipyKrylov :89-91).  Device mode: the
-        Krylov basis and every vector stay on the device (inner products across strips when partitioned)."""
+        Krylov basis and every vector stay on the device (inner products across strips when partitioned).  The
+        restart-jump safeguard (_tighten_blocks) leaves a solve whose preconditioner behaves untouched: the same
+        arithmetic, the same history."""
         it = [0]
 
         def cb(presid):
             it[0] += 1
             self._log(f'  GMRES {it[0]} ; {presid}')
 
-        if self._device:
-            res = gmres_left(self.jacobian_apply, b, atol=self.atol_gmres, rtol=0.0, restart=self.restart,
-                             maxiter=5000, precond=self.block_jacobi, callback=cb, inner=self._inner)
-            if res.info != 0:
-                raise RuntimeError(f'GMRES failed to converge in {res.info} restarts')
-            return res.x
-        mv = lambda t: torch.from_numpy(self.jacobian_apply(t.numpy()))  # noqa: E731
-        pc = lambda t: torch.from_numpy(self.block_jacobi(t.numpy()))  # noqa: E731
-        res = gmres_left(mv, torch.from_numpy(np.ascontiguousarray(b)), atol=self.atol_gmres, rtol=0.0,
-                         restart=self.restart, maxiter=5000, precond=pc, callback=cb)
+        saved = [(s, s._mtol) for s in (self.cd, self.ns) if s is not None and hasattr(s, "_mtol")]
+        self._jumps = 0
+        try:
+            if self._device:
+                res = gmres_left(self.jacobian_apply, b, atol=self.atol_gmres, rtol=0.0, restart=self.restart,
+                                 maxiter=5000, precond=self.block_jacobi, callback=cb, inner=self._inner,
+                                 jump=self._tighten_blocks, jump_ratio=self.JUMP_RATIO)
+            else:
+                mv = lambda t: torch.from_numpy(self.jacobian_apply(t.numpy()))  # noqa: E731
+                pc = lambda t: torch.from_numpy(self.block_jacobi(t.numpy()))  # noqa: E731
+                res = gmres_left(mv, torch.from_numpy(np.ascontiguousarray(b)), atol=self.atol_gmres, rtol=0.0,
+                                 restart=self.restart, maxiter=5000, precond=pc, callback=cb,
+                                 jump=self._tighten_blocks, jump_ratio=self.JUMP_RATIO)
+        finally:
+            for s, m in saved:
+                s._mtol = m
+        self.restart_jumps = getattr(self, "restart_jumps", 0) + res.jumps
         if res.info != 0:
             raise RuntimeError(f'GMRES failed to converge in {res.info} restarts')
-        return res.x.numpy()
+        return res.x if self._device else res.x.numpy()
 
     def _armijo_goldstein(self, x, dx, norm0):
         """ArmijoGoldsteinLS(maxiter=AGi, rho=AGr, c=AGc) on the residual norm along dx."""
