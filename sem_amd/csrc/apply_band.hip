@@ -455,9 +455,12 @@ __device__ __forceinline__ void band_body(const double* __restrict__ px, const d
   constexpr int n = C::n, BX = C::BX, PT = C::PT, PY = C::PY, LW = C::LW, NW = C::NW;
   __shared__ double Ts[C::RX * PT];
   __shared__ double XK[BX * PY];
-  __shared__ double XG[GRAD ? BX * PY : 1];
+  // XG, YG are allocated for the Laplacian-only form (GRAD = false) too although it never touches them: the
+  // smaller footprint let 8 workgroups share a CU instead of 6 and ran 3 % slower at 1024^2 (round-6 A/B,
+  // profiles/r06/band_ab/ab_tile_and_lds_variants.jsonl) -- more tiles in flight contend for the same L2 halos
+  __shared__ double XG[BX * PY];
   __shared__ double YK[BX * PY];
-  __shared__ double YG[GRAD ? BX * PY : 1];
+  __shared__ double YG[BX * PY];
   __shared__ double ws[n];
 
   // XCD-aware remap: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of tiles (y fastest) and
