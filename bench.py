@@ -61,7 +61,11 @@ def parse():
                     help="strong: --ne x --ne elements over all GPUs; weak: --ne x --ne elements per GPU")
     ap.add_argument("--extra-steps", type=int, default=100,
                     help="N > 1: steps timed for the strong_hbm and weak extra keys (0 = skip them)")
-    ap.add_argument("--overlap", type=int, default=1, help="N > 1: overlap the interface exchange with the interior")
+    ap.add_argument("--overlap", type=int, default=-1,
+                    help="N > 1: overlap the interface exchange with the interior apply (1), or not (0); -1 (default): "
+                         "overlap only strips of >= 2^20 local DOFs -- the overlapped step's two extra position-ranged "
+                         "launches and cross-stream waits cost ~6 us per step (measured over a one-rank RCCL group, "
+                         "profiles/r06/rccl/), more than a small strip's interior apply it could hide")
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "p2p"],
                     help="interface assembly for N > 1: one RCCL all-reduce, or send/recv with the two neighbours")
     return ap.parse_args()
@@ -288,14 +292,18 @@ def main():
 
     from sem_amd import _lib
     from sem_amd.device import get_mesh
+    from sem_amd.parallel import StripPartition
 
     P, ne, Pe = args.P, args.ne, args.Pe
 
     def strip_case(nex, ney, d, steps, warmup, seed):
         """Build this rank's strip of an nex x ney mesh and time `steps` partitioned applies (apply + interface
         exchange).  Returns (seconds max-reduced over ranks, graph used, mesh, operands)."""
+        part_cols = StripPartition(nex, world).bounds
+        local = (part_cols[rank + 1] - part_cols[rank]) * P * (ney * P + 1)
+        overlap = bool(args.overlap) if args.overlap >= 0 else local >= (1 << 20)
         step, mesh, (T, y, kw), (eb, ee) = build_strip_step(P, nex, ney, d, Pe, world, rank, dev, dist,
-                                                            args.exchange, bool(args.overlap), seed)
+                                                            args.exchange, overlap, seed)
 
         # N > 1 over RCCL: the whole step (apply, pack, RCCL all-reduce or send/recv, unpack) is captured
         # too -- RCCL collectives are stream-capturable -- so the per-step host cost (four launches and a
@@ -358,7 +366,8 @@ def main():
                    "partition": f"element-column strips x{world}" + (
                        {"allreduce": ", all-reduce of interface lines",
                         "p2p": ", send/recv of interface lines with neighbours"}[args.exchange]
-                       + (", overlapped with the interior apply" if args.overlap else "")
+                       + (", overlapped with the interior apply" if (args.overlap > 0 or (args.overlap < 0 and n_loc >= (1 << 20)))
+                          else "")
                        + (" (RCCL)" if args.dist_backend == "nccl" else " (gloo rehearsal)")
                        if world > 1 else ""),
                    "regime": regime(n_loc, latency=world > 1 and 32.0 * n_loc < 256e6), "hipgraph": use_graph},
