@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 13
+#define SEM_ABI_VERSION 14
 
 enum sem_status {
   SEM_OK = 0,
@@ -383,6 +383,36 @@ int sem_gemv_rows(int M, int K, double alpha, const double* A, int64_t lda, cons
  * is ~N_ex + 1 dependent launches instead of 2 N_ex (velocity_solve.py twisted_thomas_solve). */
 int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, int64_t lda0, const double* x0,
                    double* y0, int K1, const double* A1, int64_t lda1, const double* x1, double* y1, void* stream);
+
+/* ---- nested-dissection solve of the velocity Jacobian (ABI 14) ---------- */
+/* The streaming steps of sem_amd/solvers/nested_dissection.py, which orders the Dirichlet-row-replaced velocity
+ * Jacobian by nested dissection of the element grid (the analogue of the fill-reducing column order of the
+ * reference's `splu`, NavierStokes_Solver.py:184) and replaces its triangular solves (:189-203).
+ * One launch = one level of fronts (or the element leaves): front f has a row-major operator at op[f] (device
+ * address; R_f x K_f, leading dimension ld_f: dims[4 f .. 4 f + 2] = R_f, K_f, ld_f; K_f and ld_f even, rows
+ * 16-byte aligned), its K_f operand positions in W at xidx[xoff[f] ..] (-1: a zero operand), and
+ *   back = 0: stage[yoff[f] + r] = (A_f x)_r
+ *   back = 1: W[yidx[yoff[f] + r]] -= (A_f x)_r   (targets distinct and not operands of the same launch).
+ * tiles[2 b], tiles[2 b + 1] = (front, first row) of workgroup b; rows = 16 or 4 rows per workgroup; kmax >= every
+ * K_f of the launch (<= 8192).  All arrays are device memory; deterministic (fixed summation order). */
+typedef struct sem_front_launch {
+  int ntiles, rows, kmax, back;
+  const int64_t* op;
+  const int32_t* dims;
+  const int64_t* xoff;
+  const int64_t* yoff;
+  const int32_t* tiles;
+  const int32_t* xidx;
+  const int32_t* yidx;
+  double* W;
+  double* stage;
+} sem_front_launch;
+int sem_front_gemv(const sem_front_launch* d, void* stream);
+/* The write-back of a forward step: W[copy_tgt[i]] = stage[copy_src[i]] (i < ncopy) and
+ * W[acc_tgt[j]] -= stage[s] for s = acc_src4[4 j + k], k = 0..3 in order, skipping s = -1 (j < nacc; acc_src4
+ * 16-byte aligned).  Targets distinct.  Device memory; stream-ordered. */
+int sem_front_scatter(int ncopy, const int32_t* copy_tgt, const int32_t* copy_src, int nacc, const int32_t* acc_tgt,
+                      const int32_t* acc_src4, const double* stage, double* W, void* stream);
 
 /* ---- GMRES least-squares column (host) ------------------------------------ */
 /* Host memory, no device work (ABI 11): applies the Givens rotations 0..k-1 (cs, sn) to col[0..k+1], forms

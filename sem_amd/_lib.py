@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.environ.get("SEM_LIBDIR") or os.path.join(_HERE, "lib"), "libsemops.so")
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 # kernel-selection knobs (include/sem_ops.h enum sem_tune; process-global, not thread-safe); the values between
 # them are retired knobs (round 6), refused by sem_set_tuning
@@ -62,6 +62,12 @@ class SemNsDesc(C.Structure):
                 ("jvv", C.c_void_p), ("c_T", C.c_double), ("T", C.c_void_p), ("c_div", C.c_double),
                 ("dval_u", C.c_void_p), ("dval_v", C.c_void_p), ("dir_mask", C.c_void_p), ("dir_sides", C.c_uint),
                 ("pin_first", C.c_int), ("pin", C.c_int64), ("pin_val", C.c_double), ("uv_pitch", C.c_int64)]
+
+
+class SemFrontLaunch(C.Structure):
+    _fields_ = [("ntiles", C.c_int), ("rows", C.c_int), ("kmax", C.c_int), ("back", C.c_int), ("op", C.c_void_p),
+                ("dims", C.c_void_p), ("xoff", C.c_void_p), ("yoff", C.c_void_p), ("tiles", C.c_void_p),
+                ("xidx", C.c_void_p), ("yidx", C.c_void_p), ("W", C.c_void_p), ("stage", C.c_void_p)]
 
 
 # name -> (restype, argtypes); mirrors include/sem_ops.h one-for-one
@@ -115,6 +121,9 @@ _SIGS = {
     "sem_givens_column": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "sem_gemv_rows2": (C.c_int, [C.c_int, C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
                                  C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sem_front_gemv": (C.c_int, [C.POINTER(SemFrontLaunch), C.c_void_p]),
+    "sem_front_scatter": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p]),
     "sem_gemv_rows": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_int64, C.c_void_p, C.c_double,
                                 C.c_void_p, C.c_void_p]),
 }

@@ -18,7 +18,7 @@ LIB = os.path.join(LIBDIR, "libsemops.so")
 ARCH = os.environ.get("SEM_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["sem_ops.hip", "apply_band.hip", "gll_tables.cpp", "krylov_sweeps.hip", "ns_velocity.hip", "ns_apply.hip", "block_gemv.hip", "ns_condense.hip",
-           "dense_inverse.hip"]
+           "dense_inverse.hip", "front_solve.hip"]
 HEADERS = ["sem_internal.h", "gll_consts.h", "apply_common.h", os.path.join("..", "..", "include", "sem_ops.h")]
 
 

@@ -1,0 +1,160 @@
+// Nested-dissection solve of the Navier-Stokes velocity Jacobian (ABI 14; sem_amd/solvers/nested_dissection.py):
+// the streaming steps that replace the reference's SuperLU triangular solves (NavierStokes_Solver.py:189-203).
+//
+// sem_front_gemv: one level of fronts (or the element leaves) in ONE launch.  Front f holds a dense row-major
+// operator A_f (R_f x K_f, leading dimension ld_f): forward [S^-1; A_BS S^-1] (or [Xi; A_bi Xi] at a leaf),
+// back V = S^-1 A_SB (or Xi A_ib).  A workgroup takes `rows` rows of one front (its tile), gathers the front's
+// K operand values W[xidx[.]] into LDS once (-1: a zero operand), streams its rows with non-temporal 16-byte loads
+// (each operator is read once per solve) and reduces each row across the wave in a fixed order:
+//   forward: stage[yoff_f + r] = (A_f x)_r
+//   back:    W[yidx[yoff_f + r]] -= (A_f x)_r       (the rows' targets are not operands of the same launch)
+// sem_front_scatter: the forward step's deterministic write-back -- copy targets W[t] = stage[s] (a front's own
+// separator / a leaf's interior) and accumulation targets W[t] -= stage[s_0] .. stage[s_3] (the <= 4 fronts of a
+// level that update a node of an ancestor separator), summed in the order the host sorted them.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "sem_internal.h"
+
+namespace sem {
+
+using dvec2f = double __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ double front_wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double2 load_nt2(const double* p) {
+  const dvec2f v = __builtin_nontemporal_load(reinterpret_cast<const dvec2f*>(p));
+  return make_double2(v.x, v.y);
+}
+
+// RW rows per wave (4 waves), U pairs of columns per lane in flight per row
+template <int RW, int U>
+__global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch a) {
+  extern __shared__ double xs[];
+  const int f = a.tiles[2 * blockIdx.x], r0 = a.tiles[2 * blockIdx.x + 1];
+  const int R = a.dims[4 * f], K = a.dims[4 * f + 1], ld = a.dims[4 * f + 2];
+  const int32_t* xi = a.xidx + a.xoff[f];
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const int p = xi[k];
+    xs[k] = p >= 0 ? a.W[p] : 0.0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rb = r0 + wave * RW;
+  if (rb >= R) return;
+  const double* A = reinterpret_cast<const double*>(a.op[f]);
+  const double* rows[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) rows[i] = A + static_cast<int64_t>(min(rb + i, R - 1)) * ld;  // clamped: not stored
+  double acc[RW][2];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) acc[i][0] = acc[i][1] = 0.0;
+  const int KP = K >> 1;  // K is even (the host checks): column pairs
+  const double2* x2 = reinterpret_cast<const double2*>(xs);
+  int u = lane;
+  for (; u + 64 * (U - 1) < KP; u += 64 * U) {
+    double2 av[U][RW], xv[U];
+#pragma unroll
+    for (int t = 0; t < U; ++t) {
+      xv[t] = x2[u + 64 * t];
+#pragma unroll
+      for (int i = 0; i < RW; ++i) av[t][i] = load_nt2(rows[i] + 2 * (u + 64 * t));
+    }
+#pragma unroll
+    for (int t = 0; t < U; ++t)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        acc[i][0] = fma(av[t][i].x, xv[t].x, acc[i][0]);
+        acc[i][1] = fma(av[t][i].y, xv[t].y, acc[i][1]);
+      }
+  }
+  for (; u < KP; u += 64) {
+    const double2 xv = x2[u];
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+      const double2 av = load_nt2(rows[i] + 2 * u);
+      acc[i][0] = fma(av.x, xv.x, acc[i][0]);
+      acc[i][1] = fma(av.y, xv.y, acc[i][1]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const double v = front_wave_sum(acc[i][0] + acc[i][1]);
+    const int r = rb + i;
+    if (lane == 0 && r < R) {
+      if (a.back) {
+        const int p = a.yidx[a.yoff[f] + r];
+        a.W[p] -= v;
+      } else {
+        a.stage[a.yoff[f] + r] = v;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void front_scatter_kernel(int ncopy, const int32_t* __restrict__ ct,
+                                                            const int32_t* __restrict__ cs, int nacc,
+                                                            const int32_t* __restrict__ at,
+                                                            const int32_t* __restrict__ as4,
+                                                            const double* __restrict__ stage, double* W) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < ncopy) {
+    W[ct[i]] = stage[cs[i]];
+  } else if (i < ncopy + nacc) {
+    const int j = i - ncopy;
+    const int4 s = reinterpret_cast<const int4*>(as4)[j];
+    double v = W[at[j]];
+    if (s.x >= 0) v -= stage[s.x];
+    if (s.y >= 0) v -= stage[s.y];
+    if (s.z >= 0) v -= stage[s.z];
+    if (s.w >= 0) v -= stage[s.w];
+    W[at[j]] = v;
+  }
+}
+
+}  // namespace sem
+
+extern "C" {
+
+int sem_front_gemv(const sem_front_launch* d, void* stream) {
+  if (!d) return sem::set_error(SEM_EINVAL, "front_gemv: null descriptor");
+  if (d->ntiles < 0 || d->kmax < 0 || (d->rows != 4 && d->rows != 16))
+    return sem::set_error(SEM_EINVAL, "front_gemv: bad sizes (rows must be 4 or 16)");
+  if (d->ntiles == 0) return SEM_OK;
+  if (!d->op || !d->dims || !d->xoff || !d->yoff || !d->tiles || !d->xidx || !d->W || (d->back ? !d->yidx : !d->stage))
+    return sem::set_error(SEM_EINVAL, "front_gemv: null argument");
+  const size_t lds = static_cast<size_t>(d->kmax) * sizeof(double);
+  if (lds > 64 * 1024) return sem::set_error(SEM_EUNSUPPORTED, "front_gemv: more than 8192 operands per front");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (d->rows == 16)
+    hipLaunchKernelGGL((sem::front_gemv_kernel<4, 2>), dim3(d->ntiles), dim3(256), lds, s, *d);
+  else
+    hipLaunchKernelGGL((sem::front_gemv_kernel<1, 8>), dim3(d->ntiles), dim3(256), lds, s, *d);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("front_gemv launch: ") + hipGetErrorString(e));
+  return SEM_OK;
+}
+
+int sem_front_scatter(int ncopy, const int32_t* copy_tgt, const int32_t* copy_src, int nacc, const int32_t* acc_tgt,
+                      const int32_t* acc_src4, const double* stage, double* W, void* stream) {
+  if (ncopy < 0 || nacc < 0) return sem::set_error(SEM_EINVAL, "front_scatter: bad sizes");
+  const int64_t n = static_cast<int64_t>(ncopy) + nacc;
+  if (n == 0) return SEM_OK;
+  if (!stage || !W || (ncopy && (!copy_tgt || !copy_src)) || (nacc && (!acc_tgt || !acc_src4)))
+    return sem::set_error(SEM_EINVAL, "front_scatter: null argument");
+  if ((reinterpret_cast<uintptr_t>(acc_src4) % 16) != 0)
+    return sem::set_error(SEM_EINVAL, "front_scatter: acc_src4 must be 16-byte aligned");
+  hipLaunchKernelGGL(sem::front_scatter_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), ncopy, copy_tgt, copy_src, nacc, acc_tgt, acc_src4, stage,
+                     W);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("front_scatter launch: ") + hipGetErrorString(e));
+  return SEM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,582 @@
+"""Nested-dissection (multifrontal) direct solve of the Navier-Stokes velocity Jacobian.
+
+The reference factors the Dirichlet-row-replaced velocity Jacobian with SuperLU (`splu`,
+NavierStokes_Solver.py:176-192), whose default column order is COLAMD: a fill-reducing order.  The line
+condensation of velocity_solve.py eliminates in line order instead -- every element column's interior, then a
+block-tridiagonal system over the N_ex + 1 interface lines whose blocks are DENSE (m x m, m = 2 N_y): 28.9 of
+the 42.3 GB a cfg5 solve reads are those line blocks (tools/nd_model.py, profiles/r06/velocity/nd_model.json).
+This module orders the same Jacobian by nested dissection of the element grid, the structured-mesh analogue of
+a fill-reducing order:
+
+* leaves = elements.  Element e's matrix A_e (the element's share of the assembled operator: the x and y rows
+  of its own GLL tables with the element's weights, the mass product, the pointwise Jacobian terms on the
+  element that owns the node -- sum_e A_e is the assembled Jacobian) is split into its interior unknowns i
+  (ncomp (P-1)^2) and its boundary unknowns b (ncomp 4P); Xi = A_ii^-1, the update U_e = A_bb - A_bi Xi A_ib.
+* fronts = separators.  The element grid is bisected recursively along its longer side at the middle element
+  edge; the separator S of a piece is the skeleton nodes of that edge line strictly inside the piece, and its
+  front also holds B, the piece's perimeter nodes that belong to ancestor separators.  The front matrix over
+  [S; B] is the extend-add of its two children's updates; S^-1 is formed (batched, pivoted inside the block)
+  and the front keeps Fw = [S^-1; A_BS S^-1] ((|S| + |B|) x |S|) and V = S^-1 A_SB (|S| x |B|), and passes
+  U = A_BB - A_BS V to its parent.
+* Dirichlet rows (the whole perimeter, every component: the velocity mask of NavierStokes_Solver.py:78-94) are
+  identity rows: x_D = b_D.  They are taken out before the elimination -- the right-hand side is lifted,
+  b_N -= A_ND b_D (the perimeter elements' coupling blocks), and D appears in no front.
+* Solve = lift, leaf forward ([Xi; A_bi Xi] b_i: y_i and the boundary update), front forward level by level
+  from the deepest, front back substitution x_S = y_S - V x_B from the root down, leaf back substitution
+  x_i = y_i - V_e x_b.  Every step is one streaming GEMV launch over all fronts of a level (sem_front_gemv)
+  plus, after a forward step, one deterministic scatter (sem_front_scatter: each target sums its <= 4
+  contributions in a fixed order), so results are bitwise reproducible and the solve is graph-capturable.
+
+Bytes per solve (cfg5: 128^2 elements, P = 12): the leaves' [Xi; A_bi Xi] and V_e, the fronts' Fw and V --
+20 GB against the line condensation's 42.3 (model: tools/nd_model.py).  The strip partition (strip_solve.py)
+keeps the line condensation.  The algebra runs on any torch device: the CPU path (a per-front loop over the
+same tables) is what the CPU tests check against SciPy's sparse solve.
+"""
+import functools
+import os
+
+import numpy as np
+import torch
+
+from .velocity_solve import VelocityJacobianSolver, batched_inverse, pivot_inverse
+
+ALL_SIDES = 15   # SEM_SIDE_W | E | S | N
+
+
+class NDTree:
+    """Symbolic analysis of the nested dissection for an nex x ney mesh of order P, ncomp unknowns per node, the
+    whole perimeter Dirichlet.  Unknowns are addressed by their flat index in the solver's (NX, ncomp N_y) line
+    array: gx m + c N_y + gy (m = ncomp N_y)."""
+
+    def __init__(self, P, nex, ney, nc):
+        if P < 2:
+            raise ValueError("nested dissection needs P >= 2 (element interiors)")
+        self.P, self.nex, self.ney, self.nc = P, nex, ney, nc
+        self.NY, self.NX = ney * P + 1, nex * P + 1
+        self.m = nc * self.NY
+        NY, NX, m = self.NY, self.NX, self.m
+        # element-local order: interior (i, c, j) for i, j in 1..P-1 (the condensed layout's order), then the
+        # boundary (i, c, j) for the nodes with i or j in {0, P}, x-major
+        loc = np.full((P + 1, P + 1, nc), -1, dtype=np.int64)
+        pi, pj, pc = [], [], []
+        for i in range(1, P):
+            for c in range(nc):
+                for j in range(1, P):
+                    loc[i, j, c] = len(pi)
+                    pi.append(i), pj.append(j), pc.append(c)
+        self.ni = len(pi)
+        for i in range(P + 1):
+            for c in range(nc):
+                for j in range(P + 1):
+                    if i in (0, P) or j in (0, P):
+                        loc[i, j, c] = len(pi)
+                        pi.append(i), pj.append(j), pc.append(c)
+        self.ne = len(pi)
+        self.nb = self.ne - self.ni
+        self.loc = loc
+        self.pos_i, self.pos_j, self.pos_c = (np.asarray(a, dtype=np.int64) for a in (pi, pj, pc))
+        E = nex * ney
+        ex, ey = np.divmod(np.arange(E, dtype=np.int64), ney)      # element e = ex ney + ey
+        self.ex, self.ey = ex, ey
+        gx = ex[:, None] * P + self.pos_i[None, :]
+        gy = ey[:, None] * P + self.pos_j[None, :]
+        self.eflat = gx * m + self.pos_c[None, :] * NY + gy          # (E, ne)
+        self.enode = gx * NY + gy                                    # global node (x-major) of each position
+        self.eD = (gx == 0) | (gx == NX - 1) | (gy == 0) | (gy == NY - 1)
+        self.fronts = []
+        self.root = self._rec(0, nex, 0, ney, 0)
+        self.depth = max((f["depth"] for f in self.fronts), default=-1)
+        self._child_maps()
+
+    # ------------------------------------------------------------------ symbolic
+    def _is_d(self, gx, gy):
+        return (gx == 0) | (gx == self.NX - 1) | (gy == 0) | (gy == self.NY - 1)
+
+    def _flats(self, gx, gy):
+        """Flat indices of nodes (gx, gy) for every component, node-major then component."""
+        c = np.arange(self.nc, dtype=np.int64)
+        return (gx[:, None] * self.m + c[None, :] * self.NY + gy[:, None]).reshape(-1)
+
+    def _rec(self, x0, x1, y0, y1, depth):
+        P, ney = self.P, self.ney
+        if x1 - x0 == 1 and y1 - y0 == 1:
+            return ("e", x0 * ney + y0)
+        if x1 - x0 >= y1 - y0:
+            xm = (x0 + x1) // 2
+            gy = np.arange(y0 * P + 1, y1 * P, dtype=np.int64)
+            gx = np.full_like(gy, xm * P)
+            c0, c1 = self._rec(x0, xm, y0, y1, depth + 1), self._rec(xm, x1, y0, y1, depth + 1)
+            # component-major along the line: contiguous runs of the line array
+            S = (xm * P * self.m + np.arange(self.nc, dtype=np.int64)[:, None] * self.NY + gy[None, :]).reshape(-1)
+        else:
+            ym = (y0 + y1) // 2
+            gx = np.arange(x0 * P + 1, x1 * P, dtype=np.int64)
+            gy = np.full_like(gx, ym * P)
+            c0, c1 = self._rec(x0, x1, y0, ym, depth + 1), self._rec(x0, x1, ym, y1, depth + 1)
+            S = self._flats(gx, gy)
+        # the piece's perimeter nodes on ancestor separators (the domain perimeter is Dirichlet: not a front node)
+        nodes = []
+        ys = np.arange(y0 * P, y1 * P + 1, dtype=np.int64)
+        xs = np.arange(x0 * P, x1 * P + 1, dtype=np.int64)
+        if x0 > 0:
+            nodes.append(np.stack((np.full_like(ys, x0 * P), ys), 1))
+        if x1 < self.nex:
+            nodes.append(np.stack((np.full_like(ys, x1 * P), ys), 1))
+        if y0 > 0:
+            nodes.append(np.stack((xs, np.full_like(xs, y0 * P)), 1))
+        if y1 < self.ney:
+            nodes.append(np.stack((xs, np.full_like(xs, y1 * P)), 1))
+        if nodes:
+            nd = np.unique(np.concatenate(nodes), axis=0)
+            nd = nd[~self._is_d(nd[:, 0], nd[:, 1])]
+            B = np.sort(self._flats(nd[:, 0], nd[:, 1]))
+        else:
+            B = np.zeros(0, dtype=np.int64)
+        fid = len(self.fronts)
+        self.fronts.append(dict(depth=depth, S=S, B=B, children=(c0, c1)))
+        return ("f", fid)
+
+    def _child_maps(self):
+        """For every front, each child's update rows as positions in the front's [S; B] order (-1: Dirichlet)."""
+        for f in self.fronts:
+            key = np.concatenate((f["S"], f["B"]))
+            order = np.argsort(key, kind="stable")
+            skey = key[order]
+            maps = []
+            for kind, cid in f["children"]:
+                ck = self.eflat[cid, self.ni:] if kind == "e" else self.fronts[cid]["B"]
+                p = np.searchsorted(skey, ck)
+                p = np.minimum(p, len(skey) - 1)
+                hit = skey[p] == ck
+                pos = np.where(hit, order[p], -1)
+                if kind == "e":
+                    if np.any(~hit & ~self.eD[cid, self.ni:]):
+                        raise AssertionError("nested dissection: an element boundary node outside its parent front")
+                elif not hit.all():
+                    raise AssertionError("nested dissection: a child front's boundary outside its parent front")
+                maps.append(pos)
+            f["maps"] = maps
+
+    def bytes_per_solve(self):
+        """Operator bytes one solve reads: lift, leaves ([Xi; A_bi Xi], V_e), fronts (Fw, V)."""
+        E = self.nex * self.ney
+        nper = int(np.any(self.eD[:, self.ni:], axis=1).sum())
+        leaf = E * (self.ne * self.ni + self.ni * self.nb)
+        fr = sum(len(f["S"]) * (len(f["S"]) + 2 * len(f["B"])) for f in self.fronts)
+        return 8 * (nper * self.ne * self.nb + leaf + fr)
+
+
+@functools.lru_cache(maxsize=8)
+def nd_tree(P, nex, ney, nc):
+    return NDTree(P, nex, ney, nc)
+
+
+def element_matrices(tree, elems, dx, dy, Ks, Gs, w, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None,
+                     cv=None, juu=None, juv=None, jvu=None, jvv=None, device="cpu"):
+    """Element shares A_e (len(elems), ne, ne) of the Jacobian in the tree's element-local order, Dirichlet rows
+    zero (their columns kept: the lift reads them).  The operator is the one sem_velocity_blocks writes
+    (sem_amd/csrc/ns_velocity.hip): with f_Kx = cK dy/dx, f_Ky = cK dx/dy, f_M = cM dx dy / 4, f_X = cX dy/2,
+    f_Y = cY dx/2 and the element-local GLL weights w,
+        x row (i, j) -> (k, j): w_j (f_Kx Ks[i][k] + f_X cu(node) Gs[i][k])
+        y row (i, j) -> (i, q): w_i (f_Ky Ks[j][q] + f_Y cv(node) Gs[j][q])
+        mass: f_M w_i w_j;  juu / jvv on the diagonal, juv / jvu across the components, on the owner element
+    -- the element sums of these are the assembled rows (SEM.py:170-245, NavierStokes_Solver.py:123-136)."""
+    t = tree
+    P, nc, ne = t.P, t.nc, t.ne
+    dev = torch.device(device)
+    f64 = dict(dtype=torch.float64, device=dev)
+    e = torch.as_tensor(np.asarray(elems, dtype=np.int64), device=dev)
+    E = e.numel()
+    ex, ey = e // t.ney, e % t.ney
+    fKx, fKy = c_stiff * (dy / dx), c_stiff * (dx / dy)
+    fM, fX, fY = c_mass * (dx / 2.0) * (dy / 2.0), c_gradx * (dy / 2.0), c_grady * (dx / 2.0)
+    Ks, Gs, w = (torch.as_tensor(np.asarray(a), **f64) for a in (Ks, Gs, w))
+    n = P + 1
+    ar = torch.arange(n, device=dev)
+    loc = torch.as_tensor(t.loc, device=dev)                          # (i, j, c) -> position
+    node = (ex[:, None, None] * P + ar[None, :, None]) * t.NY + ey[:, None, None] * P + ar[None, None, :]  # (E, i, j)
+
+    def pointwise(v, default):
+        if v is None:
+            return torch.full((E, n, n), float(default), **f64)
+        return v.to(**f64).reshape(-1)[node]
+
+    cuN, cvN = pointwise(cu, 1.0), pointwise(cv, 1.0)
+    A = torch.zeros((E, ne * ne), **f64)
+    for c in range(nc):
+        # x couplings: rows (i, j, c), columns (k, j, c)
+        r = loc[:, :, c][:, :, None].expand(n, n, n)                     # (i, j, k)
+        col = loc[:, :, c].t()[None, :, :].expand(n, n, n)               # loc[k, j, c] at (i, j, k)
+        vx = w[None, None, :, None] * (fKx * Ks[None, :, None, :] + fX * cuN[:, :, :, None] * Gs[None, :, None, :])
+        A.scatter_add_(1, (r * ne + col).reshape(1, -1).expand(E, -1), vx.reshape(E, -1))
+        # y couplings: rows (i, j, c), columns (i, q, c)
+        r = loc[:, :, c][:, :, None].expand(n, n, n)                     # (i, j, q)
+        col = loc[:, :, c][:, None, :].expand(n, n, n)                   # loc[i, q, c]
+        vy = w[None, :, None, None] * (fKy * Ks[None, None, :, :] + fY * cvN[:, :, :, None] * Gs[None, None, :, :])
+        A.scatter_add_(1, (r * ne + col).reshape(1, -1).expand(E, -1), vy.reshape(E, -1))
+    own = (((ar[None, :, None] < P) | (ex[:, None, None] == t.nex - 1))
+           & ((ar[None, None, :] < P) | (ey[:, None, None] == t.ney - 1))).to(torch.float64)   # (E, i, j)
+    diag = fM * w[:, None] * w[None, :]
+    for c in range(nc):
+        d = loc[:, :, c]
+        jd = (juu if c == 0 else jvv)
+        dv = diag[None].expand(E, n, n).clone()
+        if jd is not None:
+            dv = dv + own * pointwise(jd, 0.0)
+        A.scatter_add_(1, (d * ne + d).reshape(1, -1).expand(E, -1), dv.reshape(E, -1))
+        if nc == 2:
+            jc = juv if c == 0 else jvu
+            if jc is not None:
+                o = loc[:, :, 1 - c]
+                A.scatter_add_(1, (d * ne + o).reshape(1, -1).expand(E, -1), (own * pointwise(jc, 0.0)).reshape(E, -1))
+    A = A.view(E, ne, ne)
+    rowD = torch.as_tensor(t.eD, device=dev)[e]                          # (E, ne)
+    A.masked_fill_(rowD[:, :, None], 0.0)
+    return A
+
+
+def _gll_tables(P):
+    from .. import GLL
+    return GLL.standard_stiffness_matrix(P), GLL.standard_gradient_matrix(P), GLL.standard_nodes(P)[1]
+
+
+class NestedDissectionSolver(VelocityJacobianSolver):
+    """x = J^-1 b for the velocity Jacobian J of one linearisation by nested dissection (module docstring).  Same
+    interface as VelocityJacobianSolver (solve, solve1, _solve_lines, set_operator, check_refinement, capture);
+    factor with factor_mesh(mesh, **kw) (the device mesh) or factor_coeffs(dx, dy, **kw) (any torch device)."""
+
+    def __init__(self, P, nex, ney, device, ncomp=2):
+        super().__init__(P, nex, ney, device, interior="nested", sweep="thomas", ncomp=ncomp)
+        self.interior = "nd"
+        self.tree = nd_tree(P, nex, ney, ncomp)
+        self.chunk_elems = int(os.environ.get("SEM_ND_CHUNK", "2048"))
+
+    # ------------------------------------------------------------------ factorisation
+    def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
+        return self.factor_coeffs(mesh.dx, mesh.dy, **kw)
+
+    def factor_coeffs(self, dx, dy, dir_mask=None, dir_sides=ALL_SIDES, ncomp=None, **kw):
+        """Factor the Jacobian with coefficients kw (c_mass, c_stiff, c_gradx, c_grady, cu, cv, juu, juv, jvu, jvv;
+        the keywords of sem_velocity_blocks) on a mesh of element widths dx, dy; the Dirichlet rows must be the
+        whole perimeter (dir_sides = all four, no explicit mask)."""
+        if dir_mask is not None or dir_sides != ALL_SIDES:
+            raise ValueError("nested dissection needs the whole perimeter Dirichlet (side bits, no mask)")
+        t, dev = self.tree, self.device
+        Ks, Gs, w = _gll_tables(self.P)
+        E = self.nex * self.ney
+        ni, nb, ne = t.ne - t.nb, t.nb, t.ne
+        z = dict(dtype=torch.float64, device=dev)
+        self._leafF = torch.empty((E, ne, ni), **z)          # [Xi; A_bi Xi]
+        self._leafV = torch.empty((E, ni, nb), **z)          # Xi A_ib
+        U_leaf = torch.empty((E, nb, nb), **z)
+        per = np.nonzero(np.any(t.eD[:, ni:], axis=1))[0]    # elements with Dirichlet boundary nodes
+        self._per = per
+        self._lift = torch.empty((len(per), ne, nb), **z)
+        per_slot = np.full(E, -1, dtype=np.int64)
+        per_slot[per] = np.arange(len(per))
+        eDb = torch.as_tensor(t.eD[:, ni:], device=dev)
+        with self._phase("nd_leaves"):
+            for e0 in range(0, E, self.chunk_elems):
+                e1 = min(E, e0 + self.chunk_elems)
+                A = element_matrices(t, np.arange(e0, e1), dx, dy, Ks, Gs, w, device=dev, **kw)
+                dcol = eDb[e0:e1]                                      # (q, nb) Dirichlet boundary columns
+                ps = per_slot[e0:e1]
+                sel = np.nonzero(ps >= 0)[0]
+                if len(sel):
+                    s_t = torch.as_tensor(sel, device=dev)
+                    self._lift[torch.as_tensor(ps[sel], device=dev)] = A[s_t, :, ni:] * dcol[s_t][:, None, :].to(
+                        torch.float64)
+                A[:, :, ni:].masked_fill_(dcol[:, None, :], 0.0)        # D columns: lifted, out of the elimination
+                Aii, Aib = A[:, :ni, :ni], A[:, :ni, ni:]
+                Abi, Abb = A[:, ni:, :ni], A[:, ni:, ni:]
+                Xi = batched_inverse(Aii.contiguous())
+                V = Xi @ Aib
+                self._leafF[e0:e1, :ni] = Xi
+                self._leafF[e0:e1, ni:] = Abi @ Xi
+                self._leafV[e0:e1] = V
+                U_leaf[e0:e1] = Abb - Abi @ V
+                del A, Xi, V
+        self._factor_fronts(U_leaf)
+        del U_leaf
+        self._build_steps()
+        self.factored = True
+
+    def _factor_fronts(self, U_leaf):
+        """Fronts by depth (deepest first), batched per (|S|, |B|) shape group."""
+        t, dev = self.tree, self.device
+        z = dict(dtype=torch.float64, device=dev)
+        self._fw = [None] * len(t.fronts)      # (group tensor, slot) of Fw
+        self._fv = [None] * len(t.fronts)      # (group tensor, slot) of V
+        fu = [None] * len(t.fronts)            # (group tensor, slot) of U
+        by_depth = {}
+        for fid, f in enumerate(t.fronts):
+            by_depth.setdefault(f["depth"], {}).setdefault((len(f["S"]), len(f["B"])), []).append(fid)
+        with self._phase("nd_fronts"):
+            for depth in sorted(by_depth, reverse=True):
+                for (s, b), fids in sorted(by_depth[depth].items()):
+                    nf, n = len(fids), s + b
+                    F = torch.zeros(nf * n * n + 1, **z)           # + 1: the Dirichlet sink
+                    for k in range(2):
+                        self._extend_add(F, n, fids, k, U_leaf, fu)
+                    F = F[:-1].view(nf, n, n)
+                    Ass = F[:, :s, :s]
+                    if s >= 1024:
+                        Sinv = torch.stack([pivot_inverse(Ass[q].contiguous()) for q in range(nf)])
+                    else:
+                        Sinv = batched_inverse(Ass.contiguous())
+                    Fw = torch.empty((nf, n, s), **z)
+                    Fw[:, :s] = Sinv
+                    if b:
+                        Abs, Asb, Abb = F[:, s:, :s], F[:, :s, s:], F[:, s:, s:]
+                        Fw[:, s:] = Abs @ Sinv
+                        V = Sinv @ Asb
+                        U = Abb - Abs @ V
+                    else:
+                        V = U = None
+                    del F, Sinv
+                    for q, fid in enumerate(fids):
+                        self._fw[fid] = (Fw, q)
+                        self._fv[fid] = (V, q) if b else None
+                        fu[fid] = (U, q) if b else None
+                # children's updates are no longer needed once every front of this depth has its matrix
+                for fid in [f for g in by_depth[depth].values() for f in g]:
+                    for kind, cid in t.fronts[fid]["children"]:
+                        if kind == "f":
+                            fu[cid] = None
+
+    def _extend_add(self, F, n, fids, k, U_leaf, fu):
+        """F[slot] += child k's update of every front of the group, scattered by the child's position map (distinct
+        destinations within one call; the Dirichlet rows / columns go to the sink entry F[-1])."""
+        t, dev = self.tree, self.device
+        sink = F.numel() - 1
+        groups = {}
+        for q, fid in enumerate(fids):
+            kind, cid = t.fronts[fid]["children"][k]
+            src = ("leaf", None) if kind == "e" else (id(fu[cid][0]), fu[cid][0])
+            groups.setdefault(src[0], (src[1], []))[1].append((q, kind, cid))
+        for _, (Ut, items) in groups.items():
+            for c0 in range(0, len(items), 4096):
+                part = items[c0:c0 + 4096]
+                q = torch.as_tensor([it[0] for it in part], device=dev)
+                if part[0][1] == "e":
+                    cids = [it[2] for it in part]
+                    src = U_leaf[torch.as_tensor(cids, device=dev)]
+                else:
+                    src = Ut[torch.as_tensor([fu[it[2]][1] for it in part], device=dev)]
+                pos = torch.as_tensor(np.stack([t.fronts[fids[it[0]]]["maps"][k] for it in part]), device=dev)
+                bad = pos < 0
+                dest = q[:, None, None] * (n * n) + pos[:, :, None] * n + pos[:, None, :]
+                dest = dest.masked_fill(bad[:, :, None] | bad[:, None, :], sink)
+                F.index_put_((dest.reshape(-1),), src.reshape(-1), accumulate=True)
+
+    # ------------------------------------------------------------------ solve plan
+    def _build_steps(self):
+        """The solve as a list of steps over flat line-array indices: ("fwd", launch, scatter) and ("back", launch).
+        A launch is a list of (operator view (R x K), xidx, out) per front: fwd writes stage[out:out+R], back
+        subtracts from W[out indices]."""
+        t = self.tree
+        ni, ne = t.ni, t.ne
+        steps = []
+        # lift: W_N -= A_ND b_D over the perimeter elements
+        if len(self._per):
+            items, tgt, src = [], [], []
+            for q, e in enumerate(self._per):
+                items.append((self._lift, q, t.eflat[e, ni:], q * ne))
+                keep = ~t.eD[e]
+                tgt.append(t.eflat[e][keep])
+                src.append(q * ne + np.nonzero(keep)[0])
+            steps.append(("fwd", items, self._scatter_plan(np.zeros(0, np.int64), np.zeros(0, np.int64),
+                                                           np.concatenate(tgt), np.concatenate(src))))
+        # leaves forward
+        E = self.nex * self.ney
+        items, ct, cs, bt, bs = [], [], [], [], []
+        for e in range(E):
+            items.append((self._leafF, e, t.eflat[e, :ni], e * ne))
+            ct.append(t.eflat[e, :ni])
+            cs.append(e * ne + np.arange(ni))
+            keep = ~t.eD[e, ni:]
+            bt.append(t.eflat[e, ni:][keep])
+            bs.append(e * ne + ni + np.nonzero(keep)[0])
+        steps.append(("fwd", items, self._scatter_plan(np.concatenate(ct), np.concatenate(cs), np.concatenate(bt),
+                                                       np.concatenate(bs))))
+        levels = {}
+        for fid, f in enumerate(t.fronts):
+            levels.setdefault(f["depth"], []).append(fid)
+        for depth in sorted(levels, reverse=True):
+            items, ct, cs, bt, bs = [], [], [], [], []
+            off = 0
+            for fid in levels[depth]:
+                f = t.fronts[fid]
+                s, b = len(f["S"]), len(f["B"])
+                Fw, q = self._fw[fid]
+                items.append((Fw, q, f["S"], off))
+                ct.append(f["S"])
+                cs.append(off + np.arange(s))
+                bt.append(f["B"])
+                bs.append(off + s + np.arange(b))
+                off += s + b
+            steps.append(("fwd", items, self._scatter_plan(np.concatenate(ct), np.concatenate(cs),
+                                                           np.concatenate(bt), np.concatenate(bs))))
+        for depth in sorted(levels):
+            items = []
+            for fid in levels[depth]:
+                f = t.fronts[fid]
+                if len(f["B"]) == 0:
+                    continue
+                V, q = self._fv[fid]
+                items.append((V, q, f["B"], f["S"]))
+            if items:
+                steps.append(("back", items))
+        items = []
+        for e in range(E):
+            xb = np.where(t.eD[e, ni:], -1, t.eflat[e, ni:])
+            items.append((self._leafV, e, xb, t.eflat[e, :ni]))
+        steps.append(("back", items))
+        self._steps = steps
+        self._stage_len = max(sum(it[0].shape[1] for it in st[1]) for st in steps if st[0] == "fwd")
+        self._hip = self._hip_plan() if self.device.type == "cuda" else None
+
+    @staticmethod
+    def _scatter_plan(copy_tgt, copy_src, acc_tgt, acc_src):
+        """Copy targets (W[t] = stage[s], one source each) and accumulation targets (W[t] -= sum of stage[s], up to
+        four sources, summed in increasing source order)."""
+        order = np.lexsort((acc_src, acc_tgt))
+        at, asrc = acc_tgt[order], acc_src[order]
+        uniq, start, cnt = np.unique(at, return_index=True, return_counts=True)
+        if len(cnt) and cnt.max() > 4:
+            raise AssertionError("nested dissection: a node with more than four contributions in one step")
+        src4 = np.full((len(uniq), 4), -1, dtype=np.int64)
+        rank = np.arange(len(at)) - np.repeat(start, cnt)
+        src4[np.repeat(np.arange(len(uniq)), cnt), rank] = asrc
+        return dict(copy_tgt=copy_tgt.astype(np.int64), copy_src=copy_src.astype(np.int64), acc_tgt=uniq,
+                    acc_src=src4)
+
+    # ------------------------------------------------------------------ solve
+    def _solve_lines_once(self, B):
+        if self.device.type == "cuda":
+            return self._solve_lines_hip(B)
+        W = B.reshape(-1).clone()
+        Wz = torch.cat((W, W.new_zeros(1)))      # index -1 reads the trailing zero
+        stage = W.new_zeros(self._stage_len)
+        dev = W.device
+        for st in self._steps:
+            if st[0] == "fwd":
+                for T, q, xidx, off in st[1]:
+                    x = Wz[torch.as_tensor(xidx, device=dev)]
+                    stage[off:off + T.shape[1]] = T[q] @ x
+                sc = st[2]
+                ct, cs, at, a4 = (torch.as_tensor(sc[k], device=dev) for k in ("copy_tgt", "copy_src", "acc_tgt",
+                                                                                "acc_src"))
+                Wz[ct] = stage[cs]
+                v = Wz[at]
+                for k in range(4):
+                    s = a4[:, k]
+                    v = v - torch.where(s >= 0, stage[s.clamp(min=0)], torch.zeros_like(v))
+                Wz[at] = v
+            else:
+                for T, q, xidx, yidx in st[1]:
+                    x = Wz[torch.as_tensor(xidx, device=dev)]
+                    y = torch.as_tensor(yidx, device=dev)
+                    Wz[y] = Wz[y] - T[q] @ x
+        return Wz[:-1].view(self.NX, self.m)
+
+    def _hip_plan(self):
+        """Device tables of every step (sem_front_gemv descriptors, sem_front_scatter index arrays), checked on the
+        host against the line array and the stage buffer before anything is launched."""
+        from .. import _lib
+        dev = self.device
+        nW = self.NX * self.m
+        self._stage = torch.zeros(self._stage_len, dtype=torch.float64, device=dev)
+        plan = []
+
+        def i32(a):
+            a = np.ascontiguousarray(a, dtype=np.int64)
+            if a.size and (a.min() < -1 or a.max() >= 2 ** 31 - 1):
+                raise AssertionError("nested dissection: index outside int32")
+            return torch.as_tensor(a.astype(np.int32), device=dev)
+
+        for st in self._steps:
+            items, back = st[1], st[0] == "back"
+            nf = len(items)
+            ptr = np.empty(nf, dtype=np.int64)
+            dims = np.zeros((nf, 4), dtype=np.int64)
+            xoff = np.zeros(nf, dtype=np.int64)
+            yoff = np.zeros(nf, dtype=np.int64)
+            xs, ys = [], []
+            xo = yo = 0
+            for k, (T, q, xidx, out) in enumerate(items):
+                R, K = T.shape[1], T.shape[2]
+                if T.stride(2) != 1 or T.stride(1) != K or K % 2 or T.dtype != torch.float64 or T.device != dev:
+                    raise AssertionError("nested dissection: operators must be contiguous float64 rows of even length")
+                ptr[k] = T.data_ptr() + q * T.stride(0) * 8
+                if ptr[k] % 16 or not 0 <= q < T.shape[0]:
+                    raise AssertionError("nested dissection: operator rows must be 16-byte aligned")
+                dims[k, :3] = (R, K, K)
+                if len(xidx) != K:
+                    raise AssertionError("nested dissection: operand count differs from the operator width")
+                xoff[k] = xo
+                xs.append(xidx)
+                xo += K
+                if back:
+                    if len(out) != R:
+                        raise AssertionError("nested dissection: target count differs from the operator height")
+                    yoff[k] = yo
+                    ys.append(out)
+                    yo += R
+                else:
+                    if out < 0 or out + R > self._stage_len:
+                        raise AssertionError("nested dissection: stage overflow")
+                    yoff[k] = out
+            xidx = np.concatenate(xs)
+            if xidx.size and (xidx.min() < -1 or xidx.max() >= nW):
+                raise AssertionError("nested dissection: operand index outside the line array")
+            if back:
+                yidx = np.concatenate(ys)
+                if yidx.min() < 0 or yidx.max() >= nW or len(np.unique(yidx)) != len(yidx):
+                    raise AssertionError("nested dissection: back-substitution targets must be distinct line entries")
+            R = dims[:, 0]
+            rows = 16 if int(((R + 15) // 16).sum()) >= 2048 else 4
+            nt = (R + rows - 1) // rows
+            tiles = np.stack((np.repeat(np.arange(nf), nt),
+                              np.concatenate([np.arange(n) * rows for n in nt])), 1)
+            keep = dict(ptr=torch.as_tensor(ptr, device=dev), dims=i32(dims), xoff=torch.as_tensor(xoff, device=dev),
+                        yoff=torch.as_tensor(yoff, device=dev), tiles=i32(tiles), xidx=i32(xidx),
+                        yidx=i32(yidx) if back else None)
+            d = _lib.SemFrontLaunch(len(tiles), rows, int(dims[:, 1].max()), int(back), keep["ptr"].data_ptr(),
+                                    keep["dims"].data_ptr(), keep["xoff"].data_ptr(), keep["yoff"].data_ptr(),
+                                    keep["tiles"].data_ptr(), keep["xidx"].data_ptr(),
+                                    keep["yidx"].data_ptr() if back else None, None,
+                                    None if back else self._stage.data_ptr())
+            sc = None
+            if not back:
+                p = st[2]
+                for a, hi in ((p["copy_tgt"], nW), (p["acc_tgt"], nW)):
+                    if a.size and (a.min() < 0 or a.max() >= hi):
+                        raise AssertionError("nested dissection: scatter target outside the line array")
+                for a in (p["copy_src"], p["acc_src"]):
+                    if a.size and (a.min() < -1 or a.max() >= self._stage_len):
+                        raise AssertionError("nested dissection: scatter source outside the stage")
+                if len(np.unique(np.concatenate((p["copy_tgt"], p["acc_tgt"])))) != len(p["copy_tgt"]) + len(
+                        p["acc_tgt"]):
+                    raise AssertionError("nested dissection: scatter targets must be distinct")
+                sc = dict(n_copy=len(p["copy_tgt"]), ct=i32(p["copy_tgt"]), cs=i32(p["copy_src"]),
+                          n_acc=len(p["acc_tgt"]), at=i32(p["acc_tgt"]), a4=i32(p["acc_src"]).contiguous())
+            plan.append((d, keep, sc))
+        return plan
+
+    def _solve_lines_hip(self, B):
+        """The steps on the device: one sem_front_gemv per level and direction, one sem_front_scatter after each
+        forward level (module docstring)."""
+        import ctypes as C
+        from .. import _lib
+        lib = _lib.load()
+        W = B.reshape(-1).clone()
+        st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        for d, _, sc in self._hip:
+            d.W = W.data_ptr()
+            _lib.check(lib.sem_front_gemv(C.byref(d), st))
+            if sc is not None:
+                _lib.check(lib.sem_front_scatter(sc["n_copy"], sc["ct"].data_ptr(), sc["cs"].data_ptr(), sc["n_acc"],
+                                                 sc["at"].data_ptr(), sc["a4"].data_ptr(), self._stage.data_ptr(),
+                                                 W.data_ptr(), st))
+        return W.view(self.NX, self.m)
