@@ -393,10 +393,12 @@ int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, i
  * 16-byte aligned), its K_f operand positions in W at xidx[xoff[f] ..] (-1: a zero operand), and
  *   back = 0: stage[yoff[f] + r] = (A_f x)_r
  *   back = 1: W[yidx[yoff[f] + r]] -= (A_f x)_r   (targets distinct and not operands of the same launch).
- * tiles[2 b], tiles[2 b + 1] = (front, first row) of workgroup b; rows = 16 or 4 rows per workgroup; kmax >= every
- * K_f of the launch (<= 8192).  All arrays are device memory; deterministic (fixed summation order). */
+ * tiles[2 b], tiles[2 b + 1] = (front, first row) of workgroup b; `lanes` lanes per operator row and `rows` rows
+ * per workgroup, one of (64, 16 | 4), (32, 16 | 8), (16, 32 | 16), (8, 64 | 32), (4, 128 | 64) (short rows take
+ * fewer lanes); kmax >= every K_f of the launch (<= 8192).  All arrays are device memory; deterministic (fixed
+ * summation order for a given `lanes`). */
 typedef struct sem_front_launch {
-  int ntiles, rows, kmax, back;
+  int ntiles, rows, lanes, kmax, back;
   const int64_t* op;
   const int32_t* dims;
   const int64_t* xoff;
@@ -408,6 +410,12 @@ typedef struct sem_front_launch {
   double* stage;
 } sem_front_launch;
 int sem_front_gemv(const sem_front_launch* d, void* stream);
+/* stage[i stride + out_off + r] = sum_q coef[(i nrows + r) nnz + q] stage[i stride + pat[r nnz + q]] for items
+ * i < nitems, rows r < nrows (pattern shared by the items; entries pat[.] < stride and out_off + nrows <= stride,
+ * the operand and output ranges of an item disjoint): the leaves' boundary update A_bi y_i of the nested-dissection
+ * forward solve, from the P - 1 couplings of each element-boundary unknown to its line or column.  Device memory. */
+int sem_front_sparse_rows(int nitems, int nrows, int nnz, const double* coef, const int32_t* pat, double* stage,
+                          int64_t stride, int64_t out_off, void* stream);
 /* The write-back of a forward step: W[copy_tgt[i]] = stage[copy_src[i]] (i < ncopy) and
  * W[acc_tgt[j]] -= stage[s] for s = acc_src4[4 j + k], k = 0..3 in order, skipping s = -1 (j < nacc; acc_src4
  * 16-byte aligned).  Targets distinct.  Device memory; stream-ordered. */

@@ -65,7 +65,8 @@ class SemNsDesc(C.Structure):
 
 
 class SemFrontLaunch(C.Structure):
-    _fields_ = [("ntiles", C.c_int), ("rows", C.c_int), ("kmax", C.c_int), ("back", C.c_int), ("op", C.c_void_p),
+    _fields_ = [("ntiles", C.c_int), ("rows", C.c_int), ("lanes", C.c_int), ("kmax", C.c_int), ("back", C.c_int),
+                ("op", C.c_void_p),
                 ("dims", C.c_void_p), ("xoff", C.c_void_p), ("yoff", C.c_void_p), ("tiles", C.c_void_p),
                 ("xidx", C.c_void_p), ("yidx", C.c_void_p), ("W", C.c_void_p), ("stage", C.c_void_p)]
 
@@ -122,6 +123,8 @@ _SIGS = {
     "sem_gemv_rows2": (C.c_int, [C.c_int, C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
                                  C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sem_front_gemv": (C.c_int, [C.POINTER(SemFrontLaunch), C.c_void_p]),
+    "sem_front_sparse_rows": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                        C.c_int64, C.c_void_p]),
     "sem_front_scatter": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p]),
     "sem_gemv_rows": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_int64, C.c_void_p, C.c_double,

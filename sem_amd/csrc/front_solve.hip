@@ -5,9 +5,11 @@
 // operator A_f (R_f x K_f, leading dimension ld_f): forward [S^-1; A_BS S^-1] (or [Xi; A_bi Xi] at a leaf),
 // back V = S^-1 A_SB (or Xi A_ib).  A workgroup takes `rows` rows of one front (its tile), gathers the front's
 // K operand values W[xidx[.]] into LDS once (-1: a zero operand), streams its rows with non-temporal 16-byte loads
-// (each operator is read once per solve) and reduces each row across the wave in a fixed order:
+// (each operator is read once per solve), `lanes` lanes per row, and reduces each row across its lanes in a fixed
+// order:
 //   forward: stage[yoff_f + r] = (A_f x)_r
 //   back:    W[yidx[yoff_f + r]] -= (A_f x)_r       (the rows' targets are not operands of the same launch)
+// sem_front_sparse_rows: a leaf's boundary update A_bi y_i from its sparse coupling rows (nnz = P - 1 per row).
 // sem_front_scatter: the forward step's deterministic write-back -- copy targets W[t] = stage[s] (a front's own
 // separator / a leaf's interior) and accumulation targets W[t] -= stage[s_0] .. stage[s_3] (the <= 4 fronts of a
 // level that update a node of an ancestor separator), summed in the order the host sorted them.
@@ -21,20 +23,17 @@ namespace sem {
 
 using dvec2f = double __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ double front_wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
 __device__ __forceinline__ double2 load_nt2(const double* p) {
   const dvec2f v = __builtin_nontemporal_load(reinterpret_cast<const dvec2f*>(p));
   return make_double2(v.x, v.y);
 }
 
-// RW rows per wave (4 waves), U pairs of columns per lane in flight per row
-template <int RW, int U>
+// LPR lanes per row: a wave holds 64 / LPR row groups, each group RW rows in flight, each lane U column pairs per
+// row per iteration (short rows -- the deep fronts' |S| = 22, the leaves' |b| = 96 -- would leave most of a
+// 64-lane row idle).  Rows per workgroup: 4 (64 / LPR) RW.
+template <int LPR, int RW, int U>
 __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch a) {
+  constexpr int G = 64 / LPR;
   extern __shared__ double xs[];
   const int f = a.tiles[2 * blockIdx.x], r0 = a.tiles[2 * blockIdx.x + 1];
   const int R = a.dims[4 * f], K = a.dims[4 * f + 1], ld = a.dims[4 * f + 2];
@@ -45,8 +44,9 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int rb = r0 + wave * RW;
-  if (rb >= R) return;
+  if (r0 + wave * G * RW >= R) return;  // the whole wave beyond the front (groups inside a wave stay together)
+  const int g = lane / LPR, sl = lane % LPR;
+  const int rb = r0 + (wave * G + g) * RW;
   const double* A = reinterpret_cast<const double*>(a.op[f]);
   const double* rows[RW];
 #pragma unroll
@@ -56,14 +56,14 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
   for (int i = 0; i < RW; ++i) acc[i][0] = acc[i][1] = 0.0;
   const int KP = K >> 1;  // K is even (the host checks): column pairs
   const double2* x2 = reinterpret_cast<const double2*>(xs);
-  int u = lane;
-  for (; u + 64 * (U - 1) < KP; u += 64 * U) {
+  int u = sl;
+  for (; u + LPR * (U - 1) < KP; u += LPR * U) {
     double2 av[U][RW], xv[U];
 #pragma unroll
     for (int t = 0; t < U; ++t) {
-      xv[t] = x2[u + 64 * t];
+      xv[t] = x2[u + LPR * t];
 #pragma unroll
-      for (int i = 0; i < RW; ++i) av[t][i] = load_nt2(rows[i] + 2 * (u + 64 * t));
+      for (int i = 0; i < RW; ++i) av[t][i] = load_nt2(rows[i] + 2 * (u + LPR * t));
     }
 #pragma unroll
     for (int t = 0; t < U; ++t)
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
         acc[i][1] = fma(av[t][i].y, xv[t].y, acc[i][1]);
       }
   }
-  for (; u < KP; u += 64) {
+  for (; u < KP; u += LPR) {
     const double2 xv = x2[u];
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
@@ -84,9 +84,11 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
   }
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
-    const double v = front_wave_sum(acc[i][0] + acc[i][1]);
+    double v = acc[i][0] + acc[i][1];
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     const int r = rb + i;
-    if (lane == 0 && r < R) {
+    if (sl == 0 && r < R) {
       if (a.back) {
         const int p = a.yidx[a.yoff[f] + r];
         a.W[p] -= v;
@@ -95,6 +97,24 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
       }
     }
   }
+}
+
+// A leaf's boundary update A_bi y_i, sparse: boundary unknown r of item i couples to nnz interior unknowns of its
+// own line or column (the element's y rows on a horizontal edge, x rows on a vertical edge; none at a corner).
+__global__ __launch_bounds__(256) void front_sparse_rows_kernel(int nitems, int nrows, int nnz,
+                                                                const double* __restrict__ coef,
+                                                                const int32_t* __restrict__ pat, double* stage,
+                                                                int64_t stride, int64_t out_off) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= static_cast<int64_t>(nitems) * nrows) return;
+  const int64_t i = t / nrows;
+  const int r = static_cast<int>(t - i * nrows);
+  const double* c = coef + t * nnz;
+  const int32_t* p = pat + static_cast<int64_t>(r) * nnz;
+  const double* y = stage + i * stride;
+  double v = 0.0;
+  for (int q = 0; q < nnz; ++q) v = fma(c[q], y[p[q]], v);
+  stage[i * stride + out_off + r] = v;
 }
 
 __global__ __launch_bounds__(256) void front_scatter_kernel(int ncopy, const int32_t* __restrict__ ct,
@@ -123,20 +143,41 @@ extern "C" {
 
 int sem_front_gemv(const sem_front_launch* d, void* stream) {
   if (!d) return sem::set_error(SEM_EINVAL, "front_gemv: null descriptor");
-  if (d->ntiles < 0 || d->kmax < 0 || (d->rows != 4 && d->rows != 16))
-    return sem::set_error(SEM_EINVAL, "front_gemv: bad sizes (rows must be 4 or 16)");
+  if (d->ntiles < 0 || d->kmax < 0) return sem::set_error(SEM_EINVAL, "front_gemv: bad sizes");
   if (d->ntiles == 0) return SEM_OK;
   if (!d->op || !d->dims || !d->xoff || !d->yoff || !d->tiles || !d->xidx || !d->W || (d->back ? !d->yidx : !d->stage))
     return sem::set_error(SEM_EINVAL, "front_gemv: null argument");
   const size_t lds = static_cast<size_t>(d->kmax) * sizeof(double);
   if (lds > 64 * 1024) return sem::set_error(SEM_EUNSUPPORTED, "front_gemv: more than 8192 operands per front");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (d->rows == 16)
-    hipLaunchKernelGGL((sem::front_gemv_kernel<4, 2>), dim3(d->ntiles), dim3(256), lds, s, *d);
-  else
-    hipLaunchKernelGGL((sem::front_gemv_kernel<1, 8>), dim3(d->ntiles), dim3(256), lds, s, *d);
+  const dim3 grid(d->ntiles), block(256);
+#define SEM_FRONT_CASE(L, ROWS, RW, U)                                                   \
+  if (d->lanes == L && d->rows == ROWS) {                                                \
+    hipLaunchKernelGGL((sem::front_gemv_kernel<L, RW, U>), grid, block, lds, s, *d);     \
+  } else
+  SEM_FRONT_CASE(64, 16, 4, 2) SEM_FRONT_CASE(64, 4, 1, 8) SEM_FRONT_CASE(32, 16, 2, 2) SEM_FRONT_CASE(32, 8, 1, 4)
+  SEM_FRONT_CASE(16, 32, 2, 2) SEM_FRONT_CASE(16, 16, 1, 4) SEM_FRONT_CASE(8, 64, 2, 2) SEM_FRONT_CASE(8, 32, 1, 2)
+  SEM_FRONT_CASE(4, 128, 2, 2) SEM_FRONT_CASE(4, 64, 1, 2) {
+    return sem::set_error(SEM_EINVAL, "front_gemv: unsupported (lanes, rows): lanes 64/32/16/8/4 with rows "
+                                      "16|4, 16|8, 32|16, 64|32, 128|64");
+  }
+#undef SEM_FRONT_CASE
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("front_gemv launch: ") + hipGetErrorString(e));
+  return SEM_OK;
+}
+
+int sem_front_sparse_rows(int nitems, int nrows, int nnz, const double* coef, const int32_t* pat, double* stage,
+                          int64_t stride, int64_t out_off, void* stream) {
+  if (nitems < 0 || nrows < 0 || nnz < 0 || stride < 0 || out_off < 0 || out_off + nrows > stride)
+    return sem::set_error(SEM_EINVAL, "front_sparse_rows: bad sizes");
+  const int64_t n = static_cast<int64_t>(nitems) * nrows;
+  if (n == 0) return SEM_OK;
+  if (!coef || !pat || !stage) return sem::set_error(SEM_EINVAL, "front_sparse_rows: null argument");
+  hipLaunchKernelGGL(sem::front_sparse_rows_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), nitems, nrows, nnz, coef, pat, stage, stride, out_off);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("front_sparse_rows launch: ") + hipGetErrorString(e));
   return SEM_OK;
 }
 

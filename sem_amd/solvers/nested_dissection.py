@@ -74,6 +74,16 @@ class NDTree:
         self.ne = len(pi)
         self.nb = self.ne - self.ni
         self.loc = loc
+        # A_bi is sparse: a boundary unknown couples to the P - 1 interior unknowns of its own column (y rows of a
+        # horizontal-edge node) or line (x rows of a vertical-edge node), none at a corner; bpat[r] lists them
+        bpat = np.zeros((self.nb, P - 1), dtype=np.int64)
+        for r in range(self.nb):
+            i, j, c = pi[self.ni + r], pj[self.ni + r], pc[self.ni + r]
+            if 0 < i < P:
+                bpat[r] = loc[i, 1:P, c]
+            elif 0 < j < P:
+                bpat[r] = loc[1:P, j, c]
+        self.bpat = bpat
         self.pos_i, self.pos_j, self.pos_c = (np.asarray(a, dtype=np.int64) for a in (pi, pj, pc))
         E = nex * ney
         ex, ey = np.divmod(np.arange(E, dtype=np.int64), ney)      # element e = ex ney + ey
@@ -158,10 +168,10 @@ class NDTree:
             f["maps"] = maps
 
     def bytes_per_solve(self):
-        """Operator bytes one solve reads: lift, leaves ([Xi; A_bi Xi], V_e), fronts (Fw, V)."""
+        """Operator bytes one solve reads: lift, leaves (Xi, the sparse A_bi, V_e), fronts (Fw, V)."""
         E = self.nex * self.ney
         nper = int(np.any(self.eD[:, self.ni:], axis=1).sum())
-        leaf = E * (self.ne * self.ni + self.ni * self.nb)
+        leaf = E * (self.ni * self.ni + self.nb * (self.P - 1) + self.ni * self.nb)
         fr = sum(len(f["S"]) * (len(f["S"]) + 2 * len(f["B"])) for f in self.fronts)
         return 8 * (nper * self.ne * self.nb + leaf + fr)
 
@@ -266,7 +276,9 @@ class NestedDissectionSolver(VelocityJacobianSolver):
         E = self.nex * self.ney
         ni, nb, ne = t.ne - t.nb, t.nb, t.ne
         z = dict(dtype=torch.float64, device=dev)
-        self._leafF = torch.empty((E, ne, ni), **z)          # [Xi; A_bi Xi]
+        self._leafF = torch.empty((E, ni, ni), **z)          # Xi
+        self._leafAc = torch.empty((E, nb, self.P - 1), **z)  # A_bi on its sparsity pattern (tree.bpat)
+        bpat = torch.as_tensor(t.bpat, device=dev)
         self._leafV = torch.empty((E, ni, nb), **z)          # Xi A_ib
         U_leaf = torch.empty((E, nb, nb), **z)
         per = np.nonzero(np.any(t.eD[:, ni:], axis=1))[0]    # elements with Dirichlet boundary nodes
@@ -291,8 +303,12 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 Abi, Abb = A[:, ni:, :ni], A[:, ni:, ni:]
                 Xi = batched_inverse(Aii.contiguous())
                 V = Xi @ Aib
-                self._leafF[e0:e1, :ni] = Xi
-                self._leafF[e0:e1, ni:] = Abi @ Xi
+                self._leafF[e0:e1] = Xi
+                Ac = torch.gather(Abi, 2, bpat[None].expand(e1 - e0, -1, -1))
+                rest = Abi.clone().scatter_(2, bpat[None].expand(e1 - e0, -1, -1), 0.0)
+                if bool(rest.abs().max() != 0):
+                    raise AssertionError("nested dissection: A_bi has entries outside its line / column pattern")
+                self._leafAc[e0:e1] = Ac
                 self._leafV[e0:e1] = V
                 U_leaf[e0:e1] = Abb - Abi @ V
                 del A, Xi, V
@@ -371,9 +387,10 @@ class NestedDissectionSolver(VelocityJacobianSolver):
 
     # ------------------------------------------------------------------ solve plan
     def _build_steps(self):
-        """The solve as a list of steps over flat line-array indices: ("fwd", launch, scatter) and ("back", launch).
-        A launch is a list of (operator view (R x K), xidx, out) per front: fwd writes stage[out:out+R], back
-        subtracts from W[out indices]."""
+        """The solve as a list of steps over flat line-array indices: ("fwd", launch, scatter, sparse) and
+        ("back", launch).  A launch is a list of (operator tensor T, slot q, xidx, out) per front, the operator T[q]
+        (R x K): fwd writes stage[out:out+R], back subtracts from W[out indices]; `sparse` (leaves only) then forms
+        the boundary rows from the stage (sem_front_sparse_rows) before the scatter."""
         t = self.tree
         ni, ne = t.ni, t.ne
         steps = []
@@ -386,8 +403,8 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 tgt.append(t.eflat[e][keep])
                 src.append(q * ne + np.nonzero(keep)[0])
             steps.append(("fwd", items, self._scatter_plan(np.zeros(0, np.int64), np.zeros(0, np.int64),
-                                                           np.concatenate(tgt), np.concatenate(src))))
-        # leaves forward
+                                                           np.concatenate(tgt), np.concatenate(src)), None))
+        # leaves forward: y_i = Xi b_i into stage[e ne + (0 .. ni)], the sparse A_bi y_i into stage[e ne + (ni .. ne)]
         E = self.nex * self.ney
         items, ct, cs, bt, bs = [], [], [], [], []
         for e in range(E):
@@ -398,7 +415,8 @@ class NestedDissectionSolver(VelocityJacobianSolver):
             bt.append(t.eflat[e, ni:][keep])
             bs.append(e * ne + ni + np.nonzero(keep)[0])
         steps.append(("fwd", items, self._scatter_plan(np.concatenate(ct), np.concatenate(cs), np.concatenate(bt),
-                                                       np.concatenate(bs))))
+                                                       np.concatenate(bs)),
+                      dict(coef=self._leafAc, pat=t.bpat, stride=ne, out_off=ni, nitems=E)))
         levels = {}
         for fid, f in enumerate(t.fronts):
             levels.setdefault(f["depth"], []).append(fid)
@@ -416,7 +434,7 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 bs.append(off + s + np.arange(b))
                 off += s + b
             steps.append(("fwd", items, self._scatter_plan(np.concatenate(ct), np.concatenate(cs),
-                                                           np.concatenate(bt), np.concatenate(bs))))
+                                                           np.concatenate(bt), np.concatenate(bs)), None))
         for depth in sorted(levels):
             items = []
             for fid in levels[depth]:
@@ -433,7 +451,8 @@ class NestedDissectionSolver(VelocityJacobianSolver):
             items.append((self._leafV, e, xb, t.eflat[e, :ni]))
         steps.append(("back", items))
         self._steps = steps
-        self._stage_len = max(sum(it[0].shape[1] for it in st[1]) for st in steps if st[0] == "fwd")
+        self._stage_len = max(max(max(it[3] + it[0].shape[1] for it in st[1]),
+                                  st[3]["nitems"] * st[3]["stride"] if st[3] else 0) for st in steps if st[0] == "fwd")
         self._hip = self._hip_plan() if self.device.type == "cuda" else None
 
     @staticmethod
@@ -464,6 +483,11 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 for T, q, xidx, off in st[1]:
                     x = Wz[torch.as_tensor(xidx, device=dev)]
                     stage[off:off + T.shape[1]] = T[q] @ x
+                sp = st[3]
+                if sp is not None:
+                    y = stage[:sp["nitems"] * sp["stride"]].view(sp["nitems"], sp["stride"])
+                    yi = y[:, torch.as_tensor(sp["pat"], device=dev)]                 # (items, nrows, nnz)
+                    y[:, sp["out_off"]:sp["out_off"] + sp["pat"].shape[0]] = (sp["coef"] * yi).sum(-1)
                 sc = st[2]
                 ct, cs, at, a4 = (torch.as_tensor(sc[k], device=dev) for k in ("copy_tgt", "copy_src", "acc_tgt",
                                                                                 "acc_src"))
@@ -535,14 +559,14 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 if yidx.min() < 0 or yidx.max() >= nW or len(np.unique(yidx)) != len(yidx):
                     raise AssertionError("nested dissection: back-substitution targets must be distinct line entries")
             R = dims[:, 0]
-            rows = 16 if int(((R + 15) // 16).sum()) >= 2048 else 4
+            lanes, rows = self._launch_shape(dims[:, 1], R)
             nt = (R + rows - 1) // rows
             tiles = np.stack((np.repeat(np.arange(nf), nt),
                               np.concatenate([np.arange(n) * rows for n in nt])), 1)
             keep = dict(ptr=torch.as_tensor(ptr, device=dev), dims=i32(dims), xoff=torch.as_tensor(xoff, device=dev),
                         yoff=torch.as_tensor(yoff, device=dev), tiles=i32(tiles), xidx=i32(xidx),
                         yidx=i32(yidx) if back else None)
-            d = _lib.SemFrontLaunch(len(tiles), rows, int(dims[:, 1].max()), int(back), keep["ptr"].data_ptr(),
+            d = _lib.SemFrontLaunch(len(tiles), rows, lanes, int(dims[:, 1].max()), int(back), keep["ptr"].data_ptr(),
                                     keep["dims"].data_ptr(), keep["xoff"].data_ptr(), keep["yoff"].data_ptr(),
                                     keep["tiles"].data_ptr(), keep["xidx"].data_ptr(),
                                     keep["yidx"].data_ptr() if back else None, None,
@@ -561,20 +585,48 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                     raise AssertionError("nested dissection: scatter targets must be distinct")
                 sc = dict(n_copy=len(p["copy_tgt"]), ct=i32(p["copy_tgt"]), cs=i32(p["copy_src"]),
                           n_acc=len(p["acc_tgt"]), at=i32(p["acc_tgt"]), a4=i32(p["acc_src"]).contiguous())
-            plan.append((d, keep, sc))
+            sp = None
+            if not back and st[3] is not None:
+                q = st[3]
+                coef, pat = q["coef"], np.asarray(q["pat"])
+                nrows, nnz = pat.shape
+                if (tuple(coef.shape) != (q["nitems"], nrows, nnz) or not coef.is_contiguous() or pat.min() < 0
+                        or pat.max() >= q["out_off"] or q["out_off"] + nrows > q["stride"]
+                        or q["nitems"] * q["stride"] > self._stage_len):
+                    raise AssertionError("nested dissection: bad sparse boundary step")
+                sp = dict(nitems=q["nitems"], nrows=nrows, nnz=nnz, coef=coef, pat=i32(pat), stride=q["stride"],
+                          out_off=q["out_off"])
+            plan.append((d, keep, sc, sp))
         return plan
 
+    # (lanes per row, rows per workgroup) of sem_front_gemv: (wide, narrow) per lane count
+    SHAPES = {64: (16, 4), 32: (16, 8), 16: (32, 16), 8: (64, 32), 4: (128, 64)}
+
+    @classmethod
+    def _launch_shape(cls, K, R):
+        """Lanes per row from the launch's median row length (pairs per lane ~2-4 on short rows: 64 lanes for rows of
+        >= 192 doubles), then the wide tile unless the launch would have fewer than 2048 workgroups."""
+        kp = int(np.median(K)) // 2
+        lanes = 64 if kp >= 96 else max(4, min(32, 1 << max(0, (kp // 2).bit_length() - 1)))
+        wide, narrow = cls.SHAPES[lanes]
+        rows = wide if int(((R + wide - 1) // wide).sum()) >= 2048 else narrow
+        return lanes, rows
+
     def _solve_lines_hip(self, B):
-        """The steps on the device: one sem_front_gemv per level and direction, one sem_front_scatter after each
-        forward level (module docstring)."""
+        """The steps on the device: one sem_front_gemv per level and direction, the leaves' sparse boundary rows
+        (sem_front_sparse_rows), one sem_front_scatter after each forward level (module docstring)."""
         import ctypes as C
         from .. import _lib
         lib = _lib.load()
         W = B.reshape(-1).clone()
         st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        for d, _, sc in self._hip:
+        for d, _, sc, sp in self._hip:
             d.W = W.data_ptr()
             _lib.check(lib.sem_front_gemv(C.byref(d), st))
+            if sp is not None:
+                _lib.check(lib.sem_front_sparse_rows(sp["nitems"], sp["nrows"], sp["nnz"], sp["coef"].data_ptr(),
+                                                     sp["pat"].data_ptr(), self._stage.data_ptr(), sp["stride"],
+                                                     sp["out_off"], st))
             if sc is not None:
                 _lib.check(lib.sem_front_scatter(sc["n_copy"], sc["ct"].data_ptr(), sc["cs"].data_ptr(), sc["n_acc"],
                                                  sc["at"].data_ptr(), sc["a4"].data_ptr(), self._stage.data_ptr(),

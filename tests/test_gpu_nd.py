@@ -96,4 +96,5 @@ def test_nd_refinement_gate_and_factor_size():
     eta = vs.check_refinement()
     assert np.isfinite(eta) and eta < 1e-12 and vs.refine == (eta > 1e-13)
     ops = sum(T[q].numel() for st in vs._steps for (T, q, *_rest) in st[1])
+    ops += sum(st[3]["coef"].numel() for st in vs._steps if st[0] == "fwd" and st[3] is not None)
     assert ops * 8 == vs.tree.bytes_per_solve()

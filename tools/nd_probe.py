@@ -94,11 +94,15 @@ def main():
         per = []
         for rep in range(3):
             rows = []
-            for d, keep, sc in nd._hip:
+            for d, keep, sc, sp in nd._hip:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 d.W = W.data_ptr()
                 a.record()
                 _lib.check(lib.sem_front_gemv(C.byref(d), st))
+                if sp is not None:
+                    _lib.check(lib.sem_front_sparse_rows(sp["nitems"], sp["nrows"], sp["nnz"], sp["coef"].data_ptr(),
+                                                         sp["pat"].data_ptr(), nd._stage.data_ptr(), sp["stride"],
+                                                         sp["out_off"], st))
                 if sc is not None:
                     _lib.check(lib.sem_front_scatter(sc["n_copy"], sc["ct"].data_ptr(), sc["cs"].data_ptr(),
                                                      sc["n_acc"], sc["at"].data_ptr(), sc["a4"].data_ptr(),
@@ -109,10 +113,11 @@ def main():
             per.append([a.elapsed_time(b) * 1e3 for a, b, _ in rows])
         us = np.median(np.array(per), axis=0)
         steps = []
-        for k, (d, keep, sc) in enumerate(nd._hip):
+        for k, (d, keep, sc, sp) in enumerate(nd._hip):
             dims = keep["dims"].cpu().numpy()
-            byts = int((dims[:, 0].astype(np.int64) * dims[:, 1]).sum() * 8)
+            byts = int((dims[:, 0].astype(np.int64) * dims[:, 1]).sum() * 8) + (sp["coef"].numel() * 8 if sp else 0)
             steps.append({"step": k, "back": d.back, "fronts": int(dims.shape[0]), "tiles": d.ntiles, "rows": d.rows,
+                          "lanes": d.lanes,
                           "us": float(us[k]), "op_MB": byts / 1e6, "TBs": byts / (us[k] * 1e-6) / 1e12})
         out["nd"]["steps"] = steps
         out["nd"]["steps_sum_us"] = float(us.sum())
