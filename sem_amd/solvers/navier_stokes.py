@@ -29,6 +29,7 @@ from ..krylov import Recycle, gcro, gmres
 from ..operators import ConvectionTensor, SEMOperator
 from ..tracing import phase
 from .convection_diffusion import DirichletRows
+from .nested_dissection import NestedDissectionSolver
 from .velocity_solve import VelocityJacobianSolver
 
 
@@ -45,11 +46,14 @@ def _mass_diagonal(P, nex, ney, dx, dy):
     return ((dx / 2) * (dy / 2)) * np.outer(wx, wy).ravel()
 
 
+_ALL_SIDES = _lib.SIDE_W | _lib.SIDE_E | _lib.SIDE_S | _lib.SIDE_N
+
+
 class NavierStokesSolver:
     def __init__(self, L_x: float, L_y: float, Re: float, Gr: float, P: int, N_ex: int, N_ey: int,
                  v_W: float = 0, v_E: float = 0, u_S: float = 0, u_N: float = 0,
                  mtol=1e-7, mtol_newton=1e-5, iprint: list = ['NEWTON_suc', 'NEWTON_iter'],  # noqa: B006
-                 max_basis: int = 3000, velocity_interior: str = "nested", velocity_graph: bool = True,
+                 max_basis: int = 3000, velocity_interior: str = "auto", velocity_graph: bool = True,
                  recycle_bytes: float = 0.0, velocity_sweep: str = "auto", schur_precond: str = "mass",
                  partition=None, partition_update: str = "distributed"):
         """partition: a sem_amd.parallel.Partition -- the solver then holds one element-column strip per
@@ -68,6 +72,11 @@ class NavierStokesSolver:
         matvecs on consistent right-hand sides, but the Arnoldi-relation error of the recycled space
         puts a floor near 1e-8 relative under the residual, above the couplers' mtol_internal = 1e-13,
         so inside the coupler it stagnates; off by default.
+        velocity_interior: the whole-mesh velocity-Jacobian factorisation -- "auto" (default): nested dissection of
+        the element grid (solvers/nested_dissection.py) when the Dirichlet rows are the whole perimeter (the
+        reference's velocity mask) and P >= 2, else the line condensation; "nd": nested dissection; "nested" / "lu" /
+        "inverse": the line condensation (solvers/velocity_solve.py) with its interior variants.  A partitioned
+        solver always factors by the element-partitioned line condensation (strip_solve.py).
         schur_precond: right preconditioner of the Schur-complement Krylov solve.  "mass" (default):
         the reference's mass diagonal (NavierStokes_Solver.py:207-212); "pcd": a
         pressure-convection-diffusion approximation S^-1 ~ A_p^-1 F_p M^-1 on the continuity rows,
@@ -81,6 +90,8 @@ class NavierStokesSolver:
         velocities there are reproduced only by the reference's own preconditioner."""
         if schur_precond not in ("mass", "pcd"):
             raise ValueError("schur_precond must be 'mass' or 'pcd'")
+        if velocity_interior not in ("auto", "nd", "nested", "lu", "inverse"):
+            raise ValueError("velocity_interior must be 'auto', 'nd', 'nested', 'lu' or 'inverse'")
         if partition_update not in ("distributed", "central"):
             raise ValueError("partition_update must be 'distributed' or 'central'")
         if partition is not None and schur_precond != "mass" and partition_update == "distributed":
@@ -413,8 +424,17 @@ class NavierStokesSolver:
         if self.N > 1_000_000:   # the previous linearisation's factor and graphs go before the next one
             gc.collect()
             torch.cuda.empty_cache()
-        vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device, interior=self._velocity_interior,
-                                    sweep=self._velocity_sweep)
+        interior = self._velocity_interior
+        nd_ok = self._P >= 2 and self._dir.mask is None and self._dir.sides == _ALL_SIDES
+        if interior == "nd" and not nd_ok:
+            raise ValueError("velocity_interior='nd' needs P >= 2 and the whole perimeter Dirichlet")
+        if interior == "nd" or (interior == "auto" and nd_ok):
+            # nested dissection of the element grid (solvers/nested_dissection.py): cfg5 3.9 ms per solve against
+            # the line condensation's 7.8 ms, cfg4 0.35 against 0.56 ms (profiles/r06/velocity/nd/)
+            vs = NestedDissectionSolver(self._P, self._N_ex, self._N_ey, m.device)
+        else:
+            vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device,
+                                        interior="nested" if interior == "auto" else interior, sweep=self._velocity_sweep)
         vs.factor_mesh(m, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
         vs.set_operator(self._velocity_apply_lines)
         vs.check_refinement()       # one refinement step per solve if the factor's backward error exceeds 1e-13
@@ -423,7 +443,8 @@ class NavierStokesSolver:
         self._velo = vs
         if 'LU_suc' in self._iprint:
             torch.cuda.synchronize(m.device)
-            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec (device static condensation, '
+            kind = "nested dissection" if vs.interior == "nd" else "device static condensation"
+            print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec ({kind}, '
                   f'backward error {vs.refine_eta:.1e}{", refined" if vs.refine else ""})')
         return vs
 

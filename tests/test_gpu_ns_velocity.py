@@ -16,9 +16,11 @@ CASES = [(4, 3, 2, 100.0), (2, 2, 3, 400.0), (1, 4, 3, 10.0), (6, 2, 2, 1000.0),
          (2, 7, 2, 300.0), (3, 1, 2, 50.0), (4, 8, 3, 700.0)]
 
 
-def _device_solver(P, nex, ney, Re, u, v):
+def _device_solver(P, nex, ney, Re, u, v, interior="nested"):
+    """The NS solver at (u, v); its velocity factorisation is the line condensation unless interior says otherwise
+    (the default "auto" picks nested dissection for the whole-perimeter mask: tests/test_gpu_nd.py)."""
     from sem_amd.solvers import NavierStokesSolver
-    ns = NavierStokesSolver(1.0, 1.0, Re, 0.0, P, nex, ney, u_N=1.0, iprint=[])
+    ns = NavierStokesSolver(1.0, 1.0, Re, 0.0, P, nex, ney, u_N=1.0, iprint=[], velocity_interior=interior)
     ns._get_residuals(u, v, np.zeros(ns.N), np.zeros(ns.N))
     ns._calc_jacobians(u, v)
     return ns
@@ -44,10 +46,14 @@ def test_velocity_blocks_match_oracle_jacobian(gpu, P, nex, ney, Re):
 
 
 @pytest.mark.parametrize("P,nex,ney,Re", CASES)
-def test_device_velocity_solve_matches_sparse_lu(gpu, P, nex, ney, Re):
+@pytest.mark.parametrize("interior", ["nested", "auto"])
+def test_device_velocity_solve_matches_sparse_lu(gpu, P, nex, ney, Re, interior):
+    """The NS solver's velocity factorisation -- the line condensation, and the default (nested dissection; the
+    line condensation at P = 1) -- against SciPy's sparse solve."""
     ref, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex)
-    ns = _device_solver(P, nex, ney, Re, u, v)
+    ns = _device_solver(P, nex, ney, Re, u, v, interior)
     vs = ns._velocity_solver()
+    assert vs.interior == ("nd" if interior == "auto" and P >= 2 else "nested")
     r = np.random.default_rng(3)
     bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
     xu, xv = vs.solve(ns._dev(bu), ns._dev(bv))
@@ -328,7 +334,7 @@ def test_edge_sweep_matches_abi9_sweep(gpu, P, nex, ney, Re):
                                                (1537, 3074, 3074, 1.0, 0.0), (1537, 1537, 1537, -1.0, 1.0),
                                                (5, 7, 9, 0.5, -2.0), (1, 1, 1, 1.0, 0.0), (13, 130, 131, 2.0, 0.0),
                                                (770, 1540, 1600, -1.0, 1.0)])
-def test_gemv_rows_matches_torch(gpu, M, K, lda, alpha, beta):
+def test_gemv_rows_load_widths_match_torch(gpu, M, K, lda, alpha, beta):
     """sem_gemv_rows (the block-Thomas sweep's streaming GEMV): both load widths (16-byte for even K / lda
     and aligned operands, 8-byte otherwise), row counts not a multiple of the workgroup's 4, alpha / beta,
     a leading dimension wider than K; beta = 0 must not read y (NaN there)."""
