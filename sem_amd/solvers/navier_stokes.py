@@ -72,11 +72,11 @@ class NavierStokesSolver:
         matvecs on consistent right-hand sides, but the Arnoldi-relation error of the recycled space
         puts a floor near 1e-8 relative under the residual, above the couplers' mtol_internal = 1e-13,
         so inside the coupler it stagnates; off by default.
-        velocity_interior: the whole-mesh velocity-Jacobian factorisation -- "auto" (default): nested dissection of
-        the element grid (solvers/nested_dissection.py) when the Dirichlet rows are the whole perimeter (the
-        reference's velocity mask) and P >= 2, else the line condensation; "nd": nested dissection; "nested" / "lu" /
-        "inverse": the line condensation (solvers/velocity_solve.py) with its interior variants.  A partitioned
-        solver always factors by the element-partitioned line condensation (strip_solve.py).
+        velocity_interior: the velocity-Jacobian factorisation -- "auto" (default): nested dissection of the element
+        grid (solvers/nested_dissection.py; on a partitioned solver each strip's own dissection, StripNDSolver) when
+        the Dirichlet rows are the whole perimeter (the reference's velocity mask) and P >= 2, else the line
+        condensation; "nd": nested dissection; "nested" / "lu" / "inverse": the line condensation
+        (solvers/velocity_solve.py, strip_solve.StripLineSolver) with its interior variants.
         schur_precond: right preconditioner of the Schur-complement Krylov solve.  "mass" (default):
         the reference's mass diagonal (NavierStokes_Solver.py:207-212); "pcd": a
         pressure-convection-diffusion approximation S^-1 ~ A_p^-1 F_p M^-1 on the continuity rows,
@@ -320,16 +320,27 @@ class NavierStokesSolver:
             return tuple(self._dev(a) for a in d)
         return tuple(d)
 
+    def _use_nd(self):
+        """Nested dissection (velocity_interior "auto" / "nd") needs P >= 2 and the whole perimeter Dirichlet."""
+        ok = self._P >= 2 and self._dir.mask is None and self._dir.sides == _ALL_SIDES
+        if self._velocity_interior == "nd" and not ok:
+            raise ValueError("velocity_interior='nd' needs P >= 2 and the whole perimeter Dirichlet")
+        return ok and self._velocity_interior in ("auto", "nd")
+
     def _strip_velocity_solver(self):
-        """The element-partitioned velocity factor of this linearisation (strip_solve.StripLineSolver on
-        this rank's strip handle), kept until _calc_jacobians runs again."""
+        """The element-partitioned velocity factor of this linearisation on this rank's strip handle
+        (nested_dissection.StripNDSolver, or strip_solve.StripLineSolver for other Dirichlet sets), kept until
+        _calc_jacobians runs again."""
         if self._velo is not None:
             return self._velo
+        from .nested_dissection import StripNDSolver
         from .strip_solve import StripLineSolver
         tStart = time.perf_counter()
         m, p = self._mesh, self._part
-        vs = StripLineSolver(self._P, self._N_ex, self._N_ey, m.device, p.part.bounds, p.rank, p.dist, group=p.group,
-                             gather_device=p.backend_device())
+        # every rank takes the same choice: the Dirichlet set and the option are global
+        cls = StripNDSolver if self._use_nd() else StripLineSolver
+        vs = cls(self._P, self._N_ex, self._N_ey, m.device, p.part.bounds, p.rank, p.dist, group=p.group,
+                 gather_device=p.backend_device())
         vs.factor_mesh(m, dir_mask=self._dir.mask, dir_sides=self._dir.sides, **self._jac_kw)
         vs.set_operator(self._velocity_apply_lines, amax=lambda t: p.amax(t))
         vs.check_refinement()       # every rank takes the same decision (norms max-reduced over the ranks)
@@ -425,10 +436,7 @@ class NavierStokesSolver:
             gc.collect()
             torch.cuda.empty_cache()
         interior = self._velocity_interior
-        nd_ok = self._P >= 2 and self._dir.mask is None and self._dir.sides == _ALL_SIDES
-        if interior == "nd" and not nd_ok:
-            raise ValueError("velocity_interior='nd' needs P >= 2 and the whole perimeter Dirichlet")
-        if interior == "nd" or (interior == "auto" and nd_ok):
+        if self._use_nd():
             # nested dissection of the element grid (solvers/nested_dissection.py): cfg5 3.9 ms per solve against
             # the line condensation's 7.8 ms, cfg4 0.35 against 0.56 ms (profiles/r06/velocity/nd/)
             vs = NestedDissectionSolver(self._P, self._N_ex, self._N_ey, m.device)

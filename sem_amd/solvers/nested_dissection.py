@@ -38,23 +38,29 @@ import os
 import numpy as np
 import torch
 
+from .strip_solve import _StripReduced
 from .velocity_solve import VelocityJacobianSolver, batched_inverse, pivot_inverse
 
 ALL_SIDES = 15   # SEM_SIDE_W | E | S | N
 
 
 class NDTree:
-    """Symbolic analysis of the nested dissection for an nex x ney mesh of order P, ncomp unknowns per node, the
-    whole perimeter Dirichlet.  Unknowns are addressed by their flat index in the solver's (NX, ncomp N_y) line
-    array: gx m + c N_y + gy (m = ncomp N_y)."""
+    """Symbolic analysis of the nested dissection for the element columns [xa, xb) (default: all) of an nex x ney
+    mesh of order P, ncomp unknowns per node, the mesh's whole perimeter Dirichlet.  Unknowns are addressed by their
+    flat index in the solver's local (NX, ncomp N_y) line array (lines xa P .. xb P): (gx - xa P) m + c N_y + gy
+    (m = ncomp N_y).  On a strip (xa > 0 or xb < nex) the root's boundary B is the strip's interface lines: they
+    are eliminated by the reduced system the strips share (StripNDSolver)."""
 
-    def __init__(self, P, nex, ney, nc):
+    def __init__(self, P, nex, ney, nc, xa=0, xb=None):
         if P < 2:
             raise ValueError("nested dissection needs P >= 2 (element interiors)")
-        self.P, self.nex, self.ney, self.nc = P, nex, ney, nc
-        self.NY, self.NX = ney * P + 1, nex * P + 1
+        xb = nex if xb is None else xb
+        if not 0 <= xa < xb <= nex:
+            raise ValueError("bad element-column range")
+        self.P, self.nex, self.ney, self.nc, self.xa, self.xb = P, nex, ney, nc, xa, xb
+        self.NY, self.NX, self.NXg = ney * P + 1, (xb - xa) * P + 1, nex * P + 1
         self.m = nc * self.NY
-        NY, NX, m = self.NY, self.NX, self.m
+        NY, NXg, m = self.NY, self.NXg, self.m
         # element-local order: interior (i, c, j) for i, j in 1..P-1 (the condensed layout's order), then the
         # boundary (i, c, j) for the nodes with i or j in {0, P}, x-major
         loc = np.full((P + 1, P + 1, nc), -1, dtype=np.int64)
@@ -85,39 +91,39 @@ class NDTree:
                 bpat[r] = loc[1:P, j, c]
         self.bpat = bpat
         self.pos_i, self.pos_j, self.pos_c = (np.asarray(a, dtype=np.int64) for a in (pi, pj, pc))
-        E = nex * ney
-        ex, ey = np.divmod(np.arange(E, dtype=np.int64), ney)      # element e = ex ney + ey
-        self.ex, self.ey = ex, ey
-        gx = ex[:, None] * P + self.pos_i[None, :]
+        E = (xb - xa) * ney
+        ex, ey = np.divmod(np.arange(E, dtype=np.int64), ney)      # local element e = (ex - xa) ney + ey
+        self.ex, self.ey = ex + xa, ey
+        gx = (ex[:, None] + xa) * P + self.pos_i[None, :]           # global line
         gy = ey[:, None] * P + self.pos_j[None, :]
-        self.eflat = gx * m + self.pos_c[None, :] * NY + gy          # (E, ne)
-        self.enode = gx * NY + gy                                    # global node (x-major) of each position
-        self.eD = (gx == 0) | (gx == NX - 1) | (gy == 0) | (gy == NY - 1)
+        self.eflat = (gx - xa * P) * m + self.pos_c[None, :] * NY + gy     # (E, ne) local flat index
+        self.eD = (gx == 0) | (gx == NXg - 1) | (gy == 0) | (gy == NY - 1)
         self.fronts = []
-        self.root = self._rec(0, nex, 0, ney, 0)
+        self.root = self._rec(xa, xb, 0, ney, 0)
         self.depth = max((f["depth"] for f in self.fronts), default=-1)
         self._child_maps()
 
     # ------------------------------------------------------------------ symbolic
     def _is_d(self, gx, gy):
-        return (gx == 0) | (gx == self.NX - 1) | (gy == 0) | (gy == self.NY - 1)
+        return (gx == 0) | (gx == self.NXg - 1) | (gy == 0) | (gy == self.NY - 1)
 
     def _flats(self, gx, gy):
-        """Flat indices of nodes (gx, gy) for every component, node-major then component."""
+        """Local flat indices of nodes (global gx, gy) for every component, node-major then component."""
         c = np.arange(self.nc, dtype=np.int64)
-        return (gx[:, None] * self.m + c[None, :] * self.NY + gy[:, None]).reshape(-1)
+        return ((gx[:, None] - self.xa * self.P) * self.m + c[None, :] * self.NY + gy[:, None]).reshape(-1)
 
     def _rec(self, x0, x1, y0, y1, depth):
         P, ney = self.P, self.ney
         if x1 - x0 == 1 and y1 - y0 == 1:
-            return ("e", x0 * ney + y0)
+            return ("e", (x0 - self.xa) * ney + y0)
         if x1 - x0 >= y1 - y0:
             xm = (x0 + x1) // 2
             gy = np.arange(y0 * P + 1, y1 * P, dtype=np.int64)
             gx = np.full_like(gy, xm * P)
             c0, c1 = self._rec(x0, xm, y0, y1, depth + 1), self._rec(xm, x1, y0, y1, depth + 1)
             # component-major along the line: contiguous runs of the line array
-            S = (xm * P * self.m + np.arange(self.nc, dtype=np.int64)[:, None] * self.NY + gy[None, :]).reshape(-1)
+            S = ((xm - self.xa) * P * self.m + np.arange(self.nc, dtype=np.int64)[:, None] * self.NY
+                 + gy[None, :]).reshape(-1)
         else:
             ym = (y0 + y1) // 2
             gx = np.arange(x0 * P + 1, x1 * P, dtype=np.int64)
@@ -169,7 +175,7 @@ class NDTree:
 
     def bytes_per_solve(self):
         """Operator bytes one solve reads: lift, leaves (Xi, the sparse A_bi, V_e), fronts (Fw, V)."""
-        E = self.nex * self.ney
+        E = (self.xb - self.xa) * self.ney
         nper = int(np.any(self.eD[:, self.ni:], axis=1).sum())
         leaf = E * (self.ni * self.ni + self.nb * (self.P - 1) + self.ni * self.nb)
         fr = sum(len(f["S"]) * (len(f["S"]) + 2 * len(f["B"])) for f in self.fronts)
@@ -177,8 +183,8 @@ class NDTree:
 
 
 @functools.lru_cache(maxsize=8)
-def nd_tree(P, nex, ney, nc):
-    return NDTree(P, nex, ney, nc)
+def nd_tree(P, nex, ney, nc, xa=0, xb=None):
+    return NDTree(P, nex, ney, nc, xa, xb)
 
 
 def element_matrices(tree, elems, dx, dy, Ks, Gs, w, c_mass=0.0, c_stiff=0.0, c_gradx=0.0, c_grady=0.0, cu=None,
@@ -197,7 +203,7 @@ def element_matrices(tree, elems, dx, dy, Ks, Gs, w, c_mass=0.0, c_stiff=0.0, c_
     f64 = dict(dtype=torch.float64, device=dev)
     e = torch.as_tensor(np.asarray(elems, dtype=np.int64), device=dev)
     E = e.numel()
-    ex, ey = e // t.ney, e % t.ney
+    ex, ey = e // t.ney, e % t.ney           # local element column (the strip's vectors are local)
     fKx, fKy = c_stiff * (dy / dx), c_stiff * (dx / dy)
     fM, fX, fY = c_mass * (dx / 2.0) * (dy / 2.0), c_gradx * (dy / 2.0), c_grady * (dx / 2.0)
     Ks, Gs, w = (torch.as_tensor(np.asarray(a), **f64) for a in (Ks, Gs, w))
@@ -224,7 +230,7 @@ def element_matrices(tree, elems, dx, dy, Ks, Gs, w, c_mass=0.0, c_stiff=0.0, c_
         col = loc[:, :, c][:, None, :].expand(n, n, n)                   # loc[i, q, c]
         vy = w[None, :, None, None] * (fKy * Ks[None, None, :, :] + fY * cvN[:, :, :, None] * Gs[None, None, :, :])
         A.scatter_add_(1, (r * ne + col).reshape(1, -1).expand(E, -1), vy.reshape(E, -1))
-    own = (((ar[None, :, None] < P) | (ex[:, None, None] == t.nex - 1))
+    own = (((ar[None, :, None] < P) | (ex[:, None, None] + t.xa == t.nex - 1))
            & ((ar[None, None, :] < P) | (ey[:, None, None] == t.ney - 1))).to(torch.float64)   # (E, i, j)
     diag = fM * w[:, None] * w[None, :]
     for c in range(nc):
@@ -255,10 +261,13 @@ class NestedDissectionSolver(VelocityJacobianSolver):
     interface as VelocityJacobianSolver (solve, solve1, _solve_lines, set_operator, check_refinement, capture);
     factor with factor_mesh(mesh, **kw) (the device mesh) or factor_coeffs(dx, dy, **kw) (any torch device)."""
 
-    def __init__(self, P, nex, ney, device, ncomp=2):
-        super().__init__(P, nex, ney, device, interior="nested", sweep="thomas", ncomp=ncomp)
+    def __init__(self, P, nex, ney, device, ncomp=2, cols=None):
+        """cols = (xa, xb): the element columns of a strip of the nex x ney mesh (StripNDSolver); the solver's
+        lines are then xa P .. xb P."""
+        xa, xb = (0, nex) if cols is None else cols
+        super().__init__(P, xb - xa, ney, device, interior="nested", sweep="thomas", ncomp=ncomp)
         self.interior = "nd"
-        self.tree = nd_tree(P, nex, ney, ncomp)
+        self.tree = nd_tree(P, nex, ney, ncomp, xa, xb)
         self.chunk_elems = int(os.environ.get("SEM_ND_CHUNK", "2048"))
 
     # ------------------------------------------------------------------ factorisation
@@ -312,6 +321,8 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 self._leafV[e0:e1] = V
                 U_leaf[e0:e1] = Abb - Abi @ V
                 del A, Xi, V
+        kind, rid = t.root
+        self._root_update = U_leaf[rid].clone() if kind == "e" else None   # a strip's Schur complement on its lines
         self._factor_fronts(U_leaf)
         del U_leaf
         self._build_steps()
@@ -354,6 +365,8 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                         self._fw[fid] = (Fw, q)
                         self._fv[fid] = (V, q) if b else None
                         fu[fid] = (U, q) if b else None
+                        if t.root == ("f", fid) and b:
+                            self._root_update = U[q]
                 # children's updates are no longer needed once every front of this depth has its matrix
                 for fid in [f for g in by_depth[depth].values() for f in g]:
                     for kind, cid in t.fronts[fid]["children"]:
@@ -451,6 +464,7 @@ class NestedDissectionSolver(VelocityJacobianSolver):
             items.append((self._leafV, e, xb, t.eflat[e, :ni]))
         steps.append(("back", items))
         self._steps = steps
+        self._nfwd = sum(1 for st in steps if st[0] == "fwd")
         self._stage_len = max(max(max(it[3] + it[0].shape[1] for it in st[1]),
                                   st[3]["nitems"] * st[3]["stride"] if st[3] else 0) for st in steps if st[0] == "fwd")
         self._hip = self._hip_plan() if self.device.type == "cuda" else None
@@ -472,13 +486,26 @@ class NestedDissectionSolver(VelocityJacobianSolver):
 
     # ------------------------------------------------------------------ solve
     def _solve_lines_once(self, B):
+        """Forward steps, the strip hook (the reduced system over the strip-boundary lines; nothing on a whole mesh),
+        back-substitution steps -- on the device the HIP launches, elsewhere the torch loop over the same tables.
+        The working array carries one trailing zero (operand index -1)."""
+        Wz = torch.cat((B.reshape(-1), B.new_zeros(1)))
+        nf = self._nfwd
+        self._run(Wz, 0, nf)
+        self._between(Wz[:-1].view(self.NX, self.m), B)
+        self._run(Wz, nf, len(self._steps))
+        return Wz[:-1].view(self.NX, self.m)
+
+    def _between(self, W, B):
+        """After the forward steps: W holds y on every eliminated unknown and the reduced right-hand side on the
+        root's boundary (none on a whole mesh)."""
+
+    def _run(self, Wz, lo, hi):
         if self.device.type == "cuda":
-            return self._solve_lines_hip(B)
-        W = B.reshape(-1).clone()
-        Wz = torch.cat((W, W.new_zeros(1)))      # index -1 reads the trailing zero
-        stage = W.new_zeros(self._stage_len)
-        dev = W.device
-        for st in self._steps:
+            return self._run_hip(Wz, lo, hi)
+        stage = Wz.new_zeros(self._stage_len)
+        dev = Wz.device
+        for st in self._steps[lo:hi]:
             if st[0] == "fwd":
                 for T, q, xidx, off in st[1]:
                     x = Wz[torch.as_tensor(xidx, device=dev)]
@@ -502,7 +529,6 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                     x = Wz[torch.as_tensor(xidx, device=dev)]
                     y = torch.as_tensor(yidx, device=dev)
                     Wz[y] = Wz[y] - T[q] @ x
-        return Wz[:-1].view(self.NX, self.m)
 
     def _hip_plan(self):
         """Device tables of every step (sem_front_gemv descriptors, sem_front_scatter index arrays), checked on the
@@ -612,16 +638,15 @@ class NestedDissectionSolver(VelocityJacobianSolver):
         rows = wide if int(((R + wide - 1) // wide).sum()) >= 2048 else narrow
         return lanes, rows
 
-    def _solve_lines_hip(self, B):
-        """The steps on the device: one sem_front_gemv per level and direction, the leaves' sparse boundary rows
+    def _run_hip(self, Wz, lo, hi):
+        """Steps lo..hi on the device: one sem_front_gemv per level and direction, the leaves' sparse boundary rows
         (sem_front_sparse_rows), one sem_front_scatter after each forward level (module docstring)."""
         import ctypes as C
         from .. import _lib
         lib = _lib.load()
-        W = B.reshape(-1).clone()
         st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        for d, _, sc, sp in self._hip:
-            d.W = W.data_ptr()
+        for d, _, sc, sp in self._hip[lo:hi]:
+            d.W = Wz.data_ptr()
             _lib.check(lib.sem_front_gemv(C.byref(d), st))
             if sp is not None:
                 _lib.check(lib.sem_front_sparse_rows(sp["nitems"], sp["nrows"], sp["nnz"], sp["coef"].data_ptr(),
@@ -630,5 +655,68 @@ class NestedDissectionSolver(VelocityJacobianSolver):
             if sc is not None:
                 _lib.check(lib.sem_front_scatter(sc["n_copy"], sc["ct"].data_ptr(), sc["cs"].data_ptr(), sc["n_acc"],
                                                  sc["at"].data_ptr(), sc["a4"].data_ptr(), self._stage.data_ptr(),
-                                                 W.data_ptr(), st))
-        return W.view(self.NX, self.m)
+                                                 Wz.data_ptr(), st))
+
+
+class StripNDSolver(_StripReduced, NestedDissectionSolver):
+    """The element-partitioned velocity solve with each strip ordered by nested dissection: rank r dissects its own
+    element columns [e_b, e_e) with its two interface lines as the root's boundary, so its factor ends in the
+    strip's Schur complement on those lines -- its 2 x 2 block system R of the reduced system over the G + 1
+    strip-boundary lines that the strips share (strip_solve._StripReduced: one all-gather of R at factor time, this
+    rank's two block rows of R^-1, one all-gather of 2m right-hand-side values per solve).  Element shares make the
+    partial rows of a shared line automatic (each strip adds its own elements); the Dirichlet identity rows of a
+    shared line go to its right owner, and the whole outer lines x = 0, 1 are identity rows.
+    Solve: the strip's forward steps (lift, leaves, every level up to its root), the reduced solve for the two
+    interface lines, the back-substitution steps -- no coupling solutions X0 / X1 are needed (the fronts' V panels
+    carry the interface lines like any ancestor separator)."""
+
+    def __init__(self, P, nex, ney, device, bounds, rank, dist, group=None, ncomp=2, gather_device=None):
+        NestedDissectionSolver.__init__(self, P, nex, ney, device, ncomp=ncomp, cols=(bounds[rank], bounds[rank + 1]))
+        self._strip_init(nex, bounds, rank, dist, group, gather_device)
+
+    def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
+        if mesh.ex_begin != self.eb or mesh.ex_end != self.ee:
+            raise ValueError("the mesh handle must hold this rank's strip")
+        return self.factor_coeffs(mesh.dx, mesh.dy, **kw)
+
+    def factor_coeffs(self, dx, dy, **kw):
+        NestedDissectionSolver.factor_coeffs(self, dx, dy, **kw)
+        if self.G == 1:
+            return
+        self._reduced_factor(self._interface_blocks())
+        self._root_update = None
+
+    def _interface_blocks(self):
+        """R (2, 2, m, m): the root's update U on its boundary (the strip's non-Dirichlet interface-line unknowns)
+        placed on the left / right line blocks, plus the identity rows of the lines' Dirichlet unknowns this strip
+        owns (its left line; its right line only at the mesh's right end)."""
+        t, m, NX, NY = self.tree, self.m, self.NX, self.NY
+        kind, rid = t.root
+        keys = (t.eflat[rid, t.ni:][~t.eD[rid, t.ni:]] if kind == "e" else t.fronts[rid]["B"])
+        U = self._root_update
+        if kind == "e":
+            U = U[torch.as_tensor(np.nonzero(~t.eD[rid, t.ni:])[0], device=self.device)][
+                :, torch.as_tensor(np.nonzero(~t.eD[rid, t.ni:])[0], device=self.device)]
+        gxl, r = np.divmod(keys, m)
+        if not np.all((gxl == 0) | (gxl == NX - 1)):
+            raise AssertionError("nested dissection: a strip root's boundary off its interface lines")
+        pos = torch.as_tensor(np.where(gxl == 0, 0, m) + r, device=self.device)
+        R = torch.zeros((2 * m, 2 * m), dtype=torch.float64, device=self.device)
+        R[pos[:, None], pos[None, :]] = U
+        # Dirichlet rows on the lines (both components): all of an outer line, the ends gy = 0, N_y - 1 otherwise
+        c_gy = np.arange(m) % NY
+        for side, gx_glob, own in ((0, self.eb * self.P, True), (1, self.ee * self.P, self.own_right)):
+            if not own:
+                continue
+            dmask = (c_gy == 0) | (c_gy == NY - 1) | (gx_glob == 0) | (gx_glob == t.NXg - 1)
+            idx = torch.as_tensor(side * m + np.nonzero(dmask)[0], device=self.device)
+            R[idx, idx] = 1.0
+        return R.view(2, m, 2, m).permute(0, 2, 1, 3).contiguous()
+
+    def _between(self, W, B):
+        if self.G == 1:
+            return
+        h = torch.stack((W[0], W[-1] if self.own_right else W[-1] - B[-1]))
+        xb2 = self._reduced_solve(h)
+        W[0] = xb2[:self.m]
+        W[-1] = xb2[self.m:]

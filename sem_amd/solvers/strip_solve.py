@@ -30,14 +30,14 @@ from .velocity_solve import (VelocityJacobianSolver, _gemv, _gemv2, fused_thomas
                              pivot_inverse, twisted_thomas_operators, twisted_thomas_solve, twisted_thomas_solve_mat)
 
 
-class StripLineSolver(VelocityJacobianSolver):
-    """x = J^-1 b for a Jacobian whose element columns are strip-partitioned across the ranks of `dist`."""
+class _StripReduced:
+    """The part of an element-partitioned solve that the strips share, whatever eliminates each strip's interior:
+    the strip attributes, the all-gather, the reduced block-tridiagonal system over the G + 1 strip-boundary lines
+    (this rank's two block rows of its inverse), its solve, and the graph capture agreed by every rank.  Mixed into
+    StripLineSolver (line condensation) and nested_dissection.StripNDSolver."""
 
-    def __init__(self, P, nex, ney, device, bounds, rank, dist, group=None, ncomp=2, gather_device=None):
-        """bounds: the StripPartition bounds (rank r holds element columns [bounds[r], bounds[r+1]));
-        gather_device: where the all-gathered blocks travel (the GPU under RCCL, the host under gloo)."""
+    def _strip_init(self, nex, bounds, rank, dist, group, gather_device):
         eb, ee = bounds[rank], bounds[rank + 1]
-        super().__init__(P, ee - eb, ney, device, interior="nested", sweep="auto", ncomp=ncomp)
         self.nex_global, self.eb, self.ee = nex, eb, ee
         self.bounds, self.rank, self.G = list(bounds), rank, len(bounds) - 1
         self.dist, self.group = dist, group
@@ -51,18 +51,6 @@ class StripLineSolver(VelocityJacobianSolver):
         """This strip's lines eb P .. ee P among the mesh's nex P + 1 (refinement probes agree on shared lines)."""
         return self.eb * self.P, self.ee * self.P + 1, self.nex_global * self.P + 1
 
-    # ------------------------------------------------------------------ factor
-    def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
-        """Assemble the strip's condensed pieces on its strip handle (HIP) and factor."""
-        if mesh.ex_begin != self.eb or mesh.ex_end != self.ee:
-            raise ValueError("the mesh handle must hold this rank's strip")
-        kw = dict(kw, ncomp=self.ncomp)
-        eb = self.eb
-        if self.P == 1:
-            raise ValueError("the strip solve needs P >= 2")
-        return self.factor_condensed(
-            lambda b, cols: mesh.condensed_blocks(b, cols=(cols[0] + eb, cols[1] + eb), **kw), budget_bytes)
-
     def _all_gather(self, t):
         """[t of rank 0, ..., t of rank G-1] (same shape everywhere) on this solver's device."""
         if self.G == 1:
@@ -72,61 +60,11 @@ class StripLineSolver(VelocityJacobianSolver):
         self.dist.all_gather(out, src, group=self.group)
         return [o.to(self.device) for o in out]
 
-    def _sweep_factor(self, S_diag, S_up, S_lo):
-        """Local lines 0..n: eliminate 1..n-1 (block LU), keep the strip's boundary lines 0 and n.  One
-        rank: the whole-mesh sweep."""
-        if self.G == 1:
-            self._T = None
-            return super()._sweep_factor(S_diag, S_up, S_lo)
-        n, m = self.nex, self.m
+    def _reduced_factor(self, R):
+        """The reduced system over the G + 1 strip-boundary lines from every strip's 2 x 2 block system R (its
+        Schur complement on its two boundary lines), factored on every rank."""
+        m = self.m
         dev, f64 = self.device, torch.float64
-        inv = pivot_inverse
-        if n == 1:
-            R = torch.stack((torch.stack((S_diag[0], S_up[0])), torch.stack((S_lo[0], S_diag[1]))))
-            self._T = None
-        elif self.sweep_form == "twisted" and n - 1 >= 3:
-            # two-ended sweep of the interior lines, as the whole mesh's; X0, X1 from the same factors (one set of
-            # pivot inverses: ADVICE r4 -- the one-ended factors were formed only for X0, X1 and doubled them)
-            k = n - 1
-            op = twisted_thomas_operators(S_diag[1:n], S_up[1:n - 1], S_lo[1:n - 1])
-            rhs = torch.zeros((k, m, 2 * m), dtype=f64, device=dev)
-            rhs[0, :, :m] = S_lo[0]
-            rhs[k - 1, :, m:] = S_up[n - 1]
-            X01 = twisted_thomas_solve_mat(op, rhs)
-            del rhs
-            X0, X1 = X01[..., :m], X01[..., m:]
-            R = torch.stack((torch.stack((S_diag[0] - S_up[0] @ X0[0], -(S_up[0] @ X1[0]))),
-                             torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
-            self._T = (("twisted", op), X01)
-        else:
-            k = n - 1                           # interior lines 1..n-1 -> rows 0..k-1 of T
-            Dinv = torch.empty((k, m, m), dtype=f64, device=dev)
-            Uh = torch.empty((max(k - 1, 1), m, m), dtype=f64, device=dev)
-            Dinv[0] = inv(S_diag[1])
-            for i in range(1, k):
-                Uh[i - 1] = Dinv[i - 1] @ S_up[i]                      # T's upper block of row i-1
-                Dinv[i] = inv(S_diag[i + 1] - S_lo[i] @ Uh[i - 1])     # T's lower block of row i
-            # X0 = T^-1 [S_lo[0]; 0; ...] (coupling of the interior to line 0), X1 = T^-1 [0; ...; S_up[n-1]]
-            X0 = torch.empty((k, m, m), dtype=f64, device=dev)
-            X1 = torch.zeros((k, m, m), dtype=f64, device=dev)
-            X0[0] = Dinv[0] @ S_lo[0]
-            for i in range(1, k):
-                X0[i] = -(Dinv[i] @ (S_lo[i] @ X0[i - 1]))
-            X1[k - 1] = Dinv[k - 1] @ S_up[n - 1]
-            for i in range(k - 2, -1, -1):
-                X0[i] -= Uh[i] @ X0[i + 1]
-                X1[i] = -(Uh[i] @ X1[i + 1])
-            R = torch.stack((torch.stack((S_diag[0] - S_up[0] @ X0[0], -(S_up[0] @ X1[0]))),
-                             torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
-            # the solve's operators: the fused block-Thomas sweep of the interior lines (one GEMV per line and
-            # direction, as the whole-mesh sweep) and [X0 | X1] for the back substitution in one batched GEMV
-            th = ("single", fused_thomas_operators(Dinv, S_lo[1:n - 1] if n > 2 else None, Uh[:k - 1]))
-            X01 = torch.cat((X0, X1), dim=2)
-            del Dinv, Uh, X0, X1
-            self._T = (th, X01)
-        self._S_up0, self._S_lon = S_up[0].clone(), S_lo[n - 1].clone()
-        del S_diag, S_up, S_lo
-        # the reduced system over the G + 1 strip-boundary lines, factored on every rank
         Rs = self._all_gather(R)
         G = self.G
         Rd = torch.zeros((G + 1, m, m), dtype=f64, device=dev)
@@ -189,32 +127,12 @@ class StripLineSolver(VelocityJacobianSolver):
             Z[:, j * m:(j + 1) * m] = P
         return Z
 
-    # ------------------------------------------------------------------ solve
-    def _own_rhs(self, g, B):
-        if not self.own_right:          # the right line's right-hand side is its right owner's
-            g[-1] -= B[-1]
-
-    def _thomas(self, g):
-        """y = T^-1 g for the local interior lines (g: (k, m)): the fused block-Thomas sweep, two-ended when the
-        strip has at least three interior lines."""
-        form, op = self._T[0]
-        return twisted_thomas_solve(op, g) if form == "twisted" else fused_thomas_solve(*op, g)
-
-    def _iface_solve(self, g):
-        """No host synchronisation under RCCL (the all-gather stays on the device): stream-capturable."""
-        if self.G == 1:
-            return super()._iface_solve(g)
-        n = self.nex
-        with phase("strip.interior_sweep"):
-            if self._T is not None:
-                y = self._thomas(g[1:n])
-                h = torch.stack((g[0], g[n]))   # the boundary lines' right-hand sides: one dual streaming GEMV
-                _gemv2((self._S_up0, y[0], h[0]), (self._S_lon, y[-1], h[1]), alpha=-1.0, beta=1.0)
-            else:
-                y, h = None, torch.stack((g[0], g[1]))
+    def _reduced_solve(self, h):
+        """x on this strip's two boundary lines (2m) from every strip's boundary right-hand sides h (2, m): ONE
+        all-gather and one streaming GEMV (or the replicated CR solve)."""
+        m = self.m
         with phase("strip.allgather"):
             H = torch.stack(self._all_gather(h))      # (G, 2, m): the boundary right-hand sides of every strip
-        m = self.m
         with phase("strip.reduced_solve"):
             rhs = torch.zeros((self.G + 1, m), dtype=torch.float64, device=self.device)
             rhs[:-1] += H[:, 0]
@@ -224,14 +142,7 @@ class StripLineSolver(VelocityJacobianSolver):
                 _gemv(self._Z, rhs.reshape(-1), xb2)
             else:
                 xb2 = self._red._cr_solve(rhs)[self.rank:self.rank + 2].reshape(-1)
-        out = torch.empty_like(g)
-        out[0], out[n] = xb2[:m], xb2[m:]
-        with phase("strip.back_substitution"):
-            if y is not None:   # y - X0 x0 - X1 x1 = y - [X0 | X1] [x0; x1]: one streaming GEMV over (k m) x 2m
-                X01 = self._T[1]
-                out[1:n] = y
-                _gemv(X01.view(-1, X01.shape[-1]), xb2, out[1:n].reshape(-1), alpha=-1.0, beta=1.0)
-        return out
+        return xb2
 
     def capture(self):
         """Graph capture of the solve: only when the reduced system's all-gather runs on the device (RCCL,
@@ -261,3 +172,116 @@ class StripLineSolver(VelocityJacobianSolver):
         flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=self.gather_device)
         self.dist.all_reduce(flag, op=self.dist.ReduceOp.MIN, group=self.group)
         return float(flag.item()) == 1.0
+
+
+class StripLineSolver(_StripReduced, VelocityJacobianSolver):
+    """x = J^-1 b for a Jacobian whose element columns are strip-partitioned across the ranks of `dist`, each strip
+    condensed by lines (module docstring)."""
+
+    def __init__(self, P, nex, ney, device, bounds, rank, dist, group=None, ncomp=2, gather_device=None):
+        """bounds: the StripPartition bounds (rank r holds element columns [bounds[r], bounds[r+1]));
+        gather_device: where the all-gathered blocks travel (the GPU under RCCL, the host under gloo)."""
+        super().__init__(P, bounds[rank + 1] - bounds[rank], ney, device, interior="nested", sweep="auto", ncomp=ncomp)
+        self._strip_init(nex, bounds, rank, dist, group, gather_device)
+
+    # ------------------------------------------------------------------ factor
+    def factor_mesh(self, mesh, budget_bytes=24 << 30, **kw):
+        """Assemble the strip's condensed pieces on its strip handle (HIP) and factor."""
+        if mesh.ex_begin != self.eb or mesh.ex_end != self.ee:
+            raise ValueError("the mesh handle must hold this rank's strip")
+        kw = dict(kw, ncomp=self.ncomp)
+        eb = self.eb
+        if self.P == 1:
+            raise ValueError("the strip solve needs P >= 2")
+        return self.factor_condensed(
+            lambda b, cols: mesh.condensed_blocks(b, cols=(cols[0] + eb, cols[1] + eb), **kw), budget_bytes)
+
+    def _sweep_factor(self, S_diag, S_up, S_lo):
+        """Local lines 0..n: eliminate 1..n-1 (block LU), keep the strip's boundary lines 0 and n.  One
+        rank: the whole-mesh sweep."""
+        if self.G == 1:
+            self._T = None
+            return super()._sweep_factor(S_diag, S_up, S_lo)
+        n, m = self.nex, self.m
+        dev, f64 = self.device, torch.float64
+        inv = pivot_inverse
+        if n == 1:
+            R = torch.stack((torch.stack((S_diag[0], S_up[0])), torch.stack((S_lo[0], S_diag[1]))))
+            self._T = None
+        elif self.sweep_form == "twisted" and n - 1 >= 3:
+            # two-ended sweep of the interior lines, as the whole mesh's; X0, X1 from the same factors (one set of
+            # pivot inverses: ADVICE r4 -- the one-ended factors were formed only for X0, X1 and doubled them)
+            k = n - 1
+            op = twisted_thomas_operators(S_diag[1:n], S_up[1:n - 1], S_lo[1:n - 1])
+            rhs = torch.zeros((k, m, 2 * m), dtype=f64, device=dev)
+            rhs[0, :, :m] = S_lo[0]
+            rhs[k - 1, :, m:] = S_up[n - 1]
+            X01 = twisted_thomas_solve_mat(op, rhs)
+            del rhs
+            X0, X1 = X01[..., :m], X01[..., m:]
+            R = torch.stack((torch.stack((S_diag[0] - S_up[0] @ X0[0], -(S_up[0] @ X1[0]))),
+                             torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
+            self._T = (("twisted", op), X01)
+        else:
+            k = n - 1                           # interior lines 1..n-1 -> rows 0..k-1 of T
+            Dinv = torch.empty((k, m, m), dtype=f64, device=dev)
+            Uh = torch.empty((max(k - 1, 1), m, m), dtype=f64, device=dev)
+            Dinv[0] = inv(S_diag[1])
+            for i in range(1, k):
+                Uh[i - 1] = Dinv[i - 1] @ S_up[i]                      # T's upper block of row i-1
+                Dinv[i] = inv(S_diag[i + 1] - S_lo[i] @ Uh[i - 1])     # T's lower block of row i
+            # X0 = T^-1 [S_lo[0]; 0; ...] (coupling of the interior to line 0), X1 = T^-1 [0; ...; S_up[n-1]]
+            X0 = torch.empty((k, m, m), dtype=f64, device=dev)
+            X1 = torch.zeros((k, m, m), dtype=f64, device=dev)
+            X0[0] = Dinv[0] @ S_lo[0]
+            for i in range(1, k):
+                X0[i] = -(Dinv[i] @ (S_lo[i] @ X0[i - 1]))
+            X1[k - 1] = Dinv[k - 1] @ S_up[n - 1]
+            for i in range(k - 2, -1, -1):
+                X0[i] -= Uh[i] @ X0[i + 1]
+                X1[i] = -(Uh[i] @ X1[i + 1])
+            R = torch.stack((torch.stack((S_diag[0] - S_up[0] @ X0[0], -(S_up[0] @ X1[0]))),
+                             torch.stack((-(S_lo[n - 1] @ X0[k - 1]), S_diag[n] - S_lo[n - 1] @ X1[k - 1]))))
+            # the solve's operators: the fused block-Thomas sweep of the interior lines (one GEMV per line and
+            # direction, as the whole-mesh sweep) and [X0 | X1] for the back substitution in one batched GEMV
+            th = ("single", fused_thomas_operators(Dinv, S_lo[1:n - 1] if n > 2 else None, Uh[:k - 1]))
+            X01 = torch.cat((X0, X1), dim=2)
+            del Dinv, Uh, X0, X1
+            self._T = (th, X01)
+        self._S_up0, self._S_lon = S_up[0].clone(), S_lo[n - 1].clone()
+        del S_diag, S_up, S_lo
+        self._reduced_factor(R)
+
+    # ------------------------------------------------------------------ solve
+    def _own_rhs(self, g, B):
+        if not self.own_right:          # the right line's right-hand side is its right owner's
+            g[-1] -= B[-1]
+
+    def _thomas(self, g):
+        """y = T^-1 g for the local interior lines (g: (k, m)): the fused block-Thomas sweep, two-ended when the
+        strip has at least three interior lines."""
+        form, op = self._T[0]
+        return twisted_thomas_solve(op, g) if form == "twisted" else fused_thomas_solve(*op, g)
+
+    def _iface_solve(self, g):
+        """No host synchronisation under RCCL (the all-gather stays on the device): stream-capturable."""
+        if self.G == 1:
+            return super()._iface_solve(g)
+        n = self.nex
+        with phase("strip.interior_sweep"):
+            if self._T is not None:
+                y = self._thomas(g[1:n])
+                h = torch.stack((g[0], g[n]))   # the boundary lines' right-hand sides: one dual streaming GEMV
+                _gemv2((self._S_up0, y[0], h[0]), (self._S_lon, y[-1], h[1]), alpha=-1.0, beta=1.0)
+            else:
+                y, h = None, torch.stack((g[0], g[1]))
+        xb2 = self._reduced_solve(h)
+        m = self.m
+        out = torch.empty_like(g)
+        out[0], out[n] = xb2[:m], xb2[m:]
+        with phase("strip.back_substitution"):
+            if y is not None:   # y - X0 x0 - X1 x1 = y - [X0 | X1] [x0; x1]: one streaming GEMV over (k m) x 2m
+                X01 = self._T[1]
+                out[1:n] = y
+                _gemv(X01.view(-1, X01.shape[-1]), xb2, out[1:n].reshape(-1), alpha=-1.0, beta=1.0)
+        return out

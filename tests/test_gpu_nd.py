@@ -73,7 +73,7 @@ def test_nd_hip_steps_match_the_torch_path():
     vs = NestedDissectionSolver(P, nex, ney, dev)
     vs.factor_coeffs(1.0 / nex, 1.0 / ney, **_kw(ns, u, v, Re, dev))
     B = torch.rand((vs.NX, vs.m), dtype=torch.float64, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
-    x_hip = vs._solve_lines_hip(B)
+    x_hip = vs._solve_lines_once(B.clone())      # the HIP steps
     dev_type = vs.device
     vs.device = torch.device("cpu")          # the torch loop (it reads the device tensors through the same tables)
     try:

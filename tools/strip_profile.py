@@ -108,11 +108,11 @@ def count_collectives(dist):
     return stats
 
 
-def build_solver(dist, ne, P, backend_dev=None):
+def build_solver(dist, ne, P, backend_dev=None, interior="auto"):
     from sem_amd.parallel import Partition
     from sem_amd.solvers import NavierStokesSolver
     ns = NavierStokesSolver(1.0, 1.0, 1e3, 1e6 / 0.71, P, ne, ne, mtol=1e-13, mtol_newton=1e-13, iprint=[],
-                            partition=Partition(dist) if dist is not None else None)
+                            partition=Partition(dist) if dist is not None else None, velocity_interior=interior)
     x, y = ns.points
     u0, v0, _ = smooth_step(x, y)
     ns._get_residuals(10 * u0, 10 * v0, np.zeros(ns.N), 0.5 - x)
@@ -250,9 +250,12 @@ def graph_parts(vs, dev, reps):
     m, n = vs.m, vs.nex
     B = torch.rand((vs.NX, m), dtype=torch.float64, device=dev)
     g = torch.rand((n + 1, m), dtype=torch.float64, device=dev)
-    out = {"solve_lines": graph_ms(lambda: vs._solve_lines(B), dev, reps),
-           "iface_solve": graph_ms(lambda: vs._iface_solve(g.clone()), dev, reps)}
-    if vs._T is not None:
+    out = {"solve_lines": graph_ms(lambda: vs._solve_lines(B), dev, reps)}
+    if getattr(vs, "interior", "") == "nd":      # nested-dissection strip: its operator bytes per solve
+        out["strip_nd_GB"] = vs.tree.bytes_per_solve() / 1e9
+    else:
+        out["iface_solve"] = graph_ms(lambda: vs._iface_solve(g.clone()), dev, reps)
+    if getattr(vs, "_T", None) is not None:
         out["interior_sweep"] = graph_ms(lambda: vs._thomas(g[1:n]), dev, reps)
         X01 = vs._T[1]
         xb2 = torch.rand(2 * m, dtype=torch.float64, device=dev)
@@ -292,15 +295,15 @@ def loopback_gather(fake):
 def solo(args):
     from sem_amd import tracing
     from sem_amd.krylov import _DeviceSweeps
-    from sem_amd.solvers.strip_solve import StripLineSolver
+    from sem_amd.solvers.strip_solve import _StripReduced
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     recs = []
     for r in [int(t) for t in args.ranks.split(",")]:
         fake = LoopbackDist(args.G, r)
-        StripLineSolver._all_gather = loopback_gather(fake)
+        _StripReduced._all_gather = loopback_gather(fake)     # line and nested-dissection strips alike
         rec = {"mode": "solo", "G": args.G, "rank": r, "ne": args.ne, "P": args.P}
-        ns, _ = build_solver(fake, args.ne, args.P)
+        ns, _ = build_solver(fake, args.ne, args.P, interior=args.interior)
         m = ns._mesh
         rec["strip"] = [m.ex_begin, m.ex_end]
         rec["n_local"] = m.n_local
@@ -315,7 +318,8 @@ def solo(args):
         # partition whose gate passes runs it
         rec["refine_eta_loopback"] = vs.refine_eta
         vs.refine = False
-        rec["twisted_interior"] = vs._T is not None and vs._T[0][0] == "twisted"
+        rec["strip_solver"] = type(vs).__name__
+        rec["twisted_interior"] = getattr(vs, "_T", None) is not None and vs._T[0][0] == "twisted"
         fake.calls.clear()
         wall, tab = time_eager_matvecs(ns, vs, args.reps, dev)
         rec["eager_matvec_ms"] = 1e3 * wall
@@ -371,7 +375,7 @@ def solo(args):
         torch.cuda.empty_cache()
     if args.whole:
         rec = {"mode": "whole", "ne": args.ne, "P": args.P}
-        ns, _ = build_solver(None, args.ne, args.P)
+        ns, _ = build_solver(None, args.ne, args.P, interior=args.interior)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         vs = ns._velocity_solver()
@@ -411,6 +415,7 @@ def main():
     ap.add_argument("--G", type=int, default=8, help="solo: ranks of the simulated partition")
     ap.add_argument("--ranks", default="0,3", help="solo: which ranks to run (one after the other)")
     ap.add_argument("--whole", type=int, default=1, help="solo: also time the whole-mesh matvec")
+    ap.add_argument("--interior", default="auto", help="velocity factorisation: auto (nested dissection), nested")
     ap.add_argument("--threads", type=int, default=16, help="rehearsal: host threads shared by the ranks")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
