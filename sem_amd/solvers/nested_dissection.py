@@ -343,14 +343,16 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 for (s, b), fids in sorted(by_depth[depth].items()):
                     nf, n = len(fids), s + b
                     F = torch.zeros(nf * n * n + 1, **z)           # + 1: the Dirichlet sink
-                    for k in range(2):
-                        self._extend_add(F, n, fids, k, U_leaf, fu)
+                    with self._phase(f"nd_extend_add_d{depth}"):
+                        for k in range(2):
+                            self._extend_add(F, n, fids, k, U_leaf, fu)
                     F = F[:-1].view(nf, n, n)
                     Ass = F[:, :s, :s]
-                    if s >= 1024:
-                        Sinv = torch.stack([pivot_inverse(Ass[q].contiguous()) for q in range(nf)])
-                    else:
-                        Sinv = batched_inverse(Ass.contiguous())
+                    with self._phase(f"nd_inverse_d{depth}"):
+                        if s >= 1024:
+                            Sinv = torch.stack([pivot_inverse(Ass[q].contiguous()) for q in range(nf)])
+                        else:
+                            Sinv = batched_inverse(Ass.contiguous())
                     Fw = torch.empty((nf, n, s), **z)
                     Fw[:, :s] = Sinv
                     if b:
@@ -375,7 +377,7 @@ class NestedDissectionSolver(VelocityJacobianSolver):
 
     def _extend_add(self, F, n, fids, k, U_leaf, fu):
         """F[slot] += child k's update of every front of the group, scattered by the child's position map (distinct
-        destinations within one call; the Dirichlet rows / columns go to the sink entry F[-1])."""
+        destinations within one call; the Dirichlet rows / columns go to the sink entry F[-1], never read)."""
         t, dev = self.tree, self.device
         sink = F.numel() - 1
         groups = {}
@@ -396,7 +398,10 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 bad = pos < 0
                 dest = q[:, None, None] * (n * n) + pos[:, :, None] * n + pos[:, None, :]
                 dest = dest.masked_fill(bad[:, :, None] | bad[:, None, :], sink)
-                F.index_put_((dest.reshape(-1),), src.reshape(-1), accumulate=True)
+                # index_add_ (atomic adds, no sort): every destination but the sink receives one value per call, so the
+                # sums are deterministic.  index_put_(accumulate=True) sorted the indices and, with four processes
+                # sharing one GPU, spent up to a minute per level in its temporaries (profiles/r06/strip/)
+                F.index_add_(0, dest.reshape(-1), src.reshape(-1))
 
     # ------------------------------------------------------------------ solve plan
     def _build_steps(self):

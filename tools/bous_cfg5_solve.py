@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--continuation", default="", help="Ra stages before --Ra (each starts from the last)")
     ap.add_argument("--out", default="")
     ap.add_argument("--ckpt", default="", help="directory for each finished stage's state (rank 0)")
+    ap.add_argument("--interior", default="", help="velocity factorisation: auto (nested dissection) or nested")
     ap.add_argument("--x0", default="", help="start from a saved state (.npy of [T, u, v, p])")
     args = ap.parse_args()
     if "RANK" not in os.environ:
@@ -54,6 +55,8 @@ def main():
         else:
             c = partitioned_coupler(dist, 1.0, 1.0, Re, Ra, Pr, args.P, args.ne, args.ne, args.P, args.ne, args.ne,
                                     mode=args.mode, iprint=2 if rank == 0 else 0)
+        if args.interior:   # A/B of the velocity factorisation (NavierStokesSolver velocity_interior)
+            c.ns._velocity_interior = args.interior
         if rank == 0:   # progress lines from the Schur / CD Krylov solves, and the factorisation times
             c.ns._progress, c.cd._progress = 250, 250
             c.ns._iprint = ["LU_suc"]

@@ -184,7 +184,7 @@ def rehearsal(args):
     say = (lambda m: print(f"[strip_profile r0 {time.strftime('%H:%M:%S')}] {m}", flush=True)) if rank == 0 \
         else (lambda m: None)
     rec = {"mode": "rehearsal", "backend": "gloo", "world": world, "rank": rank, "ne": args.ne, "P": args.P}
-    ns, _ = build_solver(dist, args.ne, args.P)
+    ns, _ = build_solver(dist, args.ne, args.P, interior=args.interior)
     rec["strip"] = [ns._mesh.ex_begin, ns._mesh.ex_end]
     rec["n_local"] = ns._mesh.n_local
     torch.cuda.synchronize(dev)
@@ -193,7 +193,18 @@ def rehearsal(args):
     torch.cuda.synchronize(dev)
     rec["factor_s"] = time.perf_counter() - t0
     rec["refine"], rec["refine_eta"] = bool(vs.refine), vs.refine_eta
-    say(f"factor {rec['factor_s']:.2f} s, backward error {vs.refine_eta:.1e}, refine {vs.refine}")
+    rec["factor_phases"] = dict(getattr(vs, "timing", {}))
+    say(f"factor {rec['factor_s']:.2f} s, backward error {vs.refine_eta:.1e}, refine {vs.refine}, "
+        f"phases {rec['factor_phases']}")
+    if args.refactor:   # a second factorisation of the same linearisation: first-call costs against steady state
+        ns._velo = None
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        vs = ns._strip_velocity_solver()
+        torch.cuda.synchronize(dev)
+        rec["refactor_s"] = time.perf_counter() - t0
+        rec["refactor_phases"] = dict(getattr(vs, "timing", {}))
+        say(f"refactor {rec['refactor_s']:.2f} s, phases {rec['refactor_phases']}")
     for k in list(stats):
         stats[k][:] = [0, 0, 0.0]
     wall, tab = time_eager_matvecs(ns, vs, args.reps, dev)
@@ -415,6 +426,7 @@ def main():
     ap.add_argument("--G", type=int, default=8, help="solo: ranks of the simulated partition")
     ap.add_argument("--ranks", default="0,3", help="solo: which ranks to run (one after the other)")
     ap.add_argument("--whole", type=int, default=1, help="solo: also time the whole-mesh matvec")
+    ap.add_argument("--refactor", type=int, default=0, help="rehearsal: time a second factorisation")
     ap.add_argument("--interior", default="auto", help="velocity factorisation: auto (nested dissection), nested")
     ap.add_argument("--threads", type=int, default=16, help="rehearsal: host threads shared by the ranks")
     ap.add_argument("--out", default="")
