@@ -66,6 +66,10 @@ def parse():
                          "overlap only strips of >= 2^20 local DOFs -- the overlapped step's two extra position-ranged "
                          "launches and cross-stream waits cost ~6 us per step (measured over a one-rank RCCL group, "
                          "profiles/r06/rccl/), more than a small strip's interior apply it could hide")
+    ap.add_argument("--vsolve-ne", type=int, default=128,
+                    help="N = 1: also time the NS velocity solve (nested dissection) on this mesh at --vsolve-P "
+                         "(BASELINE cfg5: 128, P = 12; 0 = skip)")
+    ap.add_argument("--vsolve-P", type=int, default=12)
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "p2p"],
                     help="interface assembly for N > 1: one RCCL all-reduce, or send/recv with the two neighbours")
     return ap.parse_args()
@@ -247,6 +251,47 @@ def cpu_baseline(P, ne, Pe, seconds):
             "sample": f"cfg2 64x64 P=8 (N={N}): median of {len(ts)} reps of (SciPy CSR Sys@T + Dirichlet "
                       f"rows) = {med * 1e3:.3f} ms, 1 thread pinned to 1 core of {os.cpu_count()} host threads "
                       f"(oracle/sem_oracle.py restatement of ConvectionDiffusion_Solver.py:85-87,112-119)"}
+
+
+def velocity_solve_line(ne, P, dev, solves=20):
+    """The inner solve of every NS Schur-complement matvec (NavierStokes_Solver.py:189-203): the velocity Jacobian of a
+    smooth linearisation (Re = 1e3, Ra = 1e6, cfg5's mesh by default) factored by nested dissection
+    (solvers/nested_dissection.py), then `solves` graph-replayed solves timed with HIP events; bytes = the operators
+    one solve streams (tree.bytes_per_solve)."""
+    import time
+    import numpy as np
+    from sem_amd.solvers import NavierStokesSolver
+    ns = NavierStokesSolver(1.0, 1.0, 1e3, 1e6 / 0.71, P, ne, ne, mtol=1e-10, mtol_newton=1e-10, iprint=[])
+    x, y = ns.points
+    u0 = 1e-2 * np.sin(np.pi * x) * np.sin(2 * np.pi * y)
+    v0 = -1e-2 * np.sin(2 * np.pi * x) * np.sin(np.pi * y)
+    ns._get_residuals(u0, v0, np.zeros(ns.N), 0.5 - x)
+    ns._calc_jacobians(u0, v0)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    vs = ns._velocity_solver()
+    torch.cuda.synchronize(dev)
+    factor_s = time.perf_counter() - t0
+    r = np.random.default_rng(5)
+    bu, bv = (ns._dev(r.uniform(-1, 1, ns.N)) for _ in range(2))
+    for _ in range(3):
+        vs.solve(bu, bv)
+    torch.cuda.synchronize(dev)
+    ts = []
+    for _ in range(solves):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        vs.solve(bu, bv)
+        b.record()
+        torch.cuda.synchronize(dev)
+        ts.append(a.elapsed_time(b) * 1e-3)
+    t = float(np.median(ts))
+    nbytes = vs.tree.bytes_per_solve() if vs.interior == "nd" else None
+    return {"workload": f"ns_velocity_solve_{ne}x{ne}_P{P}", "factorisation": vs.interior, "unknowns": 2 * ns.N,
+            "ms_per_solve": t * 1e3, "factor_s": factor_s, "backward_error": vs.refine_eta,
+            "graph": getattr(vs, "_graph", None) is not None, "bytes_per_solve": nbytes,
+            "achieved_GBs": nbytes / t / 1e9 if nbytes else None,
+            "frac_hbm": nbytes / t / 1e9 / HBM_PEAK_GBS if nbytes else None}
 
 
 def load_pmc(workload, kernel):
@@ -453,6 +498,13 @@ def main():
             wn = args.weak_ne
             out["weak_hbm"] = dict(extra(wn * world, wn, 1.0 / wn, 6072 + rank, False), scaling="weak")
             torch.cuda.empty_cache()
+
+    if rank == 0 and world == 1 and args.vsolve_ne > 0:
+        try:
+            out["velocity_solve"] = velocity_solve_line(args.vsolve_ne, args.vsolve_P, dev)
+        except (RuntimeError, ValueError) as e:   # an extra key: it never fails the headline line
+            out["velocity_solve"] = {"error": str(e)[:300]}
+        torch.cuda.empty_cache()
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(P, ne, Pe, args.cpu_seconds)

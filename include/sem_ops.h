@@ -399,6 +399,10 @@ int sem_gemv_rows2(int M, double alpha, double beta, int K0, const double* A0, i
  * summation order for a given `lanes`). */
 typedef struct sem_front_launch {
   int ntiles, rows, lanes, kmax, back;
+  /* form 0: row-major operators, `lanes` lanes per row (above); form 1: each operator stored TRANSPOSED (A^T: K
+   * rows of ld_f >= R_f doubles, 8-byte aligned), one thread per output row, rows = 256 (short rows: the deepest
+   * separators' |S| = 2 (P - 1) columns). */
+  int form;
   const int64_t* op;
   const int32_t* dims;
   const int64_t* xoff;

@@ -66,7 +66,7 @@ class SemNsDesc(C.Structure):
 
 class SemFrontLaunch(C.Structure):
     _fields_ = [("ntiles", C.c_int), ("rows", C.c_int), ("lanes", C.c_int), ("kmax", C.c_int), ("back", C.c_int),
-                ("op", C.c_void_p),
+                ("form", C.c_int), ("op", C.c_void_p),
                 ("dims", C.c_void_p), ("xoff", C.c_void_p), ("yoff", C.c_void_p), ("tiles", C.c_void_p),
                 ("xidx", C.c_void_p), ("yidx", C.c_void_p), ("W", C.c_void_p), ("stage", C.c_void_p)]
 

@@ -117,6 +117,48 @@ __global__ __launch_bounds__(256) void front_sparse_rows_kernel(int nitems, int 
   stage[i * stride + out_off + r] = v;
 }
 
+// form 1 (columns): the operator stored transposed (A^T: K rows of ld >= R doubles), one thread per output row, so
+// the fronts whose rows are a few tens of doubles long (the deepest separators: |S| = 2 (P - 1)) stream whole
+// coalesced A^T rows; x in LDS.  Each row sums its K products in order (two accumulators: even and odd k).
+template <int UK>
+__global__ __launch_bounds__(256) void front_gemv_cols_kernel(const sem_front_launch a) {
+  extern __shared__ double xs[];
+  const int f = a.tiles[2 * blockIdx.x], r0 = a.tiles[2 * blockIdx.x + 1];
+  const int R = a.dims[4 * f], K = a.dims[4 * f + 1], ld = a.dims[4 * f + 2];
+  const int32_t* xi = a.xidx + a.xoff[f];
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const int p = xi[k];
+    xs[k] = p >= 0 ? a.W[p] : 0.0;
+  }
+  __syncthreads();
+  const int r = r0 + static_cast<int>(threadIdx.x);
+  if (r >= R) return;
+  const double* A = reinterpret_cast<const double*>(a.op[f]) + r;
+  double acc0 = 0.0, acc1 = 0.0;
+  int k = 0;
+  for (; k + UK <= K; k += UK) {
+    double av[UK];
+#pragma unroll
+    for (int u = 0; u < UK; ++u) av[u] = __builtin_nontemporal_load(A + static_cast<int64_t>(k + u) * ld);
+#pragma unroll
+    for (int u = 0; u < UK; u += 2) {
+      acc0 = fma(av[u], xs[k + u], acc0);
+      if (u + 1 < UK) acc1 = fma(av[u + 1], xs[k + u + 1], acc1);
+    }
+  }
+  for (; k < K; ++k) {
+    const double v = __builtin_nontemporal_load(A + static_cast<int64_t>(k) * ld);
+    if (k & 1) acc1 = fma(v, xs[k], acc1); else acc0 = fma(v, xs[k], acc0);
+  }
+  const double v = acc0 + acc1;
+  if (a.back) {
+    const int p = a.yidx[a.yoff[f] + r];
+    a.W[p] -= v;
+  } else {
+    a.stage[a.yoff[f] + r] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void front_scatter_kernel(int ncopy, const int32_t* __restrict__ ct,
                                                             const int32_t* __restrict__ cs, int nacc,
                                                             const int32_t* __restrict__ at,
@@ -151,6 +193,12 @@ int sem_front_gemv(const sem_front_launch* d, void* stream) {
   if (lds > 64 * 1024) return sem::set_error(SEM_EUNSUPPORTED, "front_gemv: more than 8192 operands per front");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid(d->ntiles), block(256);
+  if (d->form == 1) {   // columns: A^T rows, one thread per output row, 256 rows per workgroup
+    if (d->rows != 256) return sem::set_error(SEM_EINVAL, "front_gemv: the column form takes 256 rows per workgroup");
+    hipLaunchKernelGGL((sem::front_gemv_cols_kernel<8>), grid, block, lds, s, *d);
+  } else if (d->form != 0) {
+    return sem::set_error(SEM_EINVAL, "front_gemv: form must be 0 (rows) or 1 (columns)");
+  } else
 #define SEM_FRONT_CASE(L, ROWS, RW, U)                                                   \
   if (d->lanes == L && d->rows == ROWS) {                                                \
     hipLaunchKernelGGL((sem::front_gemv_kernel<L, RW, U>), grid, block, lds, s, *d);     \

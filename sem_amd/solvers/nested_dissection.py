@@ -550,9 +550,13 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 raise AssertionError("nested dissection: index outside int32")
             return torch.as_tensor(a.astype(np.int32), device=dev)
 
+        transposed = {}     # id(group tensor) -> its operators transposed (form 1)
         for st in self._steps:
             items, back = st[1], st[0] == "back"
             nf = len(items)
+            Ks = np.array([it[0].shape[2] for it in items])
+            leaves = any(items[0][0] is t for t in (self._lift, self._leafF, self._leafV))
+            form = self._launch_form(back, nf, Ks, leaves)
             ptr = np.empty(nf, dtype=np.int64)
             dims = np.zeros((nf, 4), dtype=np.int64)
             xoff = np.zeros(nf, dtype=np.int64)
@@ -563,10 +567,19 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 R, K = T.shape[1], T.shape[2]
                 if T.stride(2) != 1 or T.stride(1) != K or K % 2 or T.dtype != torch.float64 or T.device != dev:
                     raise AssertionError("nested dissection: operators must be contiguous float64 rows of even length")
-                ptr[k] = T.data_ptr() + q * T.stride(0) * 8
-                if ptr[k] % 16 or not 0 <= q < T.shape[0]:
-                    raise AssertionError("nested dissection: operator rows must be 16-byte aligned")
-                dims[k, :3] = (R, K, K)
+                if not 0 <= q < T.shape[0]:
+                    raise AssertionError("nested dissection: operator slot outside its group")
+                if form == 1:   # A^T, one thread per row
+                    Tt = transposed.get(id(T))
+                    if Tt is None:
+                        Tt = transposed[id(T)] = (T, T.transpose(1, 2).contiguous())
+                    ptr[k] = Tt[1].data_ptr() + q * Tt[1].stride(0) * 8
+                    dims[k, :3] = (R, K, R)
+                else:
+                    ptr[k] = T.data_ptr() + q * T.stride(0) * 8
+                    if ptr[k] % 16:
+                        raise AssertionError("nested dissection: operator rows must be 16-byte aligned")
+                    dims[k, :3] = (R, K, K)
                 if len(xidx) != K:
                     raise AssertionError("nested dissection: operand count differs from the operator width")
                 xoff[k] = xo
@@ -590,14 +603,21 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 if yidx.min() < 0 or yidx.max() >= nW or len(np.unique(yidx)) != len(yidx):
                     raise AssertionError("nested dissection: back-substitution targets must be distinct line entries")
             R = dims[:, 0]
-            lanes, rows = self._launch_shape(dims[:, 1], R)
+            if form == 1:
+                lanes, rows = 1, 256
+            elif form == 2:
+                lanes, rows = 64, 8
+            else:
+                lanes, rows = self._launch_shape(dims[:, 1], R)
             nt = (R + rows - 1) // rows
             tiles = np.stack((np.repeat(np.arange(nf), nt),
                               np.concatenate([np.arange(n) * rows for n in nt])), 1)
             keep = dict(ptr=torch.as_tensor(ptr, device=dev), dims=i32(dims), xoff=torch.as_tensor(xoff, device=dev),
                         yoff=torch.as_tensor(yoff, device=dev), tiles=i32(tiles), xidx=i32(xidx),
-                        yidx=i32(yidx) if back else None)
-            d = _lib.SemFrontLaunch(len(tiles), rows, lanes, int(dims[:, 1].max()), int(back), keep["ptr"].data_ptr(),
+                        yidx=i32(yidx) if back else None, transposed=[v[1] for v in transposed.values()])
+            transposed = {}
+            d = _lib.SemFrontLaunch(len(tiles), rows, lanes, int(dims[:, 1].max()), int(back), form,
+                                    keep["ptr"].data_ptr(),
                                     keep["dims"].data_ptr(), keep["xoff"].data_ptr(), keep["yoff"].data_ptr(),
                                     keep["tiles"].data_ptr(), keep["xidx"].data_ptr(),
                                     keep["yidx"].data_ptr() if back else None, None,
@@ -629,6 +649,16 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                           out_off=q["out_off"])
             plan.append((d, keep, sc, sp))
         return plan
+
+    def _launch_form(self, back, nf, K, leaves):
+        """sem_front_gemv's form for one launch (`forms` = "auto", or "rows" for every launch in form 0): 1 (columns:
+        transposed operators, a thread per row) for the forward front levels whose rows are <= 64 doubles (the
+        deepest separators: cfg5 d13-d11 124 / 111 / 85 -> 74 / 79 / 71 us, profiles/r06/velocity/nd/), else 0 (lanes
+        per row).  A k-split form for the few long top fronts (operands in registers, four waves per row set)
+        measured slower than form 0 there (+10-25 %) and was not kept."""
+        if getattr(self, "forms", "auto") != "auto" or leaves:
+            return 0
+        return 1 if not back and int(np.median(K)) <= 64 else 0
 
     # (lanes per row, rows per workgroup) of sem_front_gemv: (wide, narrow) per lane count
     SHAPES = {64: (16, 4), 32: (16, 8), 16: (32, 16), 8: (64, 32), 4: (128, 64)}

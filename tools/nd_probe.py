@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--solves", type=int, default=20)
     ap.add_argument("--lines", type=int, default=1, help="also factor and time the line condensation")
     ap.add_argument("--steps", type=int, default=1, help="per-step eager timing of the ND solve")
+    ap.add_argument("--ab-forms", type=int, default=0,
+                    help="also time every launch in sem_front_gemv's form 0 (forms='rows') against the default plan")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     from sem_amd.solvers import NavierStokesSolver
@@ -87,6 +89,20 @@ def main():
     xe = nd._solve_lines(torch.stack((bu.view(nd.NX, -1), bv.view(nd.NX, -1)), 1).reshape(nd.NX, -1))
     out["nd"]["graph_equals_eager"] = bool(torch.equal(xe.view(nd.NX, 2, -1)[:, 0].reshape(-1), xu)
                                            and torch.equal(xe.view(nd.NX, 2, -1)[:, 1].reshape(-1), xv))
+    if args.ab_forms:   # the same factor, every launch in form 0, then back to the default plan (alternated)
+        ts_auto, ts_rows = [], []
+        for _ in range(3):
+            for forms, acc in (("rows", ts_rows), ("auto", ts_auto)):
+                nd.forms = forms
+                nd._hip = nd._hip_plan()
+                nd.capture()
+                t_, xu_f, xv_f = timed(nd)
+                acc.extend(t_)
+                if forms == "rows":
+                    xr = (xu_f.clone(), xv_f.clone())
+        out["nd"]["ab_forms"] = {"rows_ms_median": float(np.median(ts_rows)), "auto_ms_median": float(np.median(ts_auto)),
+                                 "rel_diff": float(max((xu_f - xr[0]).abs().max(), (xv_f - xr[1]).abs().max())
+                                                   / max(xr[0].abs().max(), xr[1].abs().max()))}
     if args.steps:
         lib = _lib.load()
         W = torch.stack((bu.view(nd.NX, -1), bv.view(nd.NX, -1)), 1).reshape(-1).clone()
@@ -117,13 +133,14 @@ def main():
             dims = keep["dims"].cpu().numpy()
             byts = int((dims[:, 0].astype(np.int64) * dims[:, 1]).sum() * 8) + (sp["coef"].numel() * 8 if sp else 0)
             steps.append({"step": k, "back": d.back, "fronts": int(dims.shape[0]), "tiles": d.ntiles, "rows": d.rows,
-                          "lanes": d.lanes,
+                          "lanes": d.lanes, "form": d.form,
                           "us": float(us[k]), "op_MB": byts / 1e6, "TBs": byts / (us[k] * 1e-6) / 1e12})
         out["nd"]["steps"] = steps
         out["nd"]["steps_sum_us"] = float(us.sum())
     if args.lines:
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
+        ns._velocity_interior, ns._velo = "nested", None     # the line condensation (the default is now ND)
         vs = ns._velocity_solver()
         torch.cuda.synchronize(dev)
         out["lines"] = {"factor_s": time.perf_counter() - t0, "eta": vs.refine_eta}
