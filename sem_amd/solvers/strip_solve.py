@@ -20,6 +20,12 @@ the interface right-hand side (a shared line's b counted by its right owner only
 elimination to the two boundary lines, ONE all-gather of 2 m doubles per rank, the replicated reduced
 solve, local back substitution, interior back substitution.  x comes out on every rank's lines, equal
 on shared lines.
+
+The reduced system over the strip-boundary lines (step 3 and the solve's all-gather + GEMV) and the agreed graph
+capture live in `_StripReduced`, which the NS velocity solve's default strip solver shares:
+nested_dissection.StripNDSolver eliminates each strip by nested dissection instead of by lines and hands the same
+reduced system its Schur complement on the strip's two interface lines.  StripLineSolver stays the strip solver of
+the other Dirichlet sets (the CD Jacobian's W / E rows).
 """
 import os
 
