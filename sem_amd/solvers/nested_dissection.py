@@ -595,6 +595,9 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                     if out < 0 or out + R > self._stage_len:
                         raise AssertionError("nested dissection: stage overflow")
                     yoff[k] = out
+            if int(dims[:, 1].max()) > 8192:
+                raise ValueError("nested dissection: a front with more than 8192 operands (sem_front_gemv stages them "
+                                 "in LDS); the mesh is too large for this dissection")
             xidx = np.concatenate(xs)
             if xidx.size and (xidx.min() < -1 or xidx.max() >= nW):
                 raise AssertionError("nested dissection: operand index outside the line array")
