@@ -414,7 +414,7 @@ typedef struct sem_front_launch {
   double* stage;
 } sem_front_launch;
 int sem_front_gemv(const sem_front_launch* d, void* stream);
-/* stage[i stride + out_off + r] = sum_q coef[(i nrows + r) nnz + q] stage[i stride + pat[r nnz + q]] for items
+/* stage[i stride + out_off + r] = sum_q coef[(i nnz + q) nrows + r] stage[i stride + pat[q nrows + r]] for items
  * i < nitems, rows r < nrows (pattern shared by the items; entries pat[.] < stride and out_off + nrows <= stride,
  * the operand and output ranges of an item disjoint): the leaves' boundary update A_bi y_i of the nested-dissection
  * forward solve, from the P - 1 couplings of each element-boundary unknown to its line or column.  Device memory. */

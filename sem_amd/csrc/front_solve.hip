@@ -109,11 +109,13 @@ __global__ __launch_bounds__(256) void front_sparse_rows_kernel(int nitems, int 
   if (t >= static_cast<int64_t>(nitems) * nrows) return;
   const int64_t i = t / nrows;
   const int r = static_cast<int>(t - i * nrows);
-  const double* c = coef + t * nnz;
-  const int32_t* p = pat + static_cast<int64_t>(r) * nnz;
+  // coefficient q of row r at coef[(i nnz + q) nrows + r], pattern at pat[q nrows + r]: a wave's loads of one q are
+  // consecutive rows (the row-major (nrows, nnz) layout strode 8 nnz bytes per lane: 4.6x the bytes from HBM)
+  const double* c = coef + i * nnz * nrows + r;
+  const int32_t* p = pat + r;
   const double* y = stage + i * stride;
   double v = 0.0;
-  for (int q = 0; q < nnz; ++q) v = fma(c[q], y[p[q]], v);
+  for (int q = 0; q < nnz; ++q) v = fma(c[static_cast<int64_t>(q) * nrows], y[p[q * nrows]], v);
   stage[i * stride + out_off + r] = v;
 }
 

@@ -648,8 +648,9 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                         or pat.max() >= q["out_off"] or q["out_off"] + nrows > q["stride"]
                         or q["nitems"] * q["stride"] > self._stage_len):
                     raise AssertionError("nested dissection: bad sparse boundary step")
-                sp = dict(nitems=q["nitems"], nrows=nrows, nnz=nnz, coef=coef, pat=i32(pat), stride=q["stride"],
-                          out_off=q["out_off"])
+                # the kernel reads coefficient q of every row together: (items, nnz, nrows) and (nnz, nrows)
+                sp = dict(nitems=q["nitems"], nrows=nrows, nnz=nnz, coef=coef.transpose(1, 2).contiguous(),
+                          pat=i32(pat.T), stride=q["stride"], out_off=q["out_off"])
             plan.append((d, keep, sc, sp))
         return plan
 
