@@ -257,7 +257,7 @@ def velocity_solve_line(ne, P, dev, solves=20):
     """The inner solve of every NS Schur-complement matvec (NavierStokes_Solver.py:189-203): the velocity Jacobian of a
     smooth linearisation (Re = 1e3, Ra = 1e6, cfg5's mesh by default) factored by nested dissection
     (solvers/nested_dissection.py), then `solves` graph-replayed solves timed with HIP events; bytes = the operators
-    one solve streams (tree.bytes_per_solve)."""
+    one solve streams (bytes_per_solve)."""
     import time
     import numpy as np
     from sem_amd.solvers import NavierStokesSolver
@@ -286,7 +286,7 @@ def velocity_solve_line(ne, P, dev, solves=20):
         torch.cuda.synchronize(dev)
         ts.append(a.elapsed_time(b) * 1e-3)
     t = float(np.median(ts))
-    nbytes = vs.tree.bytes_per_solve() if vs.interior == "nd" else None
+    nbytes = vs.bytes_per_solve() if vs.interior == "nd" else None
     return {"workload": f"ns_velocity_solve_{ne}x{ne}_P{P}", "factorisation": vs.interior, "unknowns": 2 * ns.N,
             "ms_per_solve": t * 1e3, "factor_s": factor_s, "backward_error": vs.refine_eta,
             "graph": getattr(vs, "_graph", None) is not None, "bytes_per_solve": nbytes,

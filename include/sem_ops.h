@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SEM_ABI_VERSION 14
+#define SEM_ABI_VERSION 15
 
 enum sem_status {
   SEM_OK = 0,
@@ -425,6 +425,29 @@ int sem_front_sparse_rows(int nitems, int nrows, int nnz, const double* coef, co
  * 16-byte aligned).  Targets distinct.  Device memory; stream-ordered. */
 int sem_front_scatter(int ncopy, const int32_t* copy_tgt, const int32_t* copy_src, int nacc, const int32_t* acc_tgt,
                       const int32_t* acc_src4, const double* stage, double* W, void* stream);
+/* ABI 15: the element leaves' forward step of the two-component (u, v) velocity Jacobian in ONE launch, one
+ * workgroup per element.  The element's interior block A_ii = [A_uu D1; D2 A_vv] couples the components only
+ * through the diagonal Newton terms D1, D2 (mass-lumped: NavierStokes_Solver.py:123-136), so y_i = A_ii^-1 b_i is
+ *   t = A_uu^-1 b_u;  y_v = S_v^-1 (b_v - D2 t);  y_u = t - A_uu^-1 (D1 y_v)      (S_v = A_vv - D2 A_uu^-1 D1)
+ * with A_uu^-1 held in registers between its two products: two n x n operators read per element instead of the
+ * (2n)^2 of A_ii^-1.  Then y_i is written to W (its interior entries: read by no other element), and the boundary
+ * rows g_r = sum_q coef[q nb + r] y[pat[q nb + r]] (A_bi y_i on its line / column pattern) go to
+ * stage[e sstride + soff + r] for the scatter.
+ * Per element e, at blob + e stride (16-byte aligned, stride even): A_uu^-1 (n x ld), S_v^-1 (n x ld), D1 (ld),
+ * D2 (ld), coef (nnz x nb); ld = n rounded up to even, pad entries zero; n = (P - 1)^2 <= 121.
+ * iidx[e 2n + k]: W index of interior u node k (k < n), v node k - n (k >= n); pat (nnz x nb): positions in
+ * [y_u; y_v].  Deterministic; device memory; stream-ordered. */
+typedef struct sem_leaf_launch {
+  int nelem, n, ld, nb, nnz;
+  int64_t stride;
+  const double* blob;
+  const int32_t* iidx;
+  const int32_t* pat;
+  double* W;
+  double* stage;
+  int64_t sstride, soff;
+} sem_leaf_launch;
+int sem_leaf_forward(const sem_leaf_launch* d, void* stream);
 
 /* ---- GMRES least-squares column (host) ------------------------------------ */
 /* Host memory, no device work (ABI 11): applies the Givens rotations 0..k-1 (cs, sn) to col[0..k+1], forms

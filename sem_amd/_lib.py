@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.environ.get("SEM_LIBDIR") or os.path.join(_HERE, "lib"), "libsemops.so")
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 SEM_OK, SEM_EINVAL, SEM_EHIP, SEM_ENOMEM, SEM_EUNSUPPORTED = 0, 1, 2, 3, 4
 # kernel-selection knobs (include/sem_ops.h enum sem_tune; process-global, not thread-safe); the values between
 # them are retired knobs (round 6), refused by sem_set_tuning
@@ -71,6 +71,12 @@ class SemFrontLaunch(C.Structure):
                 ("xidx", C.c_void_p), ("yidx", C.c_void_p), ("W", C.c_void_p), ("stage", C.c_void_p)]
 
 
+class SemLeafLaunch(C.Structure):
+    _fields_ = [("nelem", C.c_int), ("n", C.c_int), ("ld", C.c_int), ("nb", C.c_int), ("nnz", C.c_int),
+                ("stride", C.c_int64), ("blob", C.c_void_p), ("iidx", C.c_void_p), ("pat", C.c_void_p),
+                ("W", C.c_void_p), ("stage", C.c_void_p), ("sstride", C.c_int64), ("soff", C.c_int64)]
+
+
 # name -> (restype, argtypes); mirrors include/sem_ops.h one-for-one
 _SIGS = {
     "sem_abi_version": (C.c_int, []),
@@ -123,6 +129,7 @@ _SIGS = {
     "sem_gemv_rows2": (C.c_int, [C.c_int, C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
                                  C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sem_front_gemv": (C.c_int, [C.POINTER(SemFrontLaunch), C.c_void_p]),
+    "sem_leaf_forward": (C.c_int, [C.POINTER(SemLeafLaunch), C.c_void_p]),
     "sem_front_sparse_rows": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.c_int64, C.c_void_p]),
     "sem_front_scatter": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,

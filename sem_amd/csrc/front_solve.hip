@@ -37,26 +37,48 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
   extern __shared__ double xs[];
   const int f = a.tiles[2 * blockIdx.x], r0 = a.tiles[2 * blockIdx.x + 1];
   const int R = a.dims[4 * f], K = a.dims[4 * f + 1], ld = a.dims[4 * f + 2];
-  const int32_t* xi = a.xidx + a.xoff[f];
-  for (int k = threadIdx.x; k < K; k += 256) {
-    const int p = xi[k];
-    xs[k] = p >= 0 ? a.W[p] : 0.0;
-  }
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (r0 + wave * G * RW >= R) return;  // the whole wave beyond the front (groups inside a wave stay together)
+  const bool live = r0 + wave * G * RW < R;  // a wave wholly beyond the front only helps gather
   const int g = lane / LPR, sl = lane % LPR;
   const int rb = r0 + (wave * G + g) * RW;
   const double* A = reinterpret_cast<const double*>(a.op[f]);
   const double* rows[RW];
 #pragma unroll
   for (int i = 0; i < RW; ++i) rows[i] = A + static_cast<int64_t>(min(rb + i, R - 1)) * ld;  // clamped: not stored
+  const int KP = K >> 1;  // K is even (the host checks): column pairs
+  int u = sl;
+  // the first batch of operator loads is in flight while the operands are gathered into LDS
+  const bool pre = live && u + LPR * (U - 1) < KP;
+  double2 a0[U][RW];
+  if (pre) {
+#pragma unroll
+    for (int t = 0; t < U; ++t)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) a0[t][i] = load_nt2(rows[i] + 2 * (u + LPR * t));
+  }
+  const int32_t* xi = a.xidx + a.xoff[f];
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const int p = xi[k];
+    xs[k] = p >= 0 ? a.W[p] : 0.0;
+  }
+  __syncthreads();
+  if (!live) return;  // groups inside a wave stay together for the reductions below
   double acc[RW][2];
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i][0] = acc[i][1] = 0.0;
-  const int KP = K >> 1;  // K is even (the host checks): column pairs
   const double2* x2 = reinterpret_cast<const double2*>(xs);
-  int u = sl;
+  if (pre) {
+#pragma unroll
+    for (int t = 0; t < U; ++t) {
+      const double2 xv = x2[u + LPR * t];
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        acc[i][0] = fma(a0[t][i].x, xv.x, acc[i][0]);
+        acc[i][1] = fma(a0[t][i].y, xv.y, acc[i][1]);
+      }
+    }
+    u += LPR * U;
+  }
   for (; u + LPR * (U - 1) < KP; u += LPR * U) {
     double2 av[U][RW], xv[U];
 #pragma unroll
@@ -127,17 +149,31 @@ __global__ __launch_bounds__(256) void front_gemv_cols_kernel(const sem_front_la
   extern __shared__ double xs[];
   const int f = a.tiles[2 * blockIdx.x], r0 = a.tiles[2 * blockIdx.x + 1];
   const int R = a.dims[4 * f], K = a.dims[4 * f + 1], ld = a.dims[4 * f + 2];
+  const int r = r0 + static_cast<int>(threadIdx.x);
+  const double* A = reinterpret_cast<const double*>(a.op[f]) + r;
+  const bool pre = r < R && UK <= K;  // the first UK loads in flight while the operands are gathered
+  double a0[UK];
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < UK; ++u) a0[u] = __builtin_nontemporal_load(A + static_cast<int64_t>(u) * ld);
+  }
   const int32_t* xi = a.xidx + a.xoff[f];
   for (int k = threadIdx.x; k < K; k += 256) {
     const int p = xi[k];
     xs[k] = p >= 0 ? a.W[p] : 0.0;
   }
   __syncthreads();
-  const int r = r0 + static_cast<int>(threadIdx.x);
   if (r >= R) return;
-  const double* A = reinterpret_cast<const double*>(a.op[f]) + r;
   double acc0 = 0.0, acc1 = 0.0;
   int k = 0;
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < UK; u += 2) {
+      acc0 = fma(a0[u], xs[u], acc0);
+      if (u + 1 < UK) acc1 = fma(a0[u + 1], xs[u + 1], acc1);
+    }
+    k = UK;
+  }
   for (; k + UK <= K; k += UK) {
     double av[UK];
 #pragma unroll
@@ -178,6 +214,107 @@ __global__ __launch_bounds__(256) void front_scatter_kernel(int ncopy, const int
     if (s.z >= 0) v -= stage[s.z];
     if (s.w >= 0) v -= stage[s.w];
     W[at[j]] = v;
+  }
+}
+
+// sem_leaf_forward: one workgroup per element.  Thread (wave w, lane l) owns rows w 8 + l / 8 + 32 k (k < RK) and
+// column pairs l % 8 + 8 u (u < 2 RK) of the element's two n x n inverses, so a row is summed by 8 lanes (pairs in
+// u order, then an xor tree).  A_uu^-1's fragment stays in registers from t = A_uu^-1 b_u to A_uu^-1 (D1 y_v);
+// S_v^-1 streams through once.  The operand vectors live in LDS, zero beyond n (the pad column multiplies them).
+template <int NR, int NU>
+__device__ __forceinline__ void leaf_rows(const double2 (&f)[NR][NU], const double* x, int s, double (&acc)[NR]) {
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int c = 2 * (s + 8 * u);
+      v0 = fma(f[k][u].x, x[c], v0);
+      v1 = fma(f[k][u].y, x[c + 1], v1);
+    }
+    double v = v0 + v1;
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    acc[k] = v;
+  }
+}
+
+template <int NR, int NU>
+__device__ __forceinline__ void leaf_load(double2 (&f)[NR][NU], const double* A, int n, int ld, int rs, int s) {
+#pragma unroll
+  for (int k = 0; k < NR; ++k)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int r = rs + 32 * k, c = 2 * (s + 8 * u);
+      f[k][u] = (r < n && c < n) ? load_nt2(A + static_cast<int64_t>(r) * ld + c) : make_double2(0.0, 0.0);
+    }
+}
+
+// KH rows of S_v^-1 tiles per load batch: RK = 4 streams it in two halves, so A_uu^-1's 128 registers and the
+// batch fit 256 (two workgroups per CU: 2.97 against 3.32 ms per cfg5 solve with the whole S_v^-1 tile in flight
+// at one workgroup per CU, profiles/r06/velocity/split/)
+template <int RK, int KH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void leaf_forward_kernel(
+    const sem_leaf_launch a) {
+  constexpr int NX = 32 * RK;   // operand slots: every column pair a lane touches
+  __shared__ double bu[NX], bv[NX], tt[NX], yv[NX];
+  const int e = blockIdx.x, n = a.n, ld = a.ld;
+  const double* Au = a.blob + static_cast<int64_t>(e) * a.stride;
+  const double* Sv = Au + static_cast<int64_t>(n) * ld;
+  const double* d1 = Sv + static_cast<int64_t>(n) * ld;
+  const double* d2 = d1 + ld;
+  const double* coef = d2 + ld;
+  const int tid = threadIdx.x, s = tid & 7, rs = tid >> 3;   // rs = w 8 + l / 8
+  double2 fa[RK][2 * RK];
+  leaf_load<RK, 2 * RK>(fa, Au, n, ld, rs, s);                      // in flight while the operands are gathered
+  const int32_t* ix = a.iidx + static_cast<int64_t>(e) * 2 * n;
+  for (int k = tid; k < NX; k += 256) {
+    bu[k] = k < n ? a.W[ix[k]] : 0.0;
+    bv[k] = k < n ? a.W[ix[n + k]] : 0.0;
+    yv[k] = 0.0;
+  }
+  __syncthreads();
+  double acc[RK];
+  leaf_rows<RK, 2 * RK>(fa, bu, s, acc);                   // t = A_uu^-1 b_u
+#pragma unroll
+  for (int k = 0; k < RK; ++k)
+    if (s == 0 && rs + 32 * k < n) tt[rs + 32 * k] = acc[k];
+  __syncthreads();
+  if (tid < n) bv[tid] -= d2[tid] * tt[tid];               // b_v - D2 t
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < RK; h += KH) {                       // y_v = S_v^-1 (b_v - D2 t), KH rows of tiles at a time
+    double2 fs[KH][2 * RK];
+    double ah[KH];
+    leaf_load<KH, 2 * RK>(fs, Sv, n, ld, rs + 32 * h, s);
+    leaf_rows<KH, 2 * RK>(fs, bv, s, ah);
+#pragma unroll
+    for (int k = 0; k < KH; ++k) acc[h + k] = ah[k];
+  }
+#pragma unroll
+  for (int k = 0; k < RK; ++k)
+    if (s == 0 && rs + 32 * k < n) yv[rs + 32 * k] = acc[k];
+  __syncthreads();
+  if (tid < n) bu[tid] = d1[tid] * yv[tid];                // D1 y_v
+  __syncthreads();
+  leaf_rows<RK, 2 * RK>(fa, bu, s, acc);                   // y_u = t - A_uu^-1 (D1 y_v)
+#pragma unroll
+  for (int k = 0; k < RK; ++k)
+    if (s == 0 && rs + 32 * k < n) tt[rs + 32 * k] -= acc[k];
+  __syncthreads();
+  for (int k = tid; k < n; k += 256) {
+    a.W[ix[k]] = tt[k];
+    a.W[ix[n + k]] = yv[k];
+  }
+  double* out = a.stage + static_cast<int64_t>(e) * a.sstride + a.soff;
+  for (int r = tid; r < a.nb; r += 256) {                 // A_bi y_i on the boundary rows' patterns
+    double g = 0.0;
+    for (int q = 0; q < a.nnz; ++q) {
+      const int p = a.pat[q * a.nb + r];
+      g = fma(coef[static_cast<int64_t>(q) * a.nb + r], p < n ? tt[p] : yv[p - n], g);
+    }
+    out[r] = g;
   }
 }
 
@@ -245,6 +382,32 @@ int sem_front_scatter(int ncopy, const int32_t* copy_tgt, const int32_t* copy_sr
                      W);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("front_scatter launch: ") + hipGetErrorString(e));
+  return SEM_OK;
+}
+
+int sem_leaf_forward(const sem_leaf_launch* d, void* stream) {
+  if (!d) return sem::set_error(SEM_EINVAL, "leaf_forward: null descriptor");
+  if (d->nelem < 0 || d->n < 1 || d->n > 121 || d->ld < d->n || d->ld % 2 || d->nb < 0 || d->nnz < 0 ||
+      d->stride < 2 * static_cast<int64_t>(d->n) * d->ld + 2 * d->ld + static_cast<int64_t>(d->nnz) * d->nb ||
+      d->stride % 2 || d->sstride < 0 || d->soff < 0)
+    return sem::set_error(SEM_EINVAL, "leaf_forward: bad sizes (n <= 121, ld even >= n, stride even >= the blob)");
+  if (d->nelem == 0) return SEM_OK;
+  if (!d->blob || !d->iidx || !d->pat || !d->W || !d->stage)
+    return sem::set_error(SEM_EINVAL, "leaf_forward: null argument");
+  if (reinterpret_cast<uintptr_t>(d->blob) % 16) return sem::set_error(SEM_EINVAL, "leaf_forward: blob not 16-byte aligned");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid(d->nelem), block(256);
+  const int rk = (d->n + 32) / 32;   // 32 RK operand slots >= n + 1 (the pad column)
+  if (rk == 1)
+    hipLaunchKernelGGL((sem::leaf_forward_kernel<1, 1>), grid, block, 0, s, *d);
+  else if (rk == 2)
+    hipLaunchKernelGGL((sem::leaf_forward_kernel<2, 2>), grid, block, 0, s, *d);
+  else if (rk == 3)
+    hipLaunchKernelGGL((sem::leaf_forward_kernel<3, 3>), grid, block, 0, s, *d);
+  else
+    hipLaunchKernelGGL((sem::leaf_forward_kernel<4, 2>), grid, block, 0, s, *d);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sem::set_error(SEM_EHIP, std::string("leaf_forward launch: ") + hipGetErrorString(e));
   return SEM_OK;
 }
 

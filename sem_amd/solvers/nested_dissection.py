@@ -173,11 +173,20 @@ class NDTree:
                 maps.append(pos)
             f["maps"] = maps
 
-    def bytes_per_solve(self):
-        """Operator bytes one solve reads: lift, leaves (Xi, the sparse A_bi, V_e), fronts (Fw, V)."""
+    def split_perm(self):
+        """The interior positions of the u nodes, then the v nodes (element-local order (i, c, j): a component's
+        interior block is every other run of P - 1)."""
+        return np.concatenate([self.loc[1:self.P, 1:self.P, c].reshape(-1) for c in range(self.nc)])
+
+    def bytes_per_solve(self, split=False):
+        """Operator bytes one solve reads: lift, leaves (Xi -- or, split, the per-component blob A_uu^-1, S_v^-1,
+        D1, D2 -- the sparse A_bi, V_e), fronts (Fw, V)."""
         E = (self.xb - self.xa) * self.ney
         nper = int(np.any(self.eD[:, self.ni:], axis=1).sum())
-        leaf = E * (self.ni * self.ni + self.nb * (self.P - 1) + self.ni * self.nb)
+        n = (self.P - 1) ** 2
+        ld = n + (n & 1)
+        fwd = 2 * n * ld + 2 * ld if split else self.ni * self.ni
+        leaf = E * (fwd + self.nb * (self.P - 1) + self.ni * self.nb)
         fr = sum(len(f["S"]) * (len(f["S"]) + 2 * len(f["B"])) for f in self.fronts)
         return 8 * (nper * self.ne * self.nb + leaf + fr)
 
@@ -280,13 +289,46 @@ class NestedDissectionSolver(VelocityJacobianSolver):
         whole perimeter (dir_sides = all four, no explicit mask)."""
         if dir_mask is not None or dir_sides != ALL_SIDES:
             raise ValueError("nested dissection needs the whole perimeter Dirichlet (side bits, no mask)")
+        n = (self.P - 1) ** 2
+        U_leaf = None
+        if self.tree.nc == 2 and n <= 121:      # the split leaf (sem_leaf_forward) unless its probe refuses it
+            U_leaf = self._factor_leaves(dx, dy, kw, True)
+        if U_leaf is None:                      # Xi (sem_front_gemv)
+            U_leaf = self._factor_leaves(dx, dy, kw, False)
+        t = self.tree
+        kind, rid = t.root
+        self._root_update = U_leaf[rid].clone() if kind == "e" else None   # a strip's Schur complement on its lines
+        self._factor_fronts(U_leaf)
+        del U_leaf
+        self._build_steps()
+        self.factored = True
+
+    # the split leaf's probe bound: its backward error on a random right-hand side per element (explicit A_ii^-1:
+    # <= 9e-16 on the oracle's random Jacobians; split: 4.7e-16 at cfg4's Ra = 1e6 state, up to 2e-13 where the
+    # Newton coupling rivals the stiffness, i.e. random velocity fields -- those factor with Xi)
+    SPLIT_ETA = 4e-15
+
+    def _factor_leaves(self, dx, dy, kw, split):
+        """The element leaves: the lift blocks, V_e, the updates U_e (returned), and the forward operators -- split
+        (A_uu^-1, S_v^-1, D1, D2 blobs) or Xi; None when the split leaves' probe exceeds SPLIT_ETA."""
         t, dev = self.tree, self.device
         Ks, Gs, w = _gll_tables(self.P)
         E = self.nex * self.ney
         ni, nb, ne = t.ne - t.nb, t.nb, t.ne
         z = dict(dtype=torch.float64, device=dev)
-        self._leafF = torch.empty((E, ni, ni), **z)          # Xi
-        self._leafAc = torch.empty((E, nb, self.P - 1), **z)  # A_bi on its sparsity pattern (tree.bpat)
+        n = (self.P - 1) ** 2
+        self.split = split
+        if split:
+            self.split_eta = None
+        self._leafB = self._leafF = self._leafAc = self._leafV = self._lift = None
+        if self.split:
+            ld = n + (n & 1)
+            self._leafB = torch.zeros((E, 2 * n * ld + 2 * ld + (self.P - 1) * nb), **z)
+            perm = t.split_perm()
+            pu, pv = (torch.as_tensor(a, device=dev) for a in (perm[:n], perm[n:]))
+        else:
+            self._leafF = torch.empty((E, ni, ni), **z)          # Xi
+            self._leafAc = torch.empty((E, nb, self.P - 1), **z)  # A_bi on its sparsity pattern (tree.bpat)
         bpat = torch.as_tensor(t.bpat, device=dev)
         self._leafV = torch.empty((E, ni, nb), **z)          # Xi A_ib
         U_leaf = torch.empty((E, nb, nb), **z)
@@ -310,23 +352,70 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 A[:, :, ni:].masked_fill_(dcol[:, None, :], 0.0)        # D columns: lifted, out of the elimination
                 Aii, Aib = A[:, :ni, :ni], A[:, :ni, ni:]
                 Abi, Abb = A[:, ni:, :ni], A[:, ni:, ni:]
-                Xi = batched_inverse(Aii.contiguous())
-                V = Xi @ Aib
-                self._leafF[e0:e1] = Xi
                 Ac = torch.gather(Abi, 2, bpat[None].expand(e1 - e0, -1, -1))
                 rest = Abi.clone().scatter_(2, bpat[None].expand(e1 - e0, -1, -1), 0.0)
                 if bool(rest.abs().max() != 0):
                     raise AssertionError("nested dissection: A_bi has entries outside its line / column pattern")
-                self._leafAc[e0:e1] = Ac
+                if self.split:
+                    V, eta = self._split_leaves(self._leafB[e0:e1], Aii, Aib, Ac, pu, pv)
+                    self.split_eta = max(eta, self.split_eta or 0.0)
+                    if eta > self.SPLIT_ETA:
+                        return None
+                else:
+                    Xi = batched_inverse(Aii.contiguous())
+                    V = Xi @ Aib
+                    self._leafF[e0:e1] = Xi
+                    self._leafAc[e0:e1] = Ac
+                    del Xi
                 self._leafV[e0:e1] = V
                 U_leaf[e0:e1] = Abb - Abi @ V
-                del A, Xi, V
-        kind, rid = t.root
-        self._root_update = U_leaf[rid].clone() if kind == "e" else None   # a strip's Schur complement on its lines
-        self._factor_fronts(U_leaf)
-        del U_leaf
-        self._build_steps()
-        self.factored = True
+                del A, V
+        return U_leaf
+
+    def _blob_views(self, B):
+        """(A_uu^-1, S_v^-1, D1, D2, coef^T) views of split-leaf blobs B (q, L) (include/sem_ops.h sem_leaf_forward)."""
+        n = (self.P - 1) ** 2
+        ld, nb, q = n + (n & 1), self.tree.nb, B.shape[0]
+        o = 2 * n * ld
+        return (B[:, :n * ld].view(q, n, ld)[:, :, :n], B[:, n * ld:o].view(q, n, ld)[:, :, :n], B[:, o:o + n],
+                B[:, o + ld:o + ld + n], B[:, o + 2 * ld:].view(q, self.P - 1, nb))
+
+    def _split_leaves(self, B, Aii, Aib, Ac, pu, pv):
+        """Split leaves of one chunk: A_ii = [A_uu D1; D2 A_vv] in [u; v] order (the components couple only through
+        the diagonal Newton terms juv, jvu), A_uu^-1 and S_v^-1 = (A_vv - D2 A_uu^-1 D1)^-1 into the blobs B,
+        and V_e = A_ii^-1 A_ib by the same block elimination (returned, element-local row order)."""
+        Auu, Auv = Aii[:, pu][:, :, pu], Aii[:, pu][:, :, pv]
+        Avu, Avv = Aii[:, pv][:, :, pu], Aii[:, pv][:, :, pv]
+        d1, d2 = torch.diagonal(Auv, dim1=1, dim2=2), torch.diagonal(Avu, dim1=1, dim2=2)
+        if bool((Auv - torch.diag_embed(d1)).abs().max() != 0) or bool((Avu - torch.diag_embed(d2)).abs().max() != 0):
+            raise AssertionError("nested dissection: the components couple off the diagonal inside an element")
+        Au = batched_inverse(Auu.contiguous())
+        Sv = batched_inverse((Avv - d2[:, :, None] * Au * d1[:, None, :]).contiguous())
+        Aub, Avb = Aib[:, pu], Aib[:, pv]
+        Xv = Sv @ (Avb - d2[:, :, None] * (Au @ Aub))
+        V = torch.empty_like(Aib)
+        V[:, pv] = Xv
+        V[:, pu] = Au @ (Aub - d1[:, :, None] * Xv)
+        bAu, bSv, bd1, bd2, bc = self._blob_views(B)
+        bAu.copy_(Au)
+        bSv.copy_(Sv)
+        bd1.copy_(d1)
+        bd2.copy_(d2)
+        bc.copy_(Ac.transpose(1, 2))
+        # probe: the split forward solve of a fixed random right-hand side, backward error per element
+        g = torch.Generator(device=Aii.device).manual_seed(7)
+        b = torch.rand(Aii.shape[:2], dtype=Aii.dtype, device=Aii.device, generator=g) * 2 - 1
+        tt = (Au @ b[:, pu, None])[..., 0]
+        yv = (Sv @ (b[:, pv] - d2 * tt)[..., None])[..., 0]
+        y = torch.empty_like(b)
+        y[:, pv] = yv
+        y[:, pu] = tt - (Au @ (d1 * yv)[..., None])[..., 0]
+        r = (Aii @ y[..., None])[..., 0] - b
+        eta = r.abs().amax(1) / (Aii.abs().sum(2).amax(1) * y.abs().amax(1) + b.abs().amax(1))
+        return V, float(eta.max())
+
+    def bytes_per_solve(self):
+        return self.tree.bytes_per_solve(self.split)
 
     def _factor_fronts(self, U_leaf):
         """Fronts by depth (deepest first), batched per (|S|, |B|) shape group."""
@@ -422,19 +511,31 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 src.append(q * ne + np.nonzero(keep)[0])
             steps.append(("fwd", items, self._scatter_plan(np.zeros(0, np.int64), np.zeros(0, np.int64),
                                                            np.concatenate(tgt), np.concatenate(src)), None))
-        # leaves forward: y_i = Xi b_i into stage[e ne + (0 .. ni)], the sparse A_bi y_i into stage[e ne + (ni .. ne)]
+        # leaves forward: y_i = A_ii^-1 b_i and the sparse A_bi y_i into stage[e ne + (ni .. ne)]; split: one
+        # sem_leaf_forward (y_i straight to W), else Xi b_i into stage[e ne + (0 .. ni)] and sem_front_sparse_rows
         E = self.nex * self.ney
         items, ct, cs, bt, bs = [], [], [], [], []
         for e in range(E):
-            items.append((self._leafF, e, t.eflat[e, :ni], e * ne))
-            ct.append(t.eflat[e, :ni])
-            cs.append(e * ne + np.arange(ni))
+            if not self.split:
+                items.append((self._leafF, e, t.eflat[e, :ni], e * ne))
+                ct.append(t.eflat[e, :ni])
+                cs.append(e * ne + np.arange(ni))
             keep = ~t.eD[e, ni:]
             bt.append(t.eflat[e, ni:][keep])
             bs.append(e * ne + ni + np.nonzero(keep)[0])
-        steps.append(("fwd", items, self._scatter_plan(np.concatenate(ct), np.concatenate(cs), np.concatenate(bt),
-                                                       np.concatenate(bs)),
-                      dict(coef=self._leafAc, pat=t.bpat, stride=ne, out_off=ni, nitems=E)))
+        none = np.zeros(0, np.int64)
+        if self.split:
+            n = (self.P - 1) ** 2
+            perm = t.split_perm()
+            inv = np.empty_like(perm)
+            inv[perm] = np.arange(len(perm))
+            steps.append(("leaf", dict(iidx=t.eflat[:, perm], pat=inv[t.bpat.T], n=n, nb=t.nb, nelem=E, sstride=ne,
+                                       soff=ni),
+                          self._scatter_plan(none, none, np.concatenate(bt), np.concatenate(bs)), None))
+        else:
+            steps.append(("fwd", items, self._scatter_plan(np.concatenate(ct), np.concatenate(cs),
+                                                           np.concatenate(bt), np.concatenate(bs)),
+                          dict(coef=self._leafAc, pat=t.bpat, stride=ne, out_off=ni, nitems=E)))
         levels = {}
         for fid, f in enumerate(t.fronts):
             levels.setdefault(f["depth"], []).append(fid)
@@ -469,9 +570,10 @@ class NestedDissectionSolver(VelocityJacobianSolver):
             items.append((self._leafV, e, xb, t.eflat[e, :ni]))
         steps.append(("back", items))
         self._steps = steps
-        self._nfwd = sum(1 for st in steps if st[0] == "fwd")
+        self._nfwd = sum(1 for st in steps if st[0] != "back")
         self._stage_len = max(max(max(it[3] + it[0].shape[1] for it in st[1]),
-                                  st[3]["nitems"] * st[3]["stride"] if st[3] else 0) for st in steps if st[0] == "fwd")
+                                  st[3]["nitems"] * st[3]["stride"] if st[3] else 0) if st[0] == "fwd" else
+                              st[1]["nelem"] * st[1]["sstride"] for st in steps if st[0] != "back")
         self._hip = self._hip_plan() if self.device.type == "cuda" else None
 
     @staticmethod
@@ -511,8 +613,19 @@ class NestedDissectionSolver(VelocityJacobianSolver):
         stage = Wz.new_zeros(self._stage_len)
         dev = Wz.device
         for st in self._steps[lo:hi]:
-            if st[0] == "fwd":
-                for T, q, xidx, off in st[1]:
+            if st[0] == "leaf":     # the split leaves (sem_leaf_forward), batched over the elements
+                L = st[1]
+                n = L["n"]
+                Au, Sv, d1, d2, cT = self._blob_views(self._leafB)
+                ii = torch.as_tensor(L["iidx"], device=dev)
+                tt = (Au @ Wz[ii[:, :n]][..., None])[..., 0]
+                yv = (Sv @ (Wz[ii[:, n:]] - d2 * tt)[..., None])[..., 0]
+                y = torch.cat((tt - (Au @ (d1 * yv)[..., None])[..., 0], yv), 1)
+                Wz[ii.reshape(-1)] = y.reshape(-1)
+                g = (cT * y[:, torch.as_tensor(L["pat"], device=dev)]).sum(1)
+                stage[:L["nelem"] * L["sstride"]].view(L["nelem"], -1)[:, L["soff"]:L["soff"] + L["nb"]] = g
+            if st[0] in ("fwd", "leaf"):
+                for T, q, xidx, off in (st[1] if st[0] == "fwd" else ()):
                     x = Wz[torch.as_tensor(xidx, device=dev)]
                     stage[off:off + T.shape[1]] = T[q] @ x
                 sp = st[3]
@@ -552,6 +665,9 @@ class NestedDissectionSolver(VelocityJacobianSolver):
 
         transposed = {}     # id(group tensor) -> its operators transposed (form 1)
         for st in self._steps:
+            if st[0] == "leaf":
+                plan.append(self._leaf_plan(st, nW, i32))
+                continue
             items, back = st[1], st[0] == "back"
             nf = len(items)
             Ks = np.array([it[0].shape[2] for it in items])
@@ -625,20 +741,7 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                                     keep["tiles"].data_ptr(), keep["xidx"].data_ptr(),
                                     keep["yidx"].data_ptr() if back else None, None,
                                     None if back else self._stage.data_ptr())
-            sc = None
-            if not back:
-                p = st[2]
-                for a, hi in ((p["copy_tgt"], nW), (p["acc_tgt"], nW)):
-                    if a.size and (a.min() < 0 or a.max() >= hi):
-                        raise AssertionError("nested dissection: scatter target outside the line array")
-                for a in (p["copy_src"], p["acc_src"]):
-                    if a.size and (a.min() < -1 or a.max() >= self._stage_len):
-                        raise AssertionError("nested dissection: scatter source outside the stage")
-                if len(np.unique(np.concatenate((p["copy_tgt"], p["acc_tgt"])))) != len(p["copy_tgt"]) + len(
-                        p["acc_tgt"]):
-                    raise AssertionError("nested dissection: scatter targets must be distinct")
-                sc = dict(n_copy=len(p["copy_tgt"]), ct=i32(p["copy_tgt"]), cs=i32(p["copy_src"]),
-                          n_acc=len(p["acc_tgt"]), at=i32(p["acc_tgt"]), a4=i32(p["acc_src"]).contiguous())
+            sc = None if back else self._scatter_tables(st[2], nW, i32)
             sp = None
             if not back and st[3] is not None:
                 q = st[3]
@@ -653,6 +756,56 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                           pat=i32(pat.T), stride=q["stride"], out_off=q["out_off"])
             plan.append((d, keep, sc, sp))
         return plan
+
+    def _scatter_tables(self, p, nW, i32):
+        for a, hi in ((p["copy_tgt"], nW), (p["acc_tgt"], nW)):
+            if a.size and (a.min() < 0 or a.max() >= hi):
+                raise AssertionError("nested dissection: scatter target outside the line array")
+        for a in (p["copy_src"], p["acc_src"]):
+            if a.size and (a.min() < -1 or a.max() >= self._stage_len):
+                raise AssertionError("nested dissection: scatter source outside the stage")
+        if len(np.unique(np.concatenate((p["copy_tgt"], p["acc_tgt"])))) != len(p["copy_tgt"]) + len(p["acc_tgt"]):
+            raise AssertionError("nested dissection: scatter targets must be distinct")
+        return dict(n_copy=len(p["copy_tgt"]), ct=i32(p["copy_tgt"]), cs=i32(p["copy_src"]), n_acc=len(p["acc_tgt"]),
+                    at=i32(p["acc_tgt"]), a4=i32(p["acc_src"]).contiguous())
+
+    def _leaf_plan(self, st, nW, i32):
+        """The split leaves' sem_leaf_forward descriptor, its tables checked on the host: interior targets distinct
+        line entries, boundary patterns inside [y_u; y_v], the boundary rows inside the stage."""
+        from .. import _lib
+        L, B = st[1], self._leafB
+        n, nb, E = L["n"], L["nb"], L["nelem"]
+        ld = n + (n & 1)
+        iidx, pat = np.asarray(L["iidx"]), np.asarray(L["pat"])
+        if (iidx.shape != (E, 2 * n) or iidx.min() < 0 or iidx.max() >= nW or len(np.unique(iidx)) != iidx.size
+                or pat.shape != (self.P - 1, nb) or pat.min() < 0 or pat.max() >= 2 * n
+                or E * L["sstride"] > self._stage_len or L["soff"] + nb > L["sstride"] or not 1 <= n <= 121
+                or B.shape != (E, 2 * n * ld + 2 * ld + (self.P - 1) * nb) or not B.is_contiguous()
+                or B.data_ptr() % 16 or B.shape[1] % 2 or B.device != self.device):
+            raise AssertionError("nested dissection: bad split-leaf step")
+        keep = dict(iidx=i32(iidx), pat=i32(pat))
+        d = _lib.SemLeafLaunch(E, n, ld, nb, self.P - 1, B.shape[1], B.data_ptr(), keep["iidx"].data_ptr(),
+                               keep["pat"].data_ptr(), None, self._stage.data_ptr(), L["sstride"], L["soff"])
+        return d, keep, self._scatter_tables(st[2], nW, i32), None
+
+    def _launch(self, lib, entry, Wz, st):
+        """One planned step on stream st: its gemv (or split-leaf) launch, sparse rows, scatter."""
+        import ctypes as C
+        from .. import _lib
+        d, _, sc, sp = entry
+        d.W = Wz.data_ptr()
+        if isinstance(d, _lib.SemLeafLaunch):
+            _lib.check(lib.sem_leaf_forward(C.byref(d), st))
+        else:
+            _lib.check(lib.sem_front_gemv(C.byref(d), st))
+        if sp is not None:
+            _lib.check(lib.sem_front_sparse_rows(sp["nitems"], sp["nrows"], sp["nnz"], sp["coef"].data_ptr(),
+                                                 sp["pat"].data_ptr(), self._stage.data_ptr(), sp["stride"],
+                                                 sp["out_off"], st))
+        if sc is not None:
+            _lib.check(lib.sem_front_scatter(sc["n_copy"], sc["ct"].data_ptr(), sc["cs"].data_ptr(), sc["n_acc"],
+                                             sc["at"].data_ptr(), sc["a4"].data_ptr(), self._stage.data_ptr(),
+                                             Wz.data_ptr(), st))
 
     def _launch_form(self, back, nf, K, leaves):
         """sem_front_gemv's form for one launch (`forms` = "auto", or "rows" for every launch in form 0): 1 (columns:
@@ -684,17 +837,8 @@ class NestedDissectionSolver(VelocityJacobianSolver):
         from .. import _lib
         lib = _lib.load()
         st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        for d, _, sc, sp in self._hip[lo:hi]:
-            d.W = Wz.data_ptr()
-            _lib.check(lib.sem_front_gemv(C.byref(d), st))
-            if sp is not None:
-                _lib.check(lib.sem_front_sparse_rows(sp["nitems"], sp["nrows"], sp["nnz"], sp["coef"].data_ptr(),
-                                                     sp["pat"].data_ptr(), self._stage.data_ptr(), sp["stride"],
-                                                     sp["out_off"], st))
-            if sc is not None:
-                _lib.check(lib.sem_front_scatter(sc["n_copy"], sc["ct"].data_ptr(), sc["cs"].data_ptr(), sc["n_acc"],
-                                                 sc["at"].data_ptr(), sc["a4"].data_ptr(), self._stage.data_ptr(),
-                                                 Wz.data_ptr(), st))
+        for entry in self._hip[lo:hi]:
+            self._launch(lib, entry, Wz, st)
 
 
 class StripNDSolver(_StripReduced, NestedDissectionSolver):

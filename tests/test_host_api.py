@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(_lib.exported_symbols()) == declared
-    assert lib.sem_abi_version() == _lib.ABI_VERSION == 14
+    assert lib.sem_abi_version() == _lib.ABI_VERSION == 15
     assert lib.sem_max_order() == 16
 
 

@@ -73,6 +73,34 @@ def test_nd_solve_matches_sparse_lu(P, nex, ney, Re):
     assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
 
 
+@pytest.mark.parametrize("P,nex,ney,Re,smooth,split", [
+    (4, 3, 2, 100.0, 0.3, True), (8, 2, 3, 1000.0, 0.3, True), (10, 2, 2, 1000.0, 0.3, True),
+    (12, 2, 2, 1000.0, 0.3, True), (5, 3, 7, 150.0, 0.0, False), (12, 2, 3, 200.0, 0.0, False)])
+def test_nd_split_leaves(P, nex, ney, Re, smooth, split):
+    """The split leaves (A_uu^-1, S_v^-1 and the diagonal Newton couplings instead of A_ii^-1: half the leaf bytes)
+    are taken on smooth velocity fields and refused, by the factor's per-element probe, where the coupling rivals
+    the stiffness (random fields); either way the solve is SciPy's.  The split V_e and the forward step agree with
+    the dense elimination."""
+    ns, u, v = oracle_velocity_jacobian(P, nex, ney, Re, seed=P * 10 + nex, smooth=smooth)
+    vs = NestedDissectionSolver(P, nex, ney, "cpu")
+    vs.factor_coeffs(1.0 / nex, 1.0 / ney, **_kw(ns, u, v, Re))
+    assert vs.split == split and (vs._leafB is not None) == split and (vs._leafF is None) == split
+    assert vs.split_eta is not None and (vs.split_eta <= vs.SPLIT_ETA) == split
+    assert sum(st[0] == "leaf" for st in vs._steps) == int(split)
+    r = np.random.default_rng(5)
+    bu, bv = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
+    xu, xv = vs.solve(torch.as_tensor(bu), torch.as_tensor(bv))
+    want = spla.spsolve(ns.Jvelo.tocsc(), np.hstack((bu, bv)))
+    got = np.hstack((xu.numpy(), xv.numpy()))
+    assert np.abs(got - want).max() <= 1e-10 * np.abs(want).max()
+    n = (P - 1) ** 2
+    ld = n + (n & 1)
+    leaf = (2 * n * ld + 2 * ld) if split else 4 * n * n
+    t = vs.tree
+    assert vs.bytes_per_solve() - t.bytes_per_solve(not split) == 8 * nex * ney * (leaf - ((4 * n * n) if split else
+                                                                                          2 * n * ld + 2 * ld))
+
+
 def test_nd_refuses_other_dirichlet_sets():
     vs = NestedDissectionSolver(3, 2, 2, "cpu")
     with pytest.raises(ValueError):

@@ -66,13 +66,18 @@ def assemble(pieces, P, nex, ney, ncomp=2):
     return J
 
 
-def oracle_velocity_jacobian(P, nex, ney, Re, seed, Lx=1.0, Ly=1.0):
+def oracle_velocity_jacobian(P, nex, ney, Re, seed, Lx=1.0, Ly=1.0, smooth=0.0):
     """Dirichlet-row-replaced velocity Jacobian of the oracle NS at random (u, v)
-    (NavierStokes_Solver.py:123-136,176-183) and the oracle itself."""
+    (NavierStokes_Solver.py:123-136,176-183) and the oracle itself.  smooth > 0: a smooth cell-like field of that
+    amplitude plus 1 % noise instead (the Newton coupling then small beside the stiffness, as in a real flow)."""
     from oracle import sem_oracle as O
     ns = O.NSOracle(Lx, Ly, Re, 0.0, P, nex, ney, u_N=1.0)
     r = np.random.default_rng(seed)
     u, v = r.uniform(-1, 1, ns.N), r.uniform(-1, 1, ns.N)
+    if smooth:
+        x, y = (np.asarray(a) for a in ns.points)
+        u = smooth * (np.sin(np.pi * x / Lx) * np.sin(2 * np.pi * y / Ly) + 0.01 * u)
+        v = -smooth * (np.sin(2 * np.pi * x / Lx) * np.sin(np.pi * y / Ly) + 0.01 * v)
     ns.residuals(u, v, np.zeros(ns.N), np.zeros(ns.N))
     ns.calc_jacobians(u, v)
     ns.velocity_lu()

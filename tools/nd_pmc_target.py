@@ -41,7 +41,11 @@ def main():
     torch.cuda.synchronize(dev)
     if args.plan:
         steps = []
+        from sem_amd import _lib
         for k, (d, keep, sc, sp) in enumerate(vs._hip):
+            if isinstance(d, _lib.SemLeafLaunch):
+                steps.append({"step": k, "leaf": "split", "grid": d.nelem * 256, "op_bytes": vs._leafB.numel() * 8})
+                continue
             dims = keep["dims"].cpu().numpy()
             steps.append({"step": k, "back": d.back, "form": d.form, "grid": d.ntiles * 256,
                           "op_bytes": int((dims[:, 0].astype(np.int64) * dims[:, 1]).sum() * 8),

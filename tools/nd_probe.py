@@ -79,12 +79,13 @@ def main():
     cap = nd.capture()
     torch.cuda.synchronize(dev)
     out["nd"] = {"tree_s": t_tree, "factor_s": t_f, "phases": nd.timing, "resident_GB": (torch.cuda.memory_allocated(dev)
-                 - m0) / 1e9, "bytes_per_solve": nd.tree.bytes_per_solve(), "eta": eta, "refine": nd.refine,
-                 "graph": cap, "fronts": len(nd.tree.fronts), "depth": nd.tree.depth, "launches": len(nd._hip)}
+                 - m0) / 1e9, "bytes_per_solve": nd.bytes_per_solve(), "eta": eta, "refine": nd.refine,
+                 "graph": cap, "fronts": len(nd.tree.fronts), "depth": nd.tree.depth, "launches": len(nd._hip),
+                 "split": nd.split, "split_eta": nd.split_eta}
     ts, xu, xv = timed(nd)
     med = float(np.median(ts))
     out["nd"].update({"solve_ms_median": med, "solve_ms_min": float(min(ts)), "rel_residual": relres(xu, xv),
-                      "frac_8TBs": nd.tree.bytes_per_solve() / (med * 1e-3) / 8e12})
+                      "frac_8TBs": nd.bytes_per_solve() / (med * 1e-3) / 8e12})
     # bitwise: graph replay against the eager solve
     xe = nd._solve_lines(torch.stack((bu.view(nd.NX, -1), bv.view(nd.NX, -1)), 1).reshape(nd.NX, -1))
     out["nd"]["graph_equals_eager"] = bool(torch.equal(xe.view(nd.NX, 2, -1)[:, 0].reshape(-1), xu)
@@ -110,26 +111,22 @@ def main():
         per = []
         for rep in range(3):
             rows = []
-            for d, keep, sc, sp in nd._hip:
+            for entry in nd._hip:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                d.W = W.data_ptr()
                 a.record()
-                _lib.check(lib.sem_front_gemv(C.byref(d), st))
-                if sp is not None:
-                    _lib.check(lib.sem_front_sparse_rows(sp["nitems"], sp["nrows"], sp["nnz"], sp["coef"].data_ptr(),
-                                                         sp["pat"].data_ptr(), nd._stage.data_ptr(), sp["stride"],
-                                                         sp["out_off"], st))
-                if sc is not None:
-                    _lib.check(lib.sem_front_scatter(sc["n_copy"], sc["ct"].data_ptr(), sc["cs"].data_ptr(),
-                                                     sc["n_acc"], sc["at"].data_ptr(), sc["a4"].data_ptr(),
-                                                     nd._stage.data_ptr(), W.data_ptr(), st))
+                nd._launch(lib, entry, W, st)
                 b.record()
-                rows.append((a, b, d))
+                rows.append((a, b, entry[0]))
             torch.cuda.synchronize(dev)
             per.append([a.elapsed_time(b) * 1e3 for a, b, _ in rows])
         us = np.median(np.array(per), axis=0)
         steps = []
         for k, (d, keep, sc, sp) in enumerate(nd._hip):
+            if isinstance(d, _lib.SemLeafLaunch):     # the split leaves: one workgroup per element
+                byts = nd._leafB.numel() * 8
+                steps.append({"step": k, "back": 0, "leaf": "split", "fronts": d.nelem, "tiles": d.nelem,
+                              "us": float(us[k]), "op_MB": byts / 1e6, "TBs": byts / (us[k] * 1e-6) / 1e12})
+                continue
             dims = keep["dims"].cpu().numpy()
             byts = int((dims[:, 0].astype(np.int64) * dims[:, 1]).sum() * 8) + (sp["coef"].numel() * 8 if sp else 0)
             steps.append({"step": k, "back": d.back, "fronts": int(dims.shape[0]), "tiles": d.ntiles, "rows": d.rows,

@@ -263,7 +263,7 @@ def graph_parts(vs, dev, reps):
     g = torch.rand((n + 1, m), dtype=torch.float64, device=dev)
     out = {"solve_lines": graph_ms(lambda: vs._solve_lines(B), dev, reps)}
     if getattr(vs, "interior", "") == "nd":      # nested-dissection strip: its operator bytes per solve
-        out["strip_nd_GB"] = vs.tree.bytes_per_solve() / 1e9
+        out["strip_nd_GB"] = vs.bytes_per_solve() / 1e9
     else:
         out["iface_solve"] = graph_ms(lambda: vs._iface_solve(g.clone()), dev, reps)
     if getattr(vs, "_T", None) is not None:
