@@ -13,6 +13,8 @@
 // sem_front_scatter: the forward step's deterministic write-back -- copy targets W[t] = stage[s] (a front's own
 // separator / a leaf's interior) and accumulation targets W[t] -= stage[s_0] .. stage[s_3] (the <= 4 fronts of a
 // level that update a node of an ancestor separator), summed in the order the host sorted them.
+// sem_leaf_forward (ABI 15): the split element leaves' forward step -- y_i = A_ii^-1 b_i from A_uu^-1 and
+// S_v^-1 (the components couple through diagonal Newton terms only), straight into W, and A_bi y_i to the stage.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -37,48 +39,26 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
   extern __shared__ double xs[];
   const int f = a.tiles[2 * blockIdx.x], r0 = a.tiles[2 * blockIdx.x + 1];
   const int R = a.dims[4 * f], K = a.dims[4 * f + 1], ld = a.dims[4 * f + 2];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool live = r0 + wave * G * RW < R;  // a wave wholly beyond the front only helps gather
-  const int g = lane / LPR, sl = lane % LPR;
-  const int rb = r0 + (wave * G + g) * RW;
-  const double* A = reinterpret_cast<const double*>(a.op[f]);
-  const double* rows[RW];
-#pragma unroll
-  for (int i = 0; i < RW; ++i) rows[i] = A + static_cast<int64_t>(min(rb + i, R - 1)) * ld;  // clamped: not stored
-  const int KP = K >> 1;  // K is even (the host checks): column pairs
-  int u = sl;
-  // the first batch of operator loads is in flight while the operands are gathered into LDS
-  const bool pre = live && u + LPR * (U - 1) < KP;
-  double2 a0[U][RW];
-  if (pre) {
-#pragma unroll
-    for (int t = 0; t < U; ++t)
-#pragma unroll
-      for (int i = 0; i < RW; ++i) a0[t][i] = load_nt2(rows[i] + 2 * (u + LPR * t));
-  }
   const int32_t* xi = a.xidx + a.xoff[f];
   for (int k = threadIdx.x; k < K; k += 256) {
     const int p = xi[k];
     xs[k] = p >= 0 ? a.W[p] : 0.0;
   }
   __syncthreads();
-  if (!live) return;  // groups inside a wave stay together for the reductions below
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (r0 + wave * G * RW >= R) return;  // the whole wave beyond the front (groups inside a wave stay together)
+  const int g = lane / LPR, sl = lane % LPR;
+  const int rb = r0 + (wave * G + g) * RW;
+  const double* A = reinterpret_cast<const double*>(a.op[f]);
+  const double* rows[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) rows[i] = A + static_cast<int64_t>(min(rb + i, R - 1)) * ld;  // clamped: not stored
   double acc[RW][2];
 #pragma unroll
   for (int i = 0; i < RW; ++i) acc[i][0] = acc[i][1] = 0.0;
+  const int KP = K >> 1;  // K is even (the host checks): column pairs
   const double2* x2 = reinterpret_cast<const double2*>(xs);
-  if (pre) {
-#pragma unroll
-    for (int t = 0; t < U; ++t) {
-      const double2 xv = x2[u + LPR * t];
-#pragma unroll
-      for (int i = 0; i < RW; ++i) {
-        acc[i][0] = fma(a0[t][i].x, xv.x, acc[i][0]);
-        acc[i][1] = fma(a0[t][i].y, xv.y, acc[i][1]);
-      }
-    }
-    u += LPR * U;
-  }
+  int u = sl;
   for (; u + LPR * (U - 1) < KP; u += LPR * U) {
     double2 av[U][RW], xv[U];
 #pragma unroll
@@ -149,31 +129,17 @@ __global__ __launch_bounds__(256) void front_gemv_cols_kernel(const sem_front_la
   extern __shared__ double xs[];
   const int f = a.tiles[2 * blockIdx.x], r0 = a.tiles[2 * blockIdx.x + 1];
   const int R = a.dims[4 * f], K = a.dims[4 * f + 1], ld = a.dims[4 * f + 2];
-  const int r = r0 + static_cast<int>(threadIdx.x);
-  const double* A = reinterpret_cast<const double*>(a.op[f]) + r;
-  const bool pre = r < R && UK <= K;  // the first UK loads in flight while the operands are gathered
-  double a0[UK];
-  if (pre) {
-#pragma unroll
-    for (int u = 0; u < UK; ++u) a0[u] = __builtin_nontemporal_load(A + static_cast<int64_t>(u) * ld);
-  }
   const int32_t* xi = a.xidx + a.xoff[f];
   for (int k = threadIdx.x; k < K; k += 256) {
     const int p = xi[k];
     xs[k] = p >= 0 ? a.W[p] : 0.0;
   }
   __syncthreads();
+  const int r = r0 + static_cast<int>(threadIdx.x);
   if (r >= R) return;
+  const double* A = reinterpret_cast<const double*>(a.op[f]) + r;
   double acc0 = 0.0, acc1 = 0.0;
   int k = 0;
-  if (pre) {
-#pragma unroll
-    for (int u = 0; u < UK; u += 2) {
-      acc0 = fma(a0[u], xs[u], acc0);
-      if (u + 1 < UK) acc1 = fma(a0[u + 1], xs[u + 1], acc1);
-    }
-    k = UK;
-  }
   for (; k + UK <= K; k += UK) {
     double av[UK];
 #pragma unroll
@@ -266,8 +232,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void l
   const double* d2 = d1 + ld;
   const double* coef = d2 + ld;
   const int tid = threadIdx.x, s = tid & 7, rs = tid >> 3;   // rs = w 8 + l / 8
-  double2 fa[RK][2 * RK];
-  leaf_load<RK, 2 * RK>(fa, Au, n, ld, rs, s);                      // in flight while the operands are gathered
+  double2 fa[RK][2 * RK], fs[KH][2 * RK];
+  leaf_load<RK, 2 * RK>(fa, Au, n, ld, rs, s);             // in flight while the operands are gathered ...
+  leaf_load<KH, 2 * RK>(fs, Sv, n, ld, rs, s);             // ... and S_v^-1's first batch with them
   const int32_t* ix = a.iidx + static_cast<int64_t>(e) * 2 * n;
   for (int k = tid; k < NX; k += 256) {
     bu[k] = k < n ? a.W[ix[k]] : 0.0;
@@ -285,9 +252,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void l
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < RK; h += KH) {                       // y_v = S_v^-1 (b_v - D2 t), KH rows of tiles at a time
-    double2 fs[KH][2 * RK];
     double ah[KH];
-    leaf_load<KH, 2 * RK>(fs, Sv, n, ld, rs + 32 * h, s);
+    if (h) leaf_load<KH, 2 * RK>(fs, Sv, n, ld, rs + 32 * h, s);
     leaf_rows<KH, 2 * RK>(fs, bv, s, ah);
 #pragma unroll
     for (int k = 0; k < KH; ++k) acc[h + k] = ah[k];
