@@ -33,6 +33,7 @@ keeps the line condensation.  The algebra runs on any torch device: the CPU path
 same tables) is what the CPU tests check against SciPy's sparse solve.
 """
 import functools
+import math
 import os
 
 import numpy as np
@@ -357,10 +358,14 @@ class NestedDissectionSolver(VelocityJacobianSolver):
                 if bool(rest.abs().max() != 0):
                     raise AssertionError("nested dissection: A_bi has entries outside its line / column pattern")
                 if self.split:
-                    V, eta = self._split_leaves(self._leafB[e0:e1], Aii, Aib, Ac, pu, pv)
-                    self.split_eta = max(eta, self.split_eta or 0.0)
-                    if eta > self.SPLIT_ETA:
+                    try:
+                        V, eta = self._split_leaves(self._leafB[e0:e1], Aii, Aib, Ac, pu, pv)
+                    except RuntimeError:        # A_uu or S_v singular (batched_inverse gives up): refused
+                        eta = float("inf")
+                    if not math.isfinite(eta) or eta > self.SPLIT_ETA:
+                        self.split_eta = eta if math.isfinite(eta) else float("inf")
                         return None
+                    self.split_eta = max(eta, self.split_eta or 0.0)
                 else:
                     Xi = batched_inverse(Aii.contiguous())
                     V = Xi @ Aib

@@ -101,6 +101,24 @@ def test_nd_split_leaves(P, nex, ney, Re, smooth, split):
                                                                                           2 * n * ld + 2 * ld))
 
 
+def test_nd_split_refused_when_a_component_block_is_singular():
+    """A_uu singular while A_ii is not (the components coupled only through juv = jvu = 1: J swaps u and v off the
+    Dirichlet rows): the split leaves' inverse fails, the factor takes Xi instead, and the solve is exact."""
+    P, nex, ney = 3, 3, 2
+    vs = NestedDissectionSolver(P, nex, ney, "cpu")
+    N = vs.NX * (ney * P + 1)
+    one = torch.ones(N, dtype=torch.float64)
+    vs.factor_coeffs(1.0 / nex, 1.0 / ney, juv=one, jvu=one)
+    assert not vs.split and vs.split_eta == float("inf") and vs._leafF is not None
+    r = np.random.default_rng(2)
+    bu, bv = torch.as_tensor(r.uniform(-1, 1, N)), torch.as_tensor(r.uniform(-1, 1, N))
+    xu, xv = vs.solve(bu, bv)
+    x, y = np.divmod(np.arange(N), ney * P + 1)
+    D = (x == 0) | (x == vs.NX - 1) | (y == 0) | (y == ney * P)
+    assert torch.equal(xu[D], bu[D]) and torch.equal(xv[D], bv[D])
+    assert (xu[~D] - bv[~D]).abs().max() <= 1e-14 and (xv[~D] - bu[~D]).abs().max() <= 1e-14
+
+
 def test_nd_refuses_other_dirichlet_sets():
     vs = NestedDissectionSolver(3, 2, 2, "cpu")
     with pytest.raises(ValueError):
