@@ -437,8 +437,8 @@ class NavierStokesSolver:
             torch.cuda.empty_cache()
         interior = self._velocity_interior
         if self._use_nd():
-            # nested dissection of the element grid (solvers/nested_dissection.py): cfg5 3.9 ms per solve against
-            # the line condensation's 7.8 ms, cfg4 0.35 against 0.56 ms (profiles/r06/velocity/nd/)
+            # nested dissection of the element grid (solvers/nested_dissection.py): cfg5 3.0 ms per solve with the
+            # split leaves against the line condensation's 7.8 ms, cfg4 0.34 against 0.56 ms (profiles/r06/velocity/)
             vs = NestedDissectionSolver(self._P, self._N_ex, self._N_ey, m.device)
         else:
             vs = VelocityJacobianSolver(self._P, self._N_ex, self._N_ey, m.device,
@@ -451,7 +451,8 @@ class NavierStokesSolver:
         self._velo = vs
         if 'LU_suc' in self._iprint:
             torch.cuda.synchronize(m.device)
-            kind = "nested dissection" if vs.interior == "nd" else "device static condensation"
+            kind = ("nested dissection" + (", split leaves" if vs.split else ", A_ii^-1 leaves")
+                    if vs.interior == "nd" else "device static condensation")
             print(f'NavierStokes LU: Succeeded in {time.perf_counter()-tStart:0.2f}sec ({kind}, '
                   f'backward error {vs.refine_eta:.1e}{", refined" if vs.refine else ""})')
         return vs
