@@ -828,11 +828,13 @@ class NestedDissectionSolver(VelocityJacobianSolver):
     @classmethod
     def _launch_shape(cls, K, R):
         """Lanes per row from the launch's median row length (pairs per lane ~2-4 on short rows: 64 lanes for rows of
-        >= 192 doubles), then the wide tile unless the launch would have fewer than 2048 workgroups."""
+        >= 192 doubles), then the wide tile unless the launch would have fewer than 256 workgroups (the root levels:
+        1-2 fronts).  From 256 rather than 2048 on: cfg5 3.054-3.067 -> 3.000-3.003 ms, the top levels' launches of
+        384-1918 wide tiles 10-20 % faster; cfg4 unchanged (tools/nd_shapes_ab.py, profiles/r06/velocity/split/)."""
         kp = int(np.median(K)) // 2
         lanes = 64 if kp >= 96 else max(4, min(32, 1 << max(0, (kp // 2).bit_length() - 1)))
         wide, narrow = cls.SHAPES[lanes]
-        rows = wide if int(((R + wide - 1) // wide).sum()) >= 2048 else narrow
+        rows = wide if int(((R + wide - 1) // wide).sum()) >= 256 else narrow
         return lanes, rows
 
     def _run_hip(self, Wz, lo, hi):

@@ -129,13 +129,15 @@ def test_nd_refuses_other_dirichlet_sets():
 
 def test_launch_policy():
     """sem_front_gemv's per-launch choices: lanes per row by the median row length (64 for rows of >= 192 doubles),
-    the wide tile unless the launch is too small to fill the chip, and the column form only for forward front
+    the wide tile unless the launch would have fewer than 256 workgroups, and the column form only for forward front
     levels with rows of <= 64 doubles."""
     S = NestedDissectionSolver
     assert S._launch_shape(np.array([242] * 4), np.array([338] * 4)) == (64, 4)
     assert S._launch_shape(np.array([242] * 20000), np.array([242] * 20000)) == (64, 16)
     assert S._launch_shape(np.array([96] * 4), np.array([242] * 4)) == (16, 16)
     assert S._launch_shape(np.array([22] * 4), np.array([174] * 4)) == (4, 64)
+    assert S._launch_shape(np.array([3070] * 2), np.array([5000] * 2)) == (64, 16)   # 626 wide tiles
+    assert S._launch_shape(np.array([3070]), np.array([3070])) == (64, 4)            # the root: 192
     vs = S.__new__(S)
     assert vs._launch_form(False, 8192, np.array([22] * 8192), False) == 1
     assert vs._launch_form(True, 8192, np.array([22] * 8192), False) == 0
