@@ -75,14 +75,24 @@ __global__ __launch_bounds__(256) void front_gemv_kernel(const sem_front_launch 
         acc[i][1] = fma(av[t][i].y, xv[t].y, acc[i][1]);
       }
   }
-  for (; u < KP; u += LPR) {
-    const double2 xv = x2[u];
+  if (u < KP) {  // the last < U column pairs of this lane: one masked batch (the same sums, in the same order)
+    double2 av[U][RW], xv[U];
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {
-      const double2 av = load_nt2(rows[i] + 2 * u);
-      acc[i][0] = fma(av.x, xv.x, acc[i][0]);
-      acc[i][1] = fma(av.y, xv.y, acc[i][1]);
+    for (int t = 0; t < U; ++t) {
+      const bool in = u + LPR * t < KP;
+      xv[t] = in ? x2[u + LPR * t] : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int i = 0; i < RW; ++i) av[t][i] = in ? load_nt2(rows[i] + 2 * (u + LPR * t)) : make_double2(0.0, 0.0);
     }
+#pragma unroll
+    for (int t = 0; t < U; ++t)
+      if (u + LPR * t < KP) {
+#pragma unroll
+        for (int i = 0; i < RW; ++i) {
+          acc[i][0] = fma(av[t][i].x, xv[t].x, acc[i][0]);
+          acc[i][1] = fma(av[t][i].y, xv[t].y, acc[i][1]);
+        }
+      }
   }
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
@@ -150,9 +160,16 @@ __global__ __launch_bounds__(256) void front_gemv_cols_kernel(const sem_front_la
       if (u + 1 < UK) acc1 = fma(av[u + 1], xs[k + u + 1], acc1);
     }
   }
-  for (; k < K; ++k) {
-    const double v = __builtin_nontemporal_load(A + static_cast<int64_t>(k) * ld);
-    if (k & 1) acc1 = fma(v, xs[k], acc1); else acc0 = fma(v, xs[k], acc0);
+  if (k < K) {  // the last < UK columns: one masked batch (k is even: same parities, same order)
+    double av[UK];
+#pragma unroll
+    for (int u = 0; u < UK; ++u)
+      av[u] = k + u < K ? __builtin_nontemporal_load(A + static_cast<int64_t>(k + u) * ld) : 0.0;
+#pragma unroll
+    for (int u = 0; u < UK; u += 2) {
+      if (k + u < K) acc0 = fma(av[u], xs[k + u], acc0);
+      if (u + 1 < UK && k + u + 1 < K) acc1 = fma(av[u + 1], xs[k + u + 1], acc1);
+    }
   }
   const double v = acc0 + acc1;
   if (a.back) {
