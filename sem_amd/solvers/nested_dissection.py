@@ -814,13 +814,14 @@ class NestedDissectionSolver(VelocityJacobianSolver):
 
     def _launch_form(self, back, nf, K, leaves):
         """sem_front_gemv's form for one launch (`forms` = "auto", or "rows" for every launch in form 0): 1 (columns:
-        transposed operators, a thread per row) for the forward front levels whose rows are <= 64 doubles (the
-        deepest separators: cfg5 d13-d11 124 / 111 / 85 -> 74 / 79 / 71 us, profiles/r06/velocity/nd/), else 0 (lanes
-        per row).  A k-split form for the few long top fronts (operands in registers, four waves per row set)
-        measured slower than form 0 there (+10-25 %) and was not kept."""
+        transposed operators, a thread per row) for the forward front levels whose rows are <= 128 doubles (the
+        deepest separators: cfg5 d13-d11 124 / 111 / 85 -> 74 / 79 / 71 us, profiles/r06/velocity/nd/; d10-d9
+        83 / 63 -> 73 / 56 us, profiles/r06/velocity/split/cols_ab128.json), else 0 (lanes per row).  A k-split form
+        for the few long top fronts (operands in registers, four waves per row set) measured slower than form 0
+        there (+10-25 %) and was not kept."""
         if getattr(self, "forms", "auto") != "auto" or leaves:
             return 0
-        return 1 if not back and int(np.median(K)) <= 64 else 0
+        return 1 if not back and int(np.median(K)) <= 128 else 0
 
     # (lanes per row, rows per workgroup) of sem_front_gemv: (wide, narrow) per lane count
     SHAPES = {64: (16, 4), 32: (16, 8), 16: (32, 16), 8: (64, 32), 4: (128, 64)}

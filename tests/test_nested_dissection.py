@@ -130,7 +130,7 @@ def test_nd_refuses_other_dirichlet_sets():
 def test_launch_policy():
     """sem_front_gemv's per-launch choices: lanes per row by the median row length (64 for rows of >= 192 doubles),
     the wide tile unless the launch would have fewer than 256 workgroups, and the column form only for forward front
-    levels with rows of <= 64 doubles."""
+    levels with rows of <= 128 doubles."""
     S = NestedDissectionSolver
     assert S._launch_shape(np.array([242] * 4), np.array([338] * 4)) == (64, 4)
     assert S._launch_shape(np.array([242] * 20000), np.array([242] * 20000)) == (64, 16)
@@ -143,5 +143,7 @@ def test_launch_policy():
     assert vs._launch_form(True, 8192, np.array([22] * 8192), False) == 0
     assert vs._launch_form(False, 16384, np.array([242] * 16384), True) == 0
     assert vs._launch_form(False, 1, np.array([3070]), False) == 0
+    assert vs._launch_form(False, 1024, np.array([92] * 1024), False) == 1
+    assert vs._launch_form(False, 256, np.array([180] * 256), False) == 0
     vs.forms = "rows"
     assert vs._launch_form(False, 8192, np.array([22] * 8192), False) == 0

@@ -3,7 +3,8 @@ linearisation): for each policy the plan is rebuilt and captured, the graph-repl
 --solves, the policies alternated --rounds times) and every step timed eagerly; the solutions must agree to
 rounding.  Policies: "default" (NestedDissectionSolver._launch_shape), "wide64" (64 lanes always with 16 rows
 per workgroup), "narrow64" (64 lanes always with 4 rows), "lanes32" (rows of >= 1024 doubles on 32 lanes),
-"wide256" (the wide tile whenever it gives >= 256 workgroups).
+"wide256" (the wide tile whenever it gives >= 256 workgroups), "colsN" (the column form for forward front levels
+of median row length <= N; the default is 64).
 
 python tools/nd_shapes_ab.py [--ne 128 --P 12 --solves 30 --rounds 2 --out FILE]
 """
@@ -24,6 +25,7 @@ def main():
     ap.add_argument("--P", type=int, default=12)
     ap.add_argument("--solves", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--policies", default="default,wide64,narrow64,lanes32,wide256")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     from sem_amd.solvers import NavierStokesSolver
@@ -64,10 +66,17 @@ def main():
     lib = _lib.load()
     st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     res, ref = {}, None
-    policies = ["default", "wide64", "narrow64", "lanes32", "wide256"]
+    policies = args.policies.split(",")
+    base_form = ND._launch_form
     for _ in range(args.rounds):
         for pol in policies:
             ND._launch_shape = shape_for(pol)
+            if pol.startswith("cols"):     # the column form for forward front levels up to this median row length
+                lim = int(pol[4:])
+                ND._launch_form = lambda self, back, nf, K, leaves, lim=lim: (
+                    0 if leaves or back else int(int(np.median(K)) <= lim))
+            else:
+                ND._launch_form = base_form
             nd._hip = nd._hip_plan()
             nd.capture()
             for _ in range(3):
