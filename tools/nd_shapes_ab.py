@@ -3,7 +3,7 @@ linearisation): for each policy the plan is rebuilt and captured, the graph-repl
 --solves, the policies alternated --rounds times) and every step timed eagerly; the solutions must agree to
 rounding.  Policies: "default" (NestedDissectionSolver._launch_shape), "wide64" (64 lanes always with 16 rows
 per workgroup), "narrow64" (64 lanes always with 4 rows), "lanes32" (rows of >= 1024 doubles on 32 lanes),
-"wide256" (the wide tile whenever it gives >= 256 workgroups), "colsN" (the column form for forward front levels
+"wide256" (the wide tile whenever it gives >= 256 workgroups), "fit" (the narrow tile when the wide one pads the rows by > 15 % more), "colsN" (the column form for forward front levels
 of median row length <= N; the default is 64).
 
 python tools/nd_shapes_ab.py [--ne 128 --P 12 --solves 30 --rounds 2 --out FILE]
@@ -57,6 +57,13 @@ def main():
                 lanes, _ = base_shape(cls, K, R)
                 wide, narrow = cls.SHAPES[lanes]
                 return lanes, wide if int(((R + wide - 1) // wide).sum()) >= 256 else narrow
+            if policy == "fit":          # the narrow tile when the wide one pads the fronts' rows by > 15 % more
+                lanes, rows = base_shape(cls, K, R)
+                wide, narrow = cls.SHAPES[lanes]
+                tw, tn = int(((R + wide - 1) // wide).sum()), int(((R + narrow - 1) // narrow).sum())
+                if rows == wide and R.sum() / (tn * narrow) > 1.15 * R.sum() / (tw * wide):
+                    return lanes, narrow
+                return lanes, rows
             if policy == "lanes32" and kp >= 512:
                 wide, narrow = cls.SHAPES[32]
                 return 32, wide if int(((R + wide - 1) // wide).sum()) >= 2048 else narrow
