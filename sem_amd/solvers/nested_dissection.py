@@ -21,16 +21,22 @@ a fill-reducing order:
 * Dirichlet rows (the whole perimeter, every component: the velocity mask of NavierStokes_Solver.py:78-94) are
   identity rows: x_D = b_D.  They are taken out before the elimination -- the right-hand side is lifted,
   b_N -= A_ND b_D (the perimeter elements' coupling blocks), and D appears in no front.
-* Solve = lift, leaf forward ([Xi; A_bi Xi] b_i: y_i and the boundary update), front forward level by level
-  from the deepest, front back substitution x_S = y_S - V x_B from the root down, leaf back substitution
-  x_i = y_i - V_e x_b.  Every step is one streaming GEMV launch over all fronts of a level (sem_front_gemv)
-  plus, after a forward step, one deterministic scatter (sem_front_scatter: each target sums its <= 4
-  contributions in a fixed order), so results are bitwise reproducible and the solve is graph-capturable.
+* Split leaves (two components, P <= 12): inside an element u and v couple only through the diagonal Newton
+  terms, A_ii = [A_uu D1; D2 A_vv], so the leaf keeps A_uu^-1 and S_v^-1 = (A_vv - D2 A_uu^-1 D1)^-1 -- two
+  n x n blocks (n = (P-1)^2) instead of the (2n)^2 of Xi -- and sem_leaf_forward solves y_i = A_ii^-1 b_i with
+  A_uu^-1 held in registers across its two products.  A per-element probe of the split solve's backward error
+  falls back to Xi for the whole mesh when the coupling rivals the stiffness (SPLIT_ETA).
+* Solve = lift, leaf forward (y_i and the sparse boundary update A_bi y_i), front forward level by level from
+  the deepest, front back substitution x_S = y_S - V x_B from the root down, leaf back substitution
+  x_i = y_i - V_e x_b.  Every front step is one streaming GEMV launch over all fronts of a level
+  (sem_front_gemv) plus, after a forward step, one deterministic scatter (sem_front_scatter: each target sums
+  its <= 4 contributions in a fixed order), so results are bitwise reproducible and the solve is
+  graph-capturable.
 
-Bytes per solve (cfg5: 128^2 elements, P = 12): the leaves' [Xi; A_bi Xi] and V_e, the fronts' Fw and V --
-20 GB against the line condensation's 42.3 (model: tools/nd_model.py).  The strip partition (strip_solve.py)
-keeps the line condensation.  The algebra runs on any torch device: the CPU path (a per-front loop over the
-same tables) is what the CPU tests check against SciPy's sparse solve.
+Bytes per solve (cfg5: 128^2 elements, P = 12): the split leaves' blobs and V_e, the fronts' Fw and V -- 13.5 GB
+(17.2 with Xi leaves) against the line condensation's 42.3 (model: tools/nd_model.py).  Strips use it too
+(StripNDSolver).  The algebra runs on any torch device: the CPU path (a per-front loop over the same tables) is
+what the CPU tests check against SciPy's sparse solve.
 """
 import functools
 import math
